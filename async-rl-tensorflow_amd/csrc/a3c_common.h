@@ -1,0 +1,90 @@
+// Shared device helpers for the MI355X (gfx950) A3C rollout + gradient path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define A3C_WAVE 64
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define A3C_CHECK(expr)                                                       \
+  do {                                                                        \
+    hipError_t _e = (expr);                                                   \
+    if (_e != hipSuccess) return a3c_set_error((int)_e, #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+// Error reporting (defined in capi.cpp).
+extern "C" int a3c_set_error(int code, const char* what, const char* detail);
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. 2011) -- bit-identical to oracle/philox.py.
+// ---------------------------------------------------------------------------
+enum : uint32_t { P_ACTION = 1u, P_STEP = 3u, P_RESET = 6u, P_NOOP = 7u, P_POOL = 9u };
+
+struct u32x4 { uint32_t x, y, z, w; };
+
+__host__ __device__ inline u32x4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return {c0, c1, c2, c3};
+}
+
+// top 24 bits * 2^-24 : exact in fp32, identical to oracle philox.u01
+__host__ __device__ inline float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+
+// ---------------------------------------------------------------------------
+// wave reductions (64 lanes)
+// ---------------------------------------------------------------------------
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ inline float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ inline double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Addressing of stacked frame states.
+//
+// Frames (84x84 u8 planes) live in a per-env ring of R slots; the state s_tau of env e is
+// the L planes of frames tau-L+1 .. tau (oldest first == history.py:13-15 order, channel c
+// of the NHWC view history.py:20-22).  A contiguous [B][L][H][W] tensor is the special case
+// R = L, E = B, tau = L-1.
+// sample b -> (t = b / E, e = b % E); frame tau = (*tau_ptr) + t + tau_offset.
+// ---------------------------------------------------------------------------
+struct StateAddr {
+  const uint8_t* base;   // ring base
+  int64_t env_stride;    // bytes between envs
+  int64_t plane_bytes;   // bytes per plane (H*W)
+  int E;                 // envs per rollout step
+  int R;                 // ring slots
+  int L;                 // history length
+  int tau_offset;        // added to tau (+1 for next states)
+  const int64_t* tau_ptr;  // device counter (nullable -> 0)
+};
+
+__device__ inline const uint8_t* state_plane(const StateAddr& a, int64_t b, int c, int64_t tau0) {
+  int64_t t = b / a.E, e = b - t * a.E;
+  int64_t tau = tau0 + t + a.tau_offset - (a.L - 1) + c;
+  int64_t slot = tau % a.R;
+  if (slot < 0) slot += a.R;
+  return a.base + e * a.env_stride + slot * a.plane_bytes;
+}

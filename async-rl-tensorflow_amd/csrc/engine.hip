@@ -1,0 +1,439 @@
+// Batched actor-learner engine (one per GPU): E envs stepped in lock-step on device, n-step
+// rollout with the forward of every step, bootstrap forward, returns, loss + backward, per-tensor
+// clip, then (after the host's optional RCCL all-reduce of the clipped gradients) RMSProp apply.
+//
+// Reference loop it replaces (per worker): agent.py:52-67 train -> predict (:141-151) ->
+// env.act (environment.py:124-142) -> observe (:153-167) -> batch_update (:169-207) with the
+// shared RMSProp apply on the parameter server (main.py:60-66).  A3C (network.py + assets/a3c.png)
+// uses n-step returns instead of the TD target; algo Q keeps agent.py's target network.
+//
+// All per-iteration varying quantities (tau = frame counter, global env-step count, epsilon)
+// live in device memory, so the whole rollout+backward sequence is captured once into a hipGraph
+// and replayed (no host work per kernel).
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+#include "env.h"
+#include "net_bwd.h"
+#include "optim.h"
+#include "gemm.h"
+
+void a3c_init_once();
+
+struct a3c_engine {
+  a3c_engine_config cfg;
+  NetLayout L;
+  int E, n, R;
+  int64_t nE;
+  uint32_t k0, k1;
+  std::vector<void*> allocs;
+  float *params, *tparams, *ms, *mom, *grads;
+  uint8_t *ring, *pool;
+  int64_t* counters;  // [0] tau, [1] global step
+  EnvBufs env;
+  EnvParams envp;
+  int32_t* actions;
+  float* rewards;
+  uint8_t* terms;
+  float* z;
+  float* R_buf;
+  float* loss;
+  float* sumsq;
+  float *act_l1, *act_l2, *act_l3;
+  float *scr_l2, *scr_l3;  // bootstrap / target forward scratch
+  float* zt;               // q: target-net q values [nE][zs]
+  float* eps;              // q: per env epsilon
+  float* ep_end;           // q: per env final epsilon
+  float* ws;               // backward workspace
+  float* fslab_e; int fsplit_e;
+  float* fslab_b; int fsplit_b;
+  double* opt_part;
+  TensorTab tt;
+  hipGraph_t graph;
+  hipGraphExec_t gexec;
+  bool captured;
+  bool reset_done;
+};
+
+static int dalloc(a3c_engine* e, void** p, size_t bytes) {
+  bytes = (bytes + 255) & ~(size_t)255;
+  if (bytes == 0) bytes = 256;
+  hipError_t st = hipMalloc(p, bytes);
+  if (st != hipSuccess) return a3c_set_error((int)st, "a3c_engine_create", "hipMalloc failed");
+  e->allocs.push_back(*p);
+  return 0;
+}
+
+extern "C" void a3c_engine_config_default(a3c_engine_config* c) {
+  memset(c, 0, sizeof(*c));
+  c->net.algo = A3C_ALGO_A3C;
+  c->net.trunk = A3C_TRUNK_NIPS;
+  c->net.action_size = 6;
+  c->net.history_length = 4;
+  c->net.screen_h = 84;
+  c->net.screen_w = 84;
+  c->num_envs = 256;
+  c->n_step = 5;
+  c->env_id_base = 0;
+  c->world_size = 1;
+  c->start_lives = 0;
+  c->random_start = 30;
+  c->action_repeat = 1;
+  c->num_frames = 1024;
+  c->use_graph = 1;
+  c->seed = 123;
+  c->gamma = 0.99;
+  c->beta = 0.01f;
+  c->learning_rate = 0.0007f;
+  c->max_step = 80000000LL;
+  c->decay = 0.99f;
+  c->momentum = 0.0f;
+  c->epsilon = 0.1f;
+  c->clip_norm = 40.0f;
+  c->literal_adv = 0;
+  c->ep_start = 1.0f;
+  c->ep_end = 0.1f;
+  c->ep_end_t = 4000000LL;
+  c->learn_start = 32;
+  c->target_q_update_step = 40000LL;
+  c->discount = 0.99;
+}
+
+extern "C" int a3c_engine_destroy(a3c_engine* e) {
+  if (!e) return 0;
+  if (e->captured) {
+    (void)hipGraphExecDestroy(e->gexec);
+    (void)hipGraphDestroy(e->graph);
+  }
+  for (void* p : e->allocs) (void)hipFree(p);
+  delete e;
+  return 0;
+}
+
+extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out) {
+  if (!cfg || !out) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "null");
+  *out = nullptr;
+  a3c_engine* e = new (std::nothrow) a3c_engine();
+  if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "oom");
+  e->cfg = *cfg;
+  if (a3c_make_layout(&cfg->net, &e->L) || cfg->num_envs < 1 || cfg->n_step < 1 || cfg->n_step > 64 ||
+      cfg->num_frames < 1 || cfg->random_start < 1 || cfg->action_repeat < 1 || cfg->world_size < 1) {
+    delete e;
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "bad config");
+  }
+  a3c_init_once();
+  const NetLayout& L = e->L;
+  e->E = cfg->num_envs;
+  e->n = cfg->n_step;
+  e->R = e->n + HIST + (cfg->net.algo == A3C_ALGO_Q ? 1 : 0);
+  e->nE = (int64_t)e->n * e->E;
+  e->k0 = (uint32_t)cfg->seed;
+  e->k1 = (uint32_t)(cfg->seed >> 32);
+  const int64_t nE = e->nE, E = e->E;
+  const int zs = L.zs;
+  int rc = 0;
+#define ALLOC(ptr, bytes) do { void* _p; if ((rc = dalloc(e, &_p, (size_t)(bytes)))) { a3c_engine_destroy(e); return rc; } ptr = (decltype(ptr))_p; } while (0)
+  ALLOC(e->params, L.total * 4);
+  ALLOC(e->tparams, L.total * 4);
+  ALLOC(e->ms, L.total * 4);
+  ALLOC(e->mom, L.total * 4);
+  ALLOC(e->grads, L.total * 4);
+  ALLOC(e->ring, (int64_t)E * e->R * PLANE);
+  ALLOC(e->pool, (int64_t)cfg->num_frames * SCREEN_H * SCREEN_W * 3);
+  ALLOC(e->counters, 64);
+  ALLOC(e->env.episode, E * 4);
+  ALLOC(e->env.ep_step, E * 4);
+  ALLOC(e->env.ep_len, E * 4);
+  ALLOC(e->env.lives, E * 4);
+  ALLOC(e->env.frame, E * 4);
+  ALLOC(e->env.reward, E * 4);
+  ALLOC(e->env.terminal, E);
+  ALLOC(e->actions, nE * 4);
+  ALLOC(e->rewards, nE * 4);
+  ALLOC(e->terms, nE);
+  ALLOC(e->z, (nE + E) * zs * 4);
+  ALLOC(e->R_buf, nE * 4);
+  ALLOC(e->loss, 64);
+  ALLOC(e->sumsq, A3C_MAX_TENSORS * 4);
+  ALLOC(e->act_l1, nE * C1_P * C1_N * 4);
+  ALLOC(e->act_l2, nE * FLAT * 4);
+  ALLOC(e->act_l3, nE * FC * 4);
+  const int64_t scrB = cfg->net.algo == A3C_ALGO_Q ? nE : E;
+  ALLOC(e->scr_l2, scrB * FLAT * 4);
+  ALLOC(e->scr_l3, scrB * FC * 4);
+  ALLOC(e->zt, scrB * zs * 4);
+  ALLOC(e->eps, E * 4);
+  ALLOC(e->ep_end, E * 4);
+  BwdPlan bp = a3c_bwd_plan(L, nE);
+  ALLOC(e->ws, bp.total * 4);
+  int64_t f1 = a3c_fwd_slab_floats(E, &e->fsplit_e);
+  ALLOC(e->fslab_e, f1 * 4);
+  int64_t f2 = a3c_fwd_slab_floats(scrB, &e->fsplit_b);
+  ALLOC(e->fslab_b, f2 * 4);
+  ALLOC(e->opt_part, (int64_t)A3C_MAX_TENSORS * SS_BLOCKS * 8);
+#undef ALLOC
+  e->tt.n = L.nt;
+  for (int i = 0; i < L.nt; ++i) { e->tt.off[i] = L.off[i]; e->tt.size[i] = L.size[i]; }
+  e->envp.k0 = e->k0; e->envp.k1 = e->k1;
+  e->envp.P = cfg->num_frames;
+  e->envp.A = L.A;
+  e->envp.L0 = cfg->start_lives;
+  e->envp.random_start = cfg->random_start;
+  e->envp.action_repeat = cfg->action_repeat;
+  e->envp.env_id_base = cfg->env_id_base;
+  // per-env final epsilon (main.py:369 samples ep_end per worker from {0.1, 0.01, 0.5})
+  std::vector<float> ee(E);
+  static const float choices[3] = {0.1f, 0.01f, 0.5f};
+  for (int64_t i = 0; i < E; ++i) {
+    u32x4 x = philox4x32((uint32_t)(cfg->env_id_base + i), 0u, 0u, 11u, e->k0, e->k1);
+    ee[i] = choices[x.x % 3u];
+  }
+  if (hipMemcpy(e->ep_end, ee.data(), E * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    a3c_engine_destroy(e);
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "hipMemcpy");
+  }
+  *out = e;
+  return 0;
+}
+
+// ---- small device kernels -------------------------------------------------------------------
+__global__ void k_eps(float* __restrict__ eps, const float* __restrict__ ep_end, int E,
+                      const int64_t* __restrict__ counters, float ep_start, int64_t ep_end_t,
+                      int64_t learn_start) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E) return;
+  // agent.py:142-144
+  const double step = (double)counters[1];
+  const double ee = ep_end[i];
+  double d = (double)ep_end_t - fmax(0.0, step - (double)learn_start);
+  double v = ee + fmax(0.0, ((double)ep_start - ee) * d / (double)ep_end_t);
+  eps[i] = (float)v;
+}
+
+__global__ void k_advance(int64_t* __restrict__ counters, int64_t dtau, int64_t dstep) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    counters[0] += dtau;
+    counters[1] += dstep;
+  }
+}
+
+// target-network sync when the global step passes T with T % P == P-1 (agent.py:165-167)
+__global__ void k_maybe_copy(float* __restrict__ dst, const float* __restrict__ src, int64_t n,
+                             const int64_t* __restrict__ counters, int64_t inc, int64_t period) {
+  const int64_t g0 = counters[1];
+  if ((g0 + inc + 1) / period == (g0 + 1) / period) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+static StateAddr ring_addr(const a3c_engine* e, int tau_offset) {
+  StateAddr sa;
+  sa.base = e->ring;
+  sa.env_stride = (int64_t)e->R * PLANE;
+  sa.plane_bytes = PLANE;
+  sa.E = e->E;
+  sa.R = e->R;
+  sa.L = HIST;
+  sa.tau_offset = tau_offset;
+  sa.tau_ptr = e->counters;
+  return sa;
+}
+
+static int enqueue_rollout_grad(a3c_engine* e, hipStream_t s) {
+  const a3c_engine_config& c = e->cfg;
+  const NetLayout& L = e->L;
+  const int E = e->E, n = e->n, zs = L.zs;
+  const bool q = L.algo == A3C_ALGO_Q;
+  int rc;
+  if (q) {
+    hipLaunchKernelGGL(k_eps, dim3((E + 255) / 256), dim3(256), 0, s, e->eps, e->ep_end, E, e->counters,
+                       c.ep_start, c.ep_end_t, c.learn_start);
+    A3C_CHECK(hipGetLastError());
+  }
+  for (int t = 0; t < n; ++t) {
+    HeadSelect sel = {};
+    sel.mode = q ? 1 : 0;
+    sel.k0 = e->k0; sel.k1 = e->k1;
+    sel.tau_ptr = e->counters; sel.tau_add = t;
+    sel.env_ids = nullptr; sel.env_id_base = c.env_id_base; sel.E = E;
+    sel.eps = e->eps;
+    sel.actions = e->actions + (int64_t)t * E;
+    const int64_t o = (int64_t)t * E;
+    rc = a3c_forward_launch(L, e->params, ring_addr(e, t), E, e->act_l1 + o * C1_P * C1_N, e->act_l2 + o * FLAT,
+                            e->act_l3 + o * FC, e->z + o * zs, e->fslab_e, e->fsplit_e, sel, s);
+    if (rc) return rc;
+    rc = a3c_env_step_launch(e->envp, e->env, E, e->actions + o, e->rewards + o, e->terms + o, -1.0f, 1.0f,
+                             e->pool, e->ring, e->R, e->counters, t, s);
+    if (rc) return rc;
+  }
+  HeadSelect none = {};
+  none.mode = -1;
+  none.E = E;
+  if (!q) {
+    // bootstrap V(s_{t+n}) with the same parameters (assets/a3c.png)
+    rc = a3c_forward_launch(L, e->params, ring_addr(e, n), E, nullptr, e->scr_l2, e->scr_l3, e->z + e->nE * zs,
+                            e->fslab_e, e->fsplit_e, none, s);
+    if (rc) return rc;
+    rc = a3c_returns_launch(e->rewards, e->terms, e->z + e->nE * zs + L.A, zs, n, E, c.gamma, e->R_buf, s);
+    if (rc) return rc;
+  } else {
+    // target network on s_{t+1} for every transition (agent.py:186)
+    none.E = E;
+    rc = a3c_forward_launch(L, e->tparams, ring_addr(e, 1), e->nE, nullptr, e->scr_l2, e->scr_l3, e->zt,
+                            e->fslab_b, e->fsplit_b, none, s);
+    if (rc) return rc;
+    rc = a3c_td_target_launch(e->rewards, e->terms, e->zt, e->nE, L.A, zs, c.discount, e->R_buf, s);
+    if (rc) return rc;
+  }
+  rc = a3c_backward_launch(L, e->params, ring_addr(e, 0), e->nE, e->act_l1, e->act_l2, e->act_l3, e->z,
+                           e->actions, e->R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s);
+  if (rc) return rc;
+  // per-tensor clip of this worker's gradient (agent.py:319) -- before any cross-GPU exchange
+  OptParams op = {};
+  op.mode = OPT_CLIP;
+  op.clip = c.clip_norm;
+  return a3c_optim_launch(nullptr, nullptr, nullptr, e->grads, e->tt, op, e->opt_part, e->sumsq, true, s);
+}
+
+extern "C" int a3c_engine_reset(a3c_engine* e, const float* host_params, void* stream) {
+  if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_reset", "null");
+  hipStream_t s = (hipStream_t)stream;
+  const NetLayout& L = e->L;
+  if (host_params) {
+    A3C_CHECK(hipMemcpyAsync(e->params, host_params, L.total * 4, hipMemcpyHostToDevice, s));
+    A3C_CHECK(hipStreamSynchronize(s));
+  }
+  A3C_CHECK(hipMemcpyAsync(e->tparams, e->params, L.total * 4, hipMemcpyDeviceToDevice, s));
+  int rc = a3c_fill_launch(e->ms, L.total, 1.0f, s);   // TF1 RMSProp rms slot init = 1
+  if (rc) return rc;
+  A3C_CHECK(hipMemsetAsync(e->mom, 0, L.total * 4, s));
+  A3C_CHECK(hipMemsetAsync(e->grads, 0, L.total * 4, s));
+  A3C_CHECK(hipMemsetAsync(e->loss, 0, 64, s));
+  A3C_CHECK(hipMemsetAsync(e->ring, 0, (size_t)e->E * e->R * PLANE, s));
+  rc = a3c_pool_fill_launch(e->pool, e->cfg.num_frames, e->k0, e->k1, s);
+  if (rc) return rc;
+  rc = a3c_env_init_launch(e->envp, e->env, e->E, e->pool, e->ring, e->R, e->counters, s);
+  if (rc) return rc;
+  e->reset_done = true;
+  return 0;
+}
+
+extern "C" int a3c_engine_rollout_grad(a3c_engine* e, void* stream) {
+  if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_rollout_grad", "null");
+  if (!e->reset_done) return a3c_set_error(A3C_ERR_STATE, "a3c_engine_rollout_grad", "call a3c_engine_reset first");
+  hipStream_t s = (hipStream_t)stream;
+  if (!e->cfg.use_graph) return enqueue_rollout_grad(e, s);
+  if (!e->captured) {
+    hipStream_t cs;
+    A3C_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    A3C_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue_rollout_grad(e, cs);
+    hipGraph_t g;
+    hipError_t st = hipStreamEndCapture(cs, &g);
+    (void)hipStreamDestroy(cs);
+    if (rc) return rc;
+    if (st != hipSuccess) return a3c_set_error((int)st, "a3c_engine_rollout_grad", "capture failed");
+    st = hipGraphInstantiate(&e->gexec, g, nullptr, nullptr, 0);
+    if (st != hipSuccess) {
+      (void)hipGraphDestroy(g);
+      return a3c_set_error((int)st, "a3c_engine_rollout_grad", "instantiate failed");
+    }
+    e->graph = g;
+    e->captured = true;
+  }
+  A3C_CHECK(hipGraphLaunch(e->gexec, s));
+  return 0;
+}
+
+extern "C" int a3c_engine_apply(a3c_engine* e, void* stream) {
+  if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_apply", "null");
+  hipStream_t s = (hipStream_t)stream;
+  const a3c_engine_config& c = e->cfg;
+  const int64_t inc = e->nE * c.world_size;
+  OptParams op = {};
+  op.mode = OPT_APPLY;
+  op.clip = 0.f;
+  op.step_ptr = e->counters + 1;
+  op.step_add = inc;
+  op.lr0 = c.learning_rate;
+  op.max_step = c.max_step;
+  op.rho = c.decay;
+  op.momentum = c.momentum;
+  op.eps = c.epsilon;
+  int rc = a3c_optim_launch(e->params, e->ms, e->mom, e->grads, e->tt, op, e->opt_part, nullptr, false, s);
+  if (rc) return rc;
+  if (e->L.algo == A3C_ALGO_Q) {
+    hipLaunchKernelGGL(k_maybe_copy, dim3(256), dim3(256), 0, s, e->tparams, e->params, e->L.total, e->counters,
+                       inc, c.target_q_update_step);
+    A3C_CHECK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, s, e->counters, (int64_t)e->n, inc);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int a3c_engine_get_buffers(a3c_engine* e, a3c_engine_buffers* b) {
+  if (!e || !b) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_get_buffers", "null");
+  memset(b, 0, sizeof(*b));
+  b->params = e->params; b->target_params = e->tparams; b->ms = e->ms; b->mom = e->mom; b->grads = e->grads;
+  b->n_params = e->L.total;
+  b->frame_ring = e->ring; b->ring_slots = e->R;
+  b->tau = e->counters; b->global_step = e->counters + 1;
+  b->actions = e->actions; b->rewards = e->rewards; b->terminals = e->terms;
+  b->z = e->z; b->returns = e->R_buf; b->loss = e->loss; b->sumsq = e->sumsq;
+  b->act_l1 = e->act_l1; b->act_l2 = e->act_l2; b->act_l3 = e->act_l3;
+  b->frame_pool = e->pool;
+  b->env_frame = e->env.frame; b->env_lives = e->env.lives; b->env_episode = e->env.episode;
+  b->env_step = e->env.ep_step; b->env_len = e->env.ep_len;
+  b->zs = e->L.zs; b->n_tensors = e->L.nt;
+  for (int i = 0; i < e->L.nt; ++i) { b->offsets[i] = e->L.off[i]; b->sizes[i] = e->L.size[i]; }
+  return 0;
+}
+
+// ---- profiling hook: average duration of one engine kernel, HIP events on the caller's stream ----
+extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void* stream, float* avg_ms) {
+  if (!e || !avg_ms || iters < 1 || !e->reset_done)
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_time_kernel", "bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  const NetLayout& L = e->L;
+  const int E = e->E;
+  auto launch = [&]() -> int {
+    switch (kernel) {
+      case A3C_KER_CONV12_FWD:
+        return a3c_conv12_launch(L, e->params, ring_addr(e, 0), E, e->act_l1, e->act_l2, s);
+      case A3C_KER_FC_FWD: {
+        GemmArgs g = {};
+        g.A = e->act_l2; g.lda = FLAT; g.B = e->params + L.off[T_FCW]; g.ldb = FC; g.C = e->act_l3; g.ldc = FC;
+        g.M = E; g.N = FC; g.K = FLAT; g.epi = EPI_BIAS_RELU; g.bias = e->params + L.off[T_FCB];
+        g.slab = e->fslab_e; g.nsplit = e->fsplit_e;
+        return a3c_gemm(true, true, g, s);
+      }
+      case A3C_KER_ENV_STEP:
+        return a3c_env_step_launch(e->envp, e->env, E, e->actions, e->rewards, e->terms, -1.0f, 1.0f, e->pool,
+                                   e->ring, e->R, e->counters, 0, s);
+      case A3C_KER_CONV_BWD: {
+        const BwdPlan p = a3c_bwd_plan(L, e->nE);
+        return a3c_conv_bwd_launch(L, e->params, ring_addr(e, 0), e->nE, e->act_l1, e->ws + p.dl2, e->ws, s);
+      }
+      default:
+        return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_time_kernel", "unknown kernel id");
+    }
+  };
+  int rc = launch();   // warm
+  if (rc) return rc;
+  hipEvent_t a, b;
+  A3C_CHECK(hipEventCreate(&a));
+  A3C_CHECK(hipEventCreate(&b));
+  A3C_CHECK(hipEventRecord(a, s));
+  for (int i = 0; i < iters && !rc; ++i) rc = launch();
+  A3C_CHECK(hipEventRecord(b, s));
+  A3C_CHECK(hipEventSynchronize(b));
+  float ms = 0.f;
+  A3C_CHECK(hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  if (rc) return rc;
+  *avg_ms = ms / (float)iters;
+  return 0;
+}

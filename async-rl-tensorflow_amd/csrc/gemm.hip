@@ -1,0 +1,163 @@
+// FP32 GEMM on gfx950 matrix cores (v_mfma_f32_32x32x2_f32: exact fp32 products, fp32
+// accumulation) for the fully-connected layers of the trunk (ops.py:32-46 ``linear``):
+//   forward  l3 = relu(l2 @ W + b)                       (agent.py:251)
+//   backward dW = l2^T @ dl3, db = colsum(dl3), dl2 = (dl3 @ W^T) * (l2 > 0)
+//   heads    dWh = l3^T @ dz, dbh = colsum(dz)
+// Tile 64x64x16, 256 threads = 2x2 waves of 32x32, LDS-staged operands with a register
+// prefetch of the next K-tile, optional split-K into fp32 slabs (reduced by k_reduce_slabs
+// with the epilogue) and an optional fused column sum of the B operand (bias gradients).
+#include "gemm.h"
+
+#define BM 64
+#define BN 64
+#define BK 16
+#define PAD 4
+
+template <bool A_KC, bool B_NC>
+__global__ void __launch_bounds__(256) k_gemm_f32(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) float As[BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[BK][BN + PAD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int ks = blockIdx.z;
+  const int kbeg = ks * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  const bool do_colsum = g.colsum != nullptr && blockIdx.y == 0;
+
+  // per-thread load coordinates
+  int a_r, a_c, b_r, b_c;
+  if (A_KC) { a_r = tid >> 2; a_c = (tid & 3) * 4; }   // row m, k quad
+  else      { a_r = tid >> 4; a_c = (tid & 15) * 4; }  // row k, m quad
+  if (B_NC) { b_r = tid >> 4; b_c = (tid & 15) * 4; }  // row k, n quad
+  else      { b_r = tid >> 2; b_c = (tid & 3) * 4; }   // row n, k quad
+
+  auto load_a = [&](int k0) -> f32x4 {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (A_KC) {
+      int m = m0 + a_r, k = k0 + a_c;
+      if (m < g.M && k < kend) v = *(const f32x4*)(g.A + (int64_t)m * g.lda + k);
+    } else {
+      int k = k0 + a_r, m = m0 + a_c;
+      if (k < kend && m < g.M) v = *(const f32x4*)(g.A + (int64_t)k * g.lda + m);
+    }
+    return v;
+  };
+  auto load_b = [&](int k0) -> f32x4 {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (B_NC) {
+      int k = k0 + b_r, n = n0 + b_c;
+      if (k < kend && n < g.N) v = *(const f32x4*)(g.B + (int64_t)k * g.ldb + n);
+    } else {
+      int n = n0 + b_r, k = k0 + b_c;
+      if (n < g.N && k < kend) v = *(const f32x4*)(g.B + (int64_t)n * g.ldb + k);
+    }
+    return v;
+  };
+  auto store_a = [&](f32x4 v) {
+    if (A_KC) { As[a_c][a_r] = v[0]; As[a_c + 1][a_r] = v[1]; As[a_c + 2][a_r] = v[2]; As[a_c + 3][a_r] = v[3]; }
+    else      { *(f32x4*)&As[a_r][a_c] = v; }
+  };
+  auto store_b = [&](f32x4 v) {
+    if (B_NC) { *(f32x4*)&Bs[b_r][b_c] = v; }
+    else      { Bs[b_c][b_r] = v[0]; Bs[b_c + 1][b_r] = v[1]; Bs[b_c + 2][b_r] = v[2]; Bs[b_c + 3][b_r] = v[3]; }
+  };
+
+  f32x16 acc = {};
+  float csum = 0.f;
+  f32x4 ra = load_a(kbeg), rb = load_b(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();
+    store_a(ra);
+    store_b(rb);
+    __syncthreads();
+    if (k0 + BK < kend) { ra = load_a(k0 + BK); rb = load_b(k0 + BK); }
+    if (do_colsum && tid < BN) {
+#pragma unroll
+      for (int k = 0; k < BK; ++k) csum += Bs[k][tid];
+    }
+    const int kh = lane >> 5, c = lane & 31;
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      float a = As[2 * kk + kh][wm * 32 + c];
+      float b = Bs[2 * kk + kh][wn * 32 + c];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+  }
+
+  const int col = n0 + wn * 32 + (lane & 31);
+  if (g.nsplit > 1) {
+    float* out = g.slab + (int64_t)ks * g.M * g.N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < g.M && col < g.N) out[(int64_t)row * g.N + col] = acc[r];
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < g.M && col < g.N) {
+        float v = acc[r];
+        if (g.epi == EPI_BIAS_RELU) v = fmaxf(v + g.bias[col], 0.f);
+        else if (g.epi == EPI_BIAS) v = v + g.bias[col];
+        else if (g.epi == EPI_MASK) v = g.mask[(int64_t)row * g.ldm + col] > 0.f ? v : 0.f;
+        g.C[(int64_t)row * g.ldc + col] = v;
+      }
+    }
+  }
+  if (do_colsum && tid < BN && n0 + tid < g.N) g.colsum[(int64_t)ks * g.N + n0 + tid] = csum;
+}
+
+// dst[row*ldc + col] = epi(scale * sum_s slab[s][row][col])
+__global__ void k_reduce_slabs(const float* __restrict__ slab, int nsplit, int M, int N,
+                               float* __restrict__ C, int64_t ldc, int epi,
+                               const float* __restrict__ bias, const float* __restrict__ mask,
+                               int64_t ldm) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = (int64_t)M * N;
+  if (i >= total) return;
+  float v = 0.f;
+  for (int s = 0; s < nsplit; ++s) v += slab[(int64_t)s * total + i];
+  int row = (int)(i / N), col = (int)(i - (int64_t)row * N);
+  if (epi == EPI_BIAS_RELU) v = fmaxf(v + bias[col], 0.f);
+  else if (epi == EPI_BIAS) v = v + bias[col];
+  else if (epi == EPI_MASK) v = mask[(int64_t)row * ldm + col] > 0.f ? v : 0.f;
+  C[(int64_t)row * ldc + col] = v;
+}
+
+int a3c_gemm_plan_split(int M, int N, int K, int target_blocks) {
+  int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int ktiles = (K + BK - 1) / BK;
+  int split = target_blocks / (tiles > 0 ? tiles : 1);
+  if (split < 1) split = 1;
+  if (split > ktiles) split = ktiles;
+  if (split > 32) split = 32;
+  return split;
+}
+
+int a3c_gemm(bool a_kc, bool b_nc, GemmArgs g, hipStream_t s) {
+  if (g.M <= 0 || g.N <= 0) return 0;
+  if (((a_kc || !b_nc) && (g.K & 3)) || (g.lda & 3) || (g.ldb & 3) ||
+      (((uintptr_t)g.A | (uintptr_t)g.B) & 15) || (a_kc ? 0 : (g.M & 3)) || (b_nc ? (g.N & 3) : 0))
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_gemm", "unaligned operands (need 16-B alignment, dims %4)");
+  if (g.nsplit < 1) g.nsplit = 1;
+  int ktiles = (g.K + BK - 1) / BK;
+  int per = (ktiles + g.nsplit - 1) / g.nsplit;
+  g.kchunk = per * BK;
+  g.nsplit = (ktiles + per - 1) / per;
+  if (g.nsplit > 1 && !g.slab) return a3c_set_error(A3C_ERR_INVALID, "a3c_gemm", "split-K needs a slab");
+  dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, g.nsplit);
+  if (a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32<true, true>), grid, dim3(256), 0, s, g);
+  else if (a_kc && !b_nc) hipLaunchKernelGGL((k_gemm_f32<true, false>), grid, dim3(256), 0, s, g);
+  else if (!a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32<false, true>), grid, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((k_gemm_f32<false, false>), grid, dim3(256), 0, s, g);
+  A3C_CHECK(hipGetLastError());
+  if (g.nsplit > 1) {
+    int64_t total = (int64_t)g.M * g.N;
+    hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                       g.slab, g.nsplit, g.M, g.N, g.C, g.ldc, g.epi, g.bias, g.mask, g.ldm);
+    A3C_CHECK(hipGetLastError());
+  }
+  return 0;
+}

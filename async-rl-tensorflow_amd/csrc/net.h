@@ -1,0 +1,88 @@
+// NIPS trunk geometry (agent.py:226-252, network.py:439-448) and the flat parameter layout.
+#pragma once
+#include "a3c_common.h"
+#include "../../include/a3c_hip.h"
+
+// fixed trunk geometry: 84x84x4 -> conv 8x8/4 16 -> conv 4x4/2 32 -> fc 256
+#define IMG 84
+#define PLANE (IMG * IMG)      // 7056 bytes per u8 frame plane
+#define C1_K 8
+#define C1_S 4
+#define C1_O 20                 // conv1 output side
+#define C1_N 16                 // conv1 channels
+#define C1_P (C1_O * C1_O)      // 400 positions
+#define C2_K 4
+#define C2_S 2
+#define C2_O 9
+#define C2_N 32
+#define C2_Q (C2_O * C2_O)      // 81 positions
+#define FLAT (C2_Q * C2_N)      // 2592
+#define FC 256
+#define HIST 4
+#define KC1 (C1_K * C1_K * HIST) // 256 = conv1 reduction length
+#define KC2 (C2_K * C2_K * C1_N) // 256 = conv2 reduction length
+#define L1S_LD 20               // LDS row stride (floats) of the conv1 output tile
+
+enum { T_L1W = 0, T_L1B, T_L2W, T_L2B, T_FCW, T_FCB, T_HW, T_HB, T_VW, T_VB };
+
+struct NetLayout {
+  int algo, A, zs;
+  int nt;
+  int64_t off[A3C_MAX_TENSORS], size[A3C_MAX_TENSORS];
+  int64_t total;
+};
+
+inline int a3c_zs(int algo, int A) {
+  int w = algo == A3C_ALGO_A3C ? A + 1 : A;
+  return (w + 3) & ~3;
+}
+
+inline int a3c_make_layout(const a3c_net_desc* d, NetLayout* L) {
+  if (!d) return -1;
+  if (d->trunk != A3C_TRUNK_NIPS || d->history_length != HIST || d->screen_h != IMG ||
+      d->screen_w != IMG || d->action_size < 1 || d->action_size > 31 ||
+      (d->algo != A3C_ALGO_A3C && d->algo != A3C_ALGO_Q))
+    return -1;
+  const int A = d->action_size;
+  L->algo = d->algo;
+  L->A = A;
+  L->zs = a3c_zs(d->algo, A);
+  int64_t sizes[10] = {(int64_t)KC1 * C1_N, C1_N, (int64_t)KC2 * C2_N, C2_N, (int64_t)FLAT * FC, FC,
+                       (int64_t)FC * A, A, FC, 1};
+  L->nt = d->algo == A3C_ALGO_A3C ? 10 : 8;
+  int64_t o = 0;
+  for (int i = 0; i < L->nt; ++i) {
+    L->off[i] = o;
+    L->size[i] = sizes[i];
+    o += (sizes[i] + 63) & ~(int64_t)63;
+  }
+  L->total = o;
+  return 0;
+}
+
+struct HeadSelect {
+  int mode;                 // -1 none, 0 categorical (a3c), 1 epsilon-greedy argmax (q)
+  uint32_t k0, k1;          // philox key (seed)
+  const int64_t* tau_ptr;   // device tau (nullable)
+  int64_t tau_add;          // tau = *tau_ptr + tau_add
+  const int32_t* env_ids;   // nullable: env id = env_id_base + (b % E)
+  int env_id_base;
+  int E;
+  const float* eps;         // mode 1: per env (index b % E)
+  int32_t* actions;         // [B]
+};
+
+// forward of B states; returns 0 or error
+int a3c_forward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
+                       float* act_l1, float* act_l2, float* act_l3, float* z, float* slab,
+                       int fc_split, const HeadSelect& sel, hipStream_t s);
+int64_t a3c_fwd_slab_floats(int64_t B, int* split_out);
+
+// stage the HIST u8 planes of state b into LDS (HIST x 441 uint4)
+__device__ inline void stage_state(const StateAddr& sa, int64_t b, int64_t tau0, uint8_t* x8) {
+  for (int i = threadIdx.x; i < HIST * (PLANE / 16); i += blockDim.x) {
+    int c = i / (PLANE / 16), j = i - c * (PLANE / 16);
+    const uint4* src = (const uint4*)state_plane(sa, b, c, tau0);
+    ((uint4*)(x8 + c * PLANE))[j] = src[j];
+  }
+}

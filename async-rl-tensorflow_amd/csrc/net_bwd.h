@@ -1,0 +1,46 @@
+#pragma once
+#include "net.h"
+
+// per-workgroup partial slab of k_conv_bwd: dW1 [256][16] (unscaled by 1/255), dW2 [256][32],
+// db1 [16], db2 [32]
+#define CB_OFF_W1 0
+#define CB_OFF_W2 (KC1 * C1_N)                    // 4096
+#define CB_OFF_B1 (CB_OFF_W2 + KC2 * C2_N)         // 12288
+#define CB_OFF_B2 (CB_OFF_B1 + C1_N)               // 12304
+#define CB_SLAB (CB_OFF_B2 + C2_N)                 // 12336
+
+struct FinalizeSeg {
+  const float* src;       // element (r, c) of split s: src[s*split_stride + r*src_ld + col0 + c]
+  int64_t split_stride;
+  int nsplit, rows, src_ld, col0, ncols;
+  int64_t dst_off;        // dst[dst_off + r*dst_ld + c] = scale * sum_s
+  int dst_ld;
+  float scale;
+};
+struct FinalizeSegs {
+  FinalizeSeg s[12];
+  int n;
+  float* dst;
+};
+
+struct BwdPlan {
+  int nwg, per_wg, head_split, fc_split;
+  int64_t dz, dh3, dl2, terms, hgrad, hcol, hslab, fccol, fcslab, cslab, total;  // float offsets
+};
+
+BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B);
+int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
+                        const float* act_l1, const float* act_l2, const float* act_l3,
+                        const float* z, const int32_t* actions, const float* target, float beta,
+                        int literal, float* grads, float* loss_out, float* ws, hipStream_t s);
+int a3c_returns_launch(const float* rewards, const uint8_t* terms, const float* boot, int64_t boot_stride,
+                       int n, int64_t E, double gamma, float* R, hipStream_t s);
+int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float* qn, int64_t B, int A,
+                         int zs, double discount, float* target, hipStream_t s);
+int a3c_select_launch(const float* z, int64_t B, int zs, int A, const HeadSelect& sel, hipStream_t s);
+void a3c_conv12_set_smem();
+void a3c_conv_bwd_set_smem();
+int a3c_conv12_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, float* act_l1,
+                      float* act_l2, hipStream_t s);
+int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,
+                        const float* dl2, float* ws, hipStream_t s);

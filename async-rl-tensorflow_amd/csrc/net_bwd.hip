@@ -1,0 +1,454 @@
+// Loss + backward of the NIPS trunk on gfx950.
+//
+//  k_returns     n-step return per env in float64 (assets/a3c.png Algorithm S3).
+//  k_td_target   agent.py:186-190 in float64.
+//  k_head_bwd    one wave per sample: softmax/log-softmax/entropy, network.py:81-94 losses
+//                (A11 fixes) or agent.py:310-314 MSE, dz, dl3 = (W_h dz) * (l3 > 0).
+//  fc layer      gemm.hip: dW = l2^T dl3 (+colsum -> db), dl2 = (dl3 W^T) * (l2 > 0),
+//                dW_h = l3^T dz (+colsum -> db_h).
+//  k_conv_bwd    one workgroup per group of samples, three MFMA phases on LDS-resident tiles:
+//                dW2 += patches(l1)^T dl2, dl1 = col2im(dl2 W2^T) * (l1 > 0) computed per
+//                stride-2 parity class (4 waves = 4 classes, K = 2x2 taps x 32), and
+//                dW1 += patches(x/255)^T dl1 (conv1 gets weight grads only).  Per-workgroup
+//                partial slabs, reduced deterministically by k_finalize.
+#include "net.h"
+#include "gemm.h"
+#include "net_bwd.h"
+
+// ---------------------------------------------------------------------------------------
+__global__ void k_returns(const float* __restrict__ rewards, const uint8_t* __restrict__ terms,
+                          const float* __restrict__ boot, int64_t boot_stride, int n, int64_t E,
+                          double gamma, float* __restrict__ R) {
+#pragma clang fp contract(off)
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  double r = (double)boot[e * boot_stride];
+  for (int i = n - 1; i >= 0; --i) {
+    if (terms[i * E + e]) r = 0.0;
+    r = (double)rewards[i * E + e] + gamma * r;
+    R[i * E + e] = (float)r;
+  }
+}
+
+__global__ void k_td_target(const float* __restrict__ rewards, const uint8_t* __restrict__ terms,
+                            const float* __restrict__ qn, int64_t B, int A, int zs, double discount,
+                            float* __restrict__ target) {
+#pragma clang fp contract(off)
+  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float m = qn[b * zs];
+  for (int j = 1; j < A; ++j) m = fmaxf(m, qn[b * zs + j]);
+  double t = terms[b] ? 1.0 : 0.0;
+  double v = (1.0 - t) * discount * (double)m + (double)rewards[b];
+  target[b] = (float)v;
+}
+
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ z, int zs, int A, int algo,
+                                                  const int32_t* __restrict__ actions,
+                                                  const float* __restrict__ target,
+                                                  const float* __restrict__ h3,
+                                                  const float* __restrict__ Wp,
+                                                  const float* __restrict__ Wv, float beta,
+                                                  int literal, float invB, int64_t B,
+                                                  float* __restrict__ dz, float* __restrict__ dh3,
+                                                  float* __restrict__ terms) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float myz = lane < zs ? z[b * zs + lane] : 0.f;
+  const int a = actions[b];
+  const float tgt = target[b];
+  float mydz = 0.f, dV = 0.f;
+  if (algo == A3C_ALGO_A3C) {
+    float l = lane < A ? myz : -INFINITY;
+    float m = wave_max(l);
+    float ex = lane < A ? expf(myz - m) : 0.f;
+    float s = wave_sum(ex);
+    float pi = lane < A ? ex / s : 0.f;
+    float logpi = lane < A ? (myz - m) - logf(s) : 0.f;
+    float H = -wave_sum(lane < A ? pi * logpi : 0.f);
+    float V = __shfl(myz, A, 64);
+    float adv = tgt - V;
+    float lpa = __shfl(logpi, a, 64);
+    if (lane < A) mydz = -adv * ((lane == a ? 1.f : 0.f) - pi) + beta * pi * (logpi + H);
+    dV = -adv + (literal ? lpa : 0.f);
+    if (lane == A) mydz = dV;
+    if (lane == 0) {
+      float pl = -(lpa * adv) - beta * H;
+      float vl = 0.5f * adv * adv;
+      terms[b * 4 + 0] = pl;
+      terms[b * 4 + 1] = vl;
+      terms[b * 4 + 2] = H;
+      terms[b * 4 + 3] = pl + vl;
+    }
+  } else {
+    float qa = __shfl(myz, a, 64);
+    float delta = tgt - qa;
+    if (lane == a) mydz = -2.f * delta * invB;
+    if (lane == 0) {
+      terms[b * 4 + 0] = delta * delta * invB;
+      terms[b * 4 + 1] = qa * invB;
+      terms[b * 4 + 2] = 0.f;
+      terms[b * 4 + 3] = 0.f;
+    }
+  }
+  if (lane < zs) dz[b * zs + lane] = mydz;
+  // dl3[k] = (sum_j W[k][j] dz_j) * (l3[k] > 0), k = 4*lane + i
+  f32x4 g = {0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < A; ++j) {
+    float dj = __shfl(mydz, j, 64);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g[i] += Wp[(int64_t)(4 * lane + i) * A + j] * dj;
+  }
+  if (Wv) {
+    f32x4 wv = *(const f32x4*)(Wv + 4 * lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g[i] += wv[i] * dV;
+  }
+  f32x4 h = *(const f32x4*)(h3 + b * FC + 4 * lane);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) g[i] = h[i] > 0.f ? g[i] : 0.f;
+  *(f32x4*)(dh3 + b * FC + 4 * lane) = g;
+}
+
+// ---------------------------------------------------------------------------------------
+// fused conv backward
+// ---------------------------------------------------------------------------------------
+#define CB_X8 (HIST * PLANE)                 // 28224
+#define CB_L1_LD 20
+#define CB_L1 (C1_P * CB_L1_LD * 4)          // 32000
+#define CB_DL2_LD 36
+#define CB_DL2 (C2_Q * CB_DL2_LD * 4)        // 11664
+#define CB_DL1_LD 16
+#define CB_DL1 (C1_P * CB_DL1_LD * 4)        // 25600
+#define CB_SMEM (CB_X8 + CB_L1 + CB_DL2 + CB_DL1 + 4 * 64 * 4)
+
+__global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int per_wg,
+                                                  const float* __restrict__ act_l1,
+                                                  const float* __restrict__ dl2,
+                                                  const float* __restrict__ W2,
+                                                  float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* x8 = smem;
+  float* l1s = (float*)(smem + CB_X8);
+  float* dl2s = (float*)(smem + CB_X8 + CB_L1);
+  float* dl1s = (float*)(smem + CB_X8 + CB_L1 + CB_DL2);
+  float* red = (float*)(smem + CB_X8 + CB_L1 + CB_DL2 + CB_DL1);   // [4 waves][64]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int i16 = lane & 15, j4 = lane >> 4;
+  const int64_t tau0 = sa.tau_ptr ? *sa.tau_ptr : 0;
+  const int64_t b0 = (int64_t)blockIdx.x * per_wg;
+  const int64_t b1 = min(B, b0 + per_wg);
+
+  // parity class of this wave for dl1: (py, px)
+  const int py = wid >> 1, px = wid & 1;
+  // W2 taps for the class: w2c[(dy*2+dx)*8 + nb*4 + c4] = W2[py+2dy][px+2dx][ci=i16][16nb+4j4+c4]
+  float w2c[32];
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int kh = py + 2 * dy, kw = px + 2 * dx;
+        f32x4 w = *(const f32x4*)(W2 + ((kh * C2_K + kw) * C1_N + i16) * C2_N + 16 * nb + 4 * j4);
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) w2c[(dy * 2 + dx) * 8 + nb * 4 + c4] = w[c4];
+      }
+
+  f32x4 accW2[4][2];
+  f32x4 accW1[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    accW2[t][0] = accW2[t][1] = accW1[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  float db1acc = 0.f, db2acc = 0.f;
+
+  for (int64_t b = b0; b < b1; ++b) {
+    __syncthreads();   // previous sample done with LDS
+    stage_state(sa, b, tau0, x8);
+    for (int i = tid; i < C1_P * 4; i += 256) {     // l1 [400][16] -> stride 20
+      int p = i >> 2, q4 = i & 3;
+      *(f32x4*)(l1s + p * CB_L1_LD + 4 * q4) = *(const f32x4*)(act_l1 + (b * C1_P + p) * C1_N + 4 * q4);
+    }
+    for (int i = tid; i < C2_Q * 8; i += 256) {     // dl2 [81][32] -> stride 36
+      int q = i >> 3, q4 = i & 7;
+      *(f32x4*)(dl2s + q * CB_DL2_LD + 4 * q4) = *(const f32x4*)(dl2 + b * FLAT + q * C2_N + 4 * q4);
+    }
+    __syncthreads();
+
+    // ---- (a) dW2[(kh,kw,ci)][n] += sum_q l1[2oy+kh][2ox+kw][ci] * dl2[q][n] ----
+    for (int s = 0; s < (C2_Q + 3) / 4; ++s) {
+      const int q = 4 * s + j4;
+      const bool qv = q < C2_Q;
+      const int qc = qv ? q : 0;
+      const int oy = qc / C2_O, ox = qc - oy * C2_O;
+      const float bq0 = qv ? dl2s[qc * CB_DL2_LD + i16] : 0.f;
+      const float bq1 = qv ? dl2s[qc * CB_DL2_LD + 16 + i16] : 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int mt = 4 * wid + t;
+        const int kh = mt >> 2, kw = mt & 3;
+        const float av = qv ? l1s[((C2_S * oy + kh) * C1_O + C2_S * ox + kw) * CB_L1_LD + i16] : 0.f;
+        accW2[t][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bq0, accW2[t][0], 0, 0, 0);
+        accW2[t][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bq1, accW2[t][1], 0, 0, 0);
+      }
+    }
+
+    // ---- (b) dl1 for parity class (py,px): 100 positions in 7 M-tiles of 16 ----
+    for (int mt = 0; mt < 7; ++mt) {
+      const int pc = 16 * mt + i16;
+      const int pcc = pc < 100 ? pc : 99;
+      const int ay = pcc / 10, cx = pcc - ay * 10;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx) {
+          const int oy = ay - dy, ox = cx - dx;
+          const bool v = oy >= 0 && oy < C2_O && ox >= 0 && ox < C2_O && pc < 100;
+          const int qq = v ? oy * C2_O + ox : 0;
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb) {
+            f32x4 a = *(const f32x4*)(dl2s + qq * CB_DL2_LD + 16 * nb + 4 * j4);
+            if (!v) a = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4)
+              acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c4], w2c[(dy * 2 + dx) * 8 + nb * 4 + c4], acc, 0, 0, 0);
+          }
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pr = 16 * mt + 4 * j4 + r;
+        if (pr < 100) {
+          const int yy = 2 * (pr / 10) + py, xx = 2 * (pr % 10) + px;
+          const int p = yy * C1_O + xx;
+          const float g = l1s[p * CB_L1_LD + i16] > 0.f ? acc[r] : 0.f;
+          dl1s[p * CB_DL1_LD + i16] = g;
+          db1acc += g;
+        }
+      }
+    }
+    // db2[n] += sum_q dl2[q][n]
+    if (tid < C2_N) {
+      float s2 = 0.f;
+      for (int q = 0; q < C2_Q; ++q) s2 += dl2s[q * CB_DL2_LD + tid];
+      db2acc += s2;
+    }
+    __syncthreads();
+
+    // ---- (c) dW1[(kh,kw,cin)][n] += sum_p x[cin][4oy+kh][4ox+kw] * dl1[p][n]  (x unscaled) ----
+    int koff[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int k = 16 * (4 * wid + t) + i16;
+      const int s8 = k >> 2, cin = k & 3;
+      const int kh = s8 >> 3, kw = s8 & 7;
+      koff[t] = cin * PLANE + kh * IMG + kw;
+    }
+    for (int s = 0; s < C1_P / 4; ++s) {
+      const int p = 4 * s + j4;
+      const int oy = p / C1_O, ox = p - oy * C1_O;
+      const int base = (C1_S * oy) * IMG + C1_S * ox;
+      const float bv = dl1s[p * CB_DL1_LD + i16];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        accW1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)x8[base + koff[t]], bv, accW1[t], 0, 0, 0);
+    }
+  }
+
+  // ---- write this workgroup's partial slab ----
+  float* out = slab + (int64_t)blockIdx.x * CB_SLAB;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int mt = 4 * wid + t;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int krow = 16 * mt + 4 * j4 + r;     // dW1 row (kh,kw,cin) / dW2 row (kh,kw,ci)
+      out[CB_OFF_W1 + krow * C1_N + i16] = accW1[t][r];
+      out[CB_OFF_W2 + krow * C2_N + i16] = accW2[t][0][r];
+      out[CB_OFF_W2 + krow * C2_N + 16 + i16] = accW2[t][1][r];
+    }
+  }
+  // db1: lanes with equal i16 (4 j4 groups) then the 4 waves
+  db1acc += __shfl_xor(db1acc, 16, 64);
+  db1acc += __shfl_xor(db1acc, 32, 64);
+  __syncthreads();
+  if (lane < 16) red[wid * 64 + lane] = db1acc;
+  __syncthreads();
+  if (tid < 16) out[CB_OFF_B1 + tid] = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
+  if (tid < C2_N) out[CB_OFF_B2 + tid] = db2acc;
+}
+
+// ---------------------------------------------------------------------------------------
+// deterministic slab reductions into the flat gradient vector
+// ---------------------------------------------------------------------------------------
+__global__ void k_finalize(FinalizeSegs fs) {
+  const FinalizeSeg sg = fs.s[blockIdx.y];
+  const int64_t n = (int64_t)sg.rows * sg.ncols;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / sg.ncols), c = (int)(i - (int64_t)r * sg.ncols);
+    const float* src = sg.src + (int64_t)r * sg.src_ld + sg.col0 + c;
+    float v = 0.f;
+    for (int s = 0; s < sg.nsplit; ++s) v += src[(int64_t)s * sg.split_stride];
+    fs.dst[sg.dst_off + (int64_t)r * sg.dst_ld + c] = v * sg.scale;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_loss_reduce(const float* __restrict__ terms, int64_t B,
+                                                     float* __restrict__ out) {
+  __shared__ double red[4][256];
+  double s[4] = {0, 0, 0, 0};
+  for (int64_t b = threadIdx.x; b < B; b += 256)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s[c] += (double)terms[b * 4 + c];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) red[c][threadIdx.x] = s[c];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) red[c][threadIdx.x] += red[c][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) out[threadIdx.x] = (float)red[threadIdx.x][0];
+}
+
+// ---------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------
+BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
+  BwdPlan p;
+  int64_t o = 0;
+  auto take = [&](int64_t floats) { int64_t r = o; o += (floats + 63) & ~(int64_t)63; return r; };
+  p.nwg = (int)(B < 256 ? B : 256);
+  if (p.nwg < 1) p.nwg = 1;
+  p.per_wg = (int)((B + p.nwg - 1) / p.nwg);
+  p.nwg = (int)((B + p.per_wg - 1) / p.per_wg);
+  p.head_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FC, L.zs, (int)B, 128));
+  p.fc_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FLAT, FC, (int)B, 512));
+  p.dz = take(B * L.zs);
+  p.dh3 = take(B * FC);
+  p.dl2 = take(B * FLAT);
+  p.terms = take(B * 4);
+  p.hgrad = take((int64_t)FC * L.zs);
+  p.hcol = take((int64_t)p.head_split * L.zs);
+  p.hslab = take(p.head_split > 1 ? (int64_t)p.head_split * FC * L.zs : 0);
+  p.fccol = take((int64_t)p.fc_split * FC);
+  p.fcslab = take(p.fc_split > 1 ? (int64_t)p.fc_split * FLAT * FC : 0);
+  p.cslab = take((int64_t)p.nwg * CB_SLAB);
+  p.total = o;
+  return p;
+}
+
+int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
+                        const float* act_l1, const float* act_l2, const float* act_l3,
+                        const float* z, const int32_t* actions, const float* target, float beta,
+                        int literal, float* grads, float* loss_out, float* ws, hipStream_t s) {
+  if (B <= 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "B must be > 0");
+  const BwdPlan p = a3c_bwd_plan(L, B);
+  const float* P = params;
+  float* dz = ws + p.dz;
+  float* dh3 = ws + p.dh3;
+  float* dl2 = ws + p.dl2;
+  float* terms = ws + p.terms;
+  const bool a3c = L.algo == A3C_ALGO_A3C;
+
+  hipLaunchKernelGGL(k_head_bwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, z, L.zs, L.A, L.algo,
+                     actions, target, act_l3, P + L.off[T_HW], a3c ? P + L.off[T_VW] : nullptr, beta,
+                     literal, 1.0f / (float)B, B, dz, dh3, terms);
+  A3C_CHECK(hipGetLastError());
+
+  // head weights: dWh[256][zs] = l3^T dz ; dbh = colsum(dz)
+  GemmArgs g = {};
+  g.A = act_l3; g.lda = FC;          // A(m=feature, k=b) = l3[b][m]  (m contiguous)
+  g.B = dz; g.ldb = L.zs;            // B(k=b, n=j) = dz[b][j]
+  g.C = ws + p.hgrad; g.ldc = L.zs;
+  g.M = FC; g.N = L.zs; g.K = (int)B;
+  g.epi = EPI_STORE; g.slab = ws + p.hslab; g.nsplit = p.head_split; g.colsum = ws + p.hcol;
+  int rc = a3c_gemm(false, true, g, s);
+  if (rc) return rc;
+
+  // fc weights: dW[2592][256] = l2^T dl3 -> grads directly ; db = colsum(dl3)
+  g = GemmArgs{};
+  g.A = act_l2; g.lda = FLAT;
+  g.B = dh3; g.ldb = FC;
+  g.C = grads + L.off[T_FCW]; g.ldc = FC;
+  g.M = FLAT; g.N = FC; g.K = (int)B;
+  g.epi = EPI_STORE; g.slab = ws + p.fcslab; g.nsplit = p.fc_split; g.colsum = ws + p.fccol;
+  rc = a3c_gemm(false, true, g, s);
+  if (rc) return rc;
+
+  // dl2[B][2592] = (dl3 W^T) * (l2 > 0)
+  g = GemmArgs{};
+  g.A = dh3; g.lda = FC;                 // A(m=b, k) = dl3[b][k]
+  g.B = P + L.off[T_FCW]; g.ldb = FC;    // B(k, n) = W[n][k]
+  g.C = dl2; g.ldc = FLAT;
+  g.M = (int)B; g.N = FLAT; g.K = FC;
+  g.epi = EPI_MASK; g.mask = act_l2; g.ldm = FLAT; g.nsplit = 1;
+  rc = a3c_gemm(true, false, g, s);
+  if (rc) return rc;
+
+  rc = a3c_conv_bwd_launch(L, P, sa, B, act_l1, dl2, ws, s);
+  if (rc) return rc;
+
+  FinalizeSegs fs = {};
+  fs.dst = grads;
+  auto seg = [&](const float* src, int64_t stride, int nsplit, int rows, int src_ld, int col0,
+                 int ncols, int64_t dst_off, int dst_ld, float scale) {
+    FinalizeSeg& q = fs.s[fs.n++];
+    q.src = src; q.split_stride = stride; q.nsplit = nsplit; q.rows = rows; q.src_ld = src_ld;
+    q.col0 = col0; q.ncols = ncols; q.dst_off = dst_off; q.dst_ld = dst_ld; q.scale = scale;
+  };
+  const float* cs = ws + p.cslab;
+  seg(cs + CB_OFF_W1, CB_SLAB, p.nwg, 1, 0, 0, KC1 * C1_N, L.off[T_L1W], 0, 1.0f / 255.0f);
+  seg(cs + CB_OFF_B1, CB_SLAB, p.nwg, 1, 0, 0, C1_N, L.off[T_L1B], 0, 1.0f);
+  seg(cs + CB_OFF_W2, CB_SLAB, p.nwg, 1, 0, 0, KC2 * C2_N, L.off[T_L2W], 0, 1.0f);
+  seg(cs + CB_OFF_B2, CB_SLAB, p.nwg, 1, 0, 0, C2_N, L.off[T_L2B], 0, 1.0f);
+  seg(ws + p.fccol, FC, p.fc_split, 1, 0, 0, FC, L.off[T_FCB], 0, 1.0f);
+  seg(ws + p.hgrad, 0, 1, FC, L.zs, 0, L.A, L.off[T_HW], L.A, 1.0f);
+  seg(ws + p.hcol, L.zs, p.head_split, 1, 0, 0, L.A, L.off[T_HB], 0, 1.0f);
+  if (a3c) {
+    seg(ws + p.hgrad, 0, 1, FC, L.zs, L.A, 1, L.off[T_VW], 1, 1.0f);
+    seg(ws + p.hcol, L.zs, p.head_split, 1, 0, L.A, 1, L.off[T_VB], 0, 1.0f);
+  }
+  hipLaunchKernelGGL(k_finalize, dim3(32, fs.n), dim3(256), 0, s, fs);
+  A3C_CHECK(hipGetLastError());
+  if (loss_out) {
+    hipLaunchKernelGGL(k_loss_reduce, dim3(1), dim3(256), 0, s, terms, B, loss_out);
+    A3C_CHECK(hipGetLastError());
+  }
+  return 0;
+}
+
+int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,
+                        const float* dl2, float* ws, hipStream_t s) {
+  const BwdPlan p = a3c_bwd_plan(L, B);
+  hipLaunchKernelGGL(k_conv_bwd, dim3((unsigned)p.nwg), dim3(256), CB_SMEM, s, sa, B, p.per_wg, act_l1,
+                     dl2, P + L.off[T_L2W], ws + p.cslab);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+int a3c_returns_launch(const float* rewards, const uint8_t* terms, const float* boot, int64_t boot_stride,
+                       int n, int64_t E, double gamma, float* R, hipStream_t s) {
+  if (E <= 0) return 0;
+  hipLaunchKernelGGL(k_returns, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, rewards, terms, boot,
+                     boot_stride, n, E, gamma, R);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float* qn, int64_t B, int A,
+                         int zs, double discount, float* target, hipStream_t s) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(k_td_target, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, rewards, terms, qn,
+                     B, A, zs, discount, target);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+void a3c_conv_bwd_set_smem() {
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, CB_SMEM);
+}

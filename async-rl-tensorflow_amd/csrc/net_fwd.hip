@@ -1,0 +1,242 @@
+// Forward of the NIPS trunk + heads on gfx950 matrix cores.
+//
+//  k_conv12_fwd : one workgroup per state.  The 4 u8 frame planes (28 KB) are staged in LDS;
+//                 conv1 (8x8/4, 4->16, ops.py:22-28 VALID NHWC, weights [kh,kw,cin,cout]) runs as
+//                 an implicit GEMM on v_mfma_f32_16x16x4_f32 (M = 400 positions in 25 tiles,
+//                 N = 16, K = 256) with the whole W1 in 64 VGPRs per lane and the A operand
+//                 converted u8 -> f32 in registers (the /255 of agent.py:226 is applied to the
+//                 accumulator).  conv1 + relu goes to LDS (and HBM when the backward needs it);
+//                 conv2 (4x4/2, 16->32, K = 256) reads it back as 16-byte fragments, W2 in
+//                 registers, and writes the (h,w,c)-flattened l2 (agent.py:231-232).
+//  fc layer     : gemm.hip (M = B, N = 256, K = 2592, split-K, bias+relu epilogue).
+//  k_head_fwd   : one wave per state: logits/value (network.py:458,475) or q (agent.py:252),
+//                 then the action draw (softmax sample / epsilon-greedy argmax).
+#include "net.h"
+#include "gemm.h"
+#include "net_bwd.h"
+
+#define X8_BYTES (HIST * PLANE)                      // 28224
+#define L1S_BYTES (C1_P * L1S_LD * 4)                // 32000
+#define CONV12_SMEM (X8_BYTES + L1S_BYTES)
+
+template <bool SAVE_L1>
+__global__ void __launch_bounds__(256) k_conv12_fwd(StateAddr sa, int64_t B,
+                                                    const float* __restrict__ W1,
+                                                    const float* __restrict__ b1,
+                                                    const float* __restrict__ W2,
+                                                    const float* __restrict__ b2,
+                                                    float* __restrict__ act_l1,
+                                                    float* __restrict__ act_l2) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* x8 = smem;
+  float* l1s = (float*)(smem + X8_BYTES);
+  const int64_t b = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i16 = lane & 15, j4 = lane >> 4;
+  const int64_t tau0 = sa.tau_ptr ? *sa.tau_ptr : 0;
+
+  stage_state(sa, b, tau0, x8);
+
+  // conv1 weights: lane (k-sub j4 = cin, col i16 = cout) holds W1[kh][kw][j4][i16] for all 64 (kh,kw)
+  float w1r[64];
+#pragma unroll
+  for (int s = 0; s < 64; ++s) w1r[s] = W1[(s * HIST + j4) * C1_N + i16];
+  const float bias1 = b1[i16];
+  __syncthreads();
+
+  // ---- conv1: 25 M-tiles of 16 positions, K = 64 steps of (kh,kw) x 4 cin ----
+  for (int m = wid; m < C1_P / 16; m += 4) {
+    const int p = 16 * m + i16;
+    const int oy = p / C1_O, ox = p - oy * C1_O;
+    const uint8_t* row = x8 + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < C1_K; ++kh) {
+      uint32_t lo = *(const uint32_t*)(row + kh * IMG);
+      uint32_t hi = *(const uint32_t*)(row + kh * IMG + 4);
+#pragma unroll
+      for (int kw = 0; kw < 4; ++kw)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32((float)((lo >> (8 * kw)) & 255u), w1r[kh * 8 + kw], acc, 0, 0, 0);
+#pragma unroll
+      for (int kw = 0; kw < 4; ++kw)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32((float)((hi >> (8 * kw)) & 255u), w1r[kh * 8 + 4 + kw], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int pos = 16 * m + 4 * j4 + r;
+      float v = fmaxf(acc[r] * (1.0f / 255.0f) + bias1, 0.f);
+      l1s[pos * L1S_LD + i16] = v;
+      if (SAVE_L1) act_l1[(b * C1_P + pos) * C1_N + i16] = v;
+    }
+  }
+
+  // conv2 weights for this wave's N tile: W2[kh][kw][4*j4 + c4][16*nt + i16]
+  const int nt = wid >> 1, mbase = (wid & 1) * 3;
+  float w2r[64];
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) w2r[kk * 4 + c4] = W2[(kk * C1_N + 4 * j4 + c4) * C2_N + 16 * nt + i16];
+  const float bias2 = b2[16 * nt + i16];
+  __syncthreads();
+
+  // ---- conv2: 6 M-tiles (81 rows padded to 96) x 2 N-tiles, K = 16 (kh,kw) x 16 cin ----
+  int pos0[3];
+#pragma unroll
+  for (int mi = 0; mi < 3; ++mi) {
+    int q = 16 * (mbase + mi) + i16;
+    q = q < C2_Q ? q : C2_Q - 1;
+    int oy = q / C2_O, ox = q - oy * C2_O;
+    pos0[mi] = (C2_S * oy) * C1_O + C2_S * ox;
+  }
+  f32x4 acc2[3];
+#pragma unroll
+  for (int mi = 0; mi < 3; ++mi) acc2[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kh = 0; kh < C2_K; ++kh)
+#pragma unroll
+    for (int kw = 0; kw < C2_K; ++kw)
+#pragma unroll
+      for (int mi = 0; mi < 3; ++mi) {
+        f32x4 a = *(const f32x4*)(l1s + (pos0[mi] + kh * C1_O + kw) * L1S_LD + 4 * j4);
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4)
+          acc2[mi] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c4], w2r[(kh * 4 + kw) * 4 + c4], acc2[mi], 0, 0, 0);
+      }
+#pragma unroll
+  for (int mi = 0; mi < 3; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = 16 * (mbase + mi) + 4 * j4 + r;
+      if (q < C2_Q) act_l2[b * FLAT + q * C2_N + 16 * nt + i16] = fmaxf(acc2[mi][r] + bias2, 0.f);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// action selection from a head row held one-value-per-lane (lane j holds z[j])
+// ---------------------------------------------------------------------------------------
+__device__ inline int32_t select_from_lanes(float myz, int lane, int A, const HeadSelect& sel,
+                                            int64_t b) {
+  const int64_t tau = (sel.tau_ptr ? *sel.tau_ptr : 0) + sel.tau_add;
+  const int e = (int)(b % sel.E);
+  const uint32_t env = sel.env_ids ? (uint32_t)sel.env_ids[b] : (uint32_t)(sel.env_id_base + e);
+  u32x4 x = philox4x32((uint32_t)tau, (uint32_t)((uint64_t)tau >> 32), env, P_ACTION, sel.k0, sel.k1);
+  if (sel.mode == 0) {
+    float l = lane < A ? myz : -INFINITY;
+    float m = wave_max(l);
+    float ex = lane < A ? expf(myz - m) : 0.f;
+    float ssum = wave_sum(ex);
+    float pi = ex / ssum;
+    float u = u01(x.x);
+    float cdf = 0.f;
+    int32_t act = A - 1;
+    for (int j = 0; j < A; ++j) {
+      cdf += __shfl(pi, j, 64);
+      if (cdf > u) { act = j; break; }
+    }
+    return act;
+  } else {
+    float eps = sel.eps ? sel.eps[e] : 0.f;
+    if (u01(x.x) < eps) return (int32_t)(x.y % (uint32_t)A);
+    float best = __shfl(myz, 0, 64);
+    int32_t arg = 0;
+    for (int j = 1; j < A; ++j) {
+      float v = __shfl(myz, j, 64);
+      if (v > best) { best = v; arg = j; }
+    }
+    return arg;
+  }
+}
+
+// head: one wave per state.  z[b][j] = h3[b] . W[:,j] + bias[j]
+__global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, int64_t B,
+                                                  const float* __restrict__ Wp, const float* __restrict__ bp,
+                                                  const float* __restrict__ Wv, const float* __restrict__ bv,
+                                                  int A, int zs, float* __restrict__ z, HeadSelect sel) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  f32x4 h = *(const f32x4*)(h3 + b * FC + 4 * lane);
+  float myz = 0.f;
+  for (int j = 0; j < A; ++j) {
+    const float* w = Wp + (int64_t)(4 * lane) * A + j;
+    float p = h[0] * w[0] + h[1] * w[A] + h[2] * w[2 * A] + h[3] * w[3 * A];
+    p = wave_sum(p);
+    if (lane == j) myz = p + bp[j];
+  }
+  if (Wv) {
+    f32x4 w = *(const f32x4*)(Wv + 4 * lane);
+    float p = wave_sum(h[0] * w[0] + h[1] * w[1] + h[2] * w[2] + h[3] * w[3]);
+    if (lane == A) myz = p + bv[0];
+  }
+  if (lane < zs) z[b * zs + lane] = myz;   // padding columns are 0
+  if (sel.mode >= 0) {
+    int32_t a = select_from_lanes(myz, lane, A, sel, b);
+    if (lane == 0) sel.actions[b] = a;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_select(const float* __restrict__ z, int64_t B, int zs, int A,
+                                                HeadSelect sel) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  float myz = lane < zs ? z[b * zs + lane] : 0.f;
+  int32_t a = select_from_lanes(myz, lane, A, sel, b);
+  if (lane == 0) sel.actions[b] = a;
+}
+
+int64_t a3c_fwd_slab_floats(int64_t B, int* split_out) {
+  int split = a3c_gemm_plan_split((int)B, FC, FLAT, 512);
+  split = a3c_gemm_effective_split(FLAT, split);
+  if (split_out) *split_out = split;
+  return split > 1 ? (int64_t)split * B * FC : 0;
+}
+
+int a3c_forward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
+                       float* act_l1, float* act_l2, float* act_l3, float* z, float* slab,
+                       int fc_split, const HeadSelect& sel, hipStream_t s) {
+  if (B <= 0) return 0;
+  const float* P = params;
+  int rc0 = a3c_conv12_launch(L, P, sa, B, act_l1, act_l2, s);
+  if (rc0) return rc0;
+  GemmArgs g = {};
+  g.A = act_l2; g.lda = FLAT;
+  g.B = P + L.off[T_FCW]; g.ldb = FC;
+  g.C = act_l3; g.ldc = FC;
+  g.M = (int)B; g.N = FC; g.K = FLAT;
+  g.epi = EPI_BIAS_RELU; g.bias = P + L.off[T_FCB];
+  g.slab = slab; g.nsplit = fc_split;
+  int rc = a3c_gemm(true, true, g, s);
+  if (rc) return rc;
+  const float* Wv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VW] : nullptr;
+  const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
+  hipLaunchKernelGGL(k_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, act_l3, B,
+                     P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+int a3c_conv12_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, float* act_l1,
+                      float* act_l2, hipStream_t s) {
+  if (act_l1)
+    hipLaunchKernelGGL((k_conv12_fwd<true>), dim3((unsigned)B), dim3(256), CONV12_SMEM, s, sa, B,
+                       P + L.off[T_L1W], P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2);
+  else
+    hipLaunchKernelGGL((k_conv12_fwd<false>), dim3((unsigned)B), dim3(256), CONV12_SMEM, s, sa, B,
+                       P + L.off[T_L1W], P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+int a3c_select_launch(const float* z, int64_t B, int zs, int A, const HeadSelect& sel, hipStream_t s) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(k_select, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, z, B, zs, A, sel);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+void a3c_conv12_set_smem() {
+  (void)hipFuncSetAttribute((const void*)k_conv12_fwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize, CONV12_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_conv12_fwd<false>, hipFuncAttributeMaxDynamicSharedMemorySize, CONV12_SMEM);
+}

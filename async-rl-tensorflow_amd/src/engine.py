@@ -1,0 +1,141 @@
+"""Batched A3C / Q-learning actor-learner engine (one per GPU) over the C-ABI.
+
+``Engine.iterate()`` is one pass of the rollout + gradient path for E envs: n env steps
+(forward, action draw, env step, Atari preprocessing into the frame ring), bootstrap /
+target-net forward, returns, loss + backward, per-tensor clip, then the optional multi-GPU
+gradient exchange (``exchange`` callback, e.g. an RCCL all-reduce) and the RMSProp apply.
+It replaces the per-worker loop of agent.py:52-67 (+ observe/batch_update :153-207) and the
+parameter-server apply of main.py:60-66.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+GAMES = {  # ALE minimal action sets / starting lives
+    'Pong-v0': (6, 0),
+    'Breakout-v0': (4, 5),
+    'SpaceInvaders-v0': (6, 3),
+}
+
+
+class _DevArray:
+    """Zero-copy view of engine-owned device memory for torch.as_tensor."""
+
+    def __init__(self, ptr, shape, typestr):
+        self.__cuda_array_interface__ = {'data': (int(ptr), False), 'shape': tuple(int(s) for s in shape),
+                                         'typestr': typestr, 'version': 2, 'strides': None}
+
+
+def _view(ptr, shape, dtype):
+    typestr = {torch.float32: '<f4', torch.int32: '<i4', torch.uint8: '|u1', torch.int64: '<i8',
+               torch.uint32: '<u4'}[dtype]
+    return torch.as_tensor(_DevArray(ptr, shape, typestr), device='cuda')
+
+
+class Engine:
+    def __init__(self, num_envs=256, n_step=5, action_size=6, algo='a3c', start_lives=0, num_frames=1024,
+                 seed=123, env_id_base=0, world_size=1, use_graph=True, **overrides):
+        _lib.require_device()
+        cfg = _lib.EngineConfig()
+        lib().a3c_engine_config_default(ctypes.byref(cfg))
+        cfg.net = _lib.net_desc(action_size, algo)
+        cfg.num_envs = int(num_envs)
+        cfg.n_step = int(n_step)
+        cfg.start_lives = int(start_lives)
+        cfg.num_frames = int(num_frames)
+        cfg.seed = int(seed)
+        cfg.env_id_base = int(env_id_base)
+        cfg.world_size = int(world_size)
+        cfg.use_graph = 1 if use_graph else 0
+        for k, v in overrides.items():
+            if not hasattr(cfg, k):
+                raise ValueError(f'unknown engine option {k}')
+            setattr(cfg, k, v)
+        self.cfg = cfg
+        self.algo = algo
+        self.A = int(action_size)
+        self.E, self.n = int(num_envs), int(n_step)
+        h = ctypes.c_void_p()
+        check(lib().a3c_engine_create(ctypes.byref(cfg), ctypes.byref(h)), 'a3c_engine_create')
+        self._h = h
+        b = _lib.EngineBuffers()
+        check(lib().a3c_engine_get_buffers(h, ctypes.byref(b)), 'a3c_engine_get_buffers')
+        self._b = b
+        self.zs = int(b.zs)
+        self.offsets = [int(b.offsets[i]) for i in range(b.n_tensors)]
+        self.sizes = [int(b.sizes[i]) for i in range(b.n_tensors)]
+        P, E, n = int(b.n_params), self.E, self.n
+        self.params = _view(b.params, (P,), torch.float32)
+        self.target_params = _view(b.target_params, (P,), torch.float32)
+        self.ms = _view(b.ms, (P,), torch.float32)
+        self.mom = _view(b.mom, (P,), torch.float32)
+        self.grads = _view(b.grads, (P,), torch.float32)
+        self.frame_ring = _view(b.frame_ring, (E, b.ring_slots, 84, 84), torch.uint8)
+        self.ring_slots = int(b.ring_slots)
+        self.counters = _view(b.tau, (2,), torch.int64)
+        self.actions = _view(b.actions, (n, E), torch.int32)
+        self.rewards = _view(b.rewards, (n, E), torch.float32)
+        self.terminals = _view(b.terminals, (n, E), torch.uint8)
+        self.z = _view(b.z, (n + 1, E, self.zs), torch.float32)
+        self.returns = _view(b.returns, (n, E), torch.float32)
+        self.loss = _view(b.loss, (4,), torch.float32)
+        self.sumsq = _view(b.sumsq, (b.n_tensors,), torch.float32)
+        self.act_l1 = _view(b.act_l1, (n * E, 6400), torch.float32)
+        self.act_l2 = _view(b.act_l2, (n * E, 2592), torch.float32)
+        self.act_l3 = _view(b.act_l3, (n * E, 256), torch.float32)
+        self.frame_pool = _view(b.frame_pool, (int(cfg.num_frames), 210, 160, 3), torch.uint8)
+        self.env_frame = _view(b.env_frame, (E,), torch.int32)
+        self.env_lives = _view(b.env_lives, (E,), torch.int32)
+        self.env_episode = _view(b.env_episode, (E,), torch.int32)
+        self.env_step = _view(b.env_step, (E,), torch.int32)
+        self.env_len = _view(b.env_len, (E,), torch.int32)
+
+    def close(self):
+        if getattr(self, '_h', None):
+            lib().a3c_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------------------------
+    def reset(self, host_params=None):
+        """host_params: flat float32 numpy array of the engine layout (None keeps params)."""
+        arg = None
+        if host_params is not None:
+            hp = np.ascontiguousarray(np.asarray(host_params, dtype=np.float32))
+            if hp.size != self.params.numel():
+                raise ValueError('host_params has the wrong length')
+            self._hp = hp
+            arg = hp.ctypes.data_as(ctypes.c_void_p)
+        check(lib().a3c_engine_reset(self._h, arg, _lib.stream_handle()), 'a3c_engine_reset')
+
+    def rollout_grad(self):
+        check(lib().a3c_engine_rollout_grad(self._h, _lib.stream_handle()), 'a3c_engine_rollout_grad')
+
+    def apply(self):
+        check(lib().a3c_engine_apply(self._h, _lib.stream_handle()), 'a3c_engine_apply')
+
+    def iterate(self, exchange=None):
+        self.rollout_grad()
+        if exchange is not None:
+            exchange(self.grads)
+        self.apply()
+
+    def time_kernel(self, kernel, iters=20):
+        """Average device ms of one engine kernel (HIP events on the current stream)."""
+        out = ctypes.c_float()
+        check(lib().a3c_engine_time_kernel(self._h, int(kernel), int(iters), _lib.stream_handle(),
+                                           ctypes.byref(out)), 'a3c_engine_time_kernel')
+        return float(out.value)
+
+    @property
+    def env_steps_per_iteration(self):
+        return self.E * self.n

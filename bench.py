@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Headline benchmark: env-steps/s of the A3C rollout + gradient path (BASELINE.json metric).
+
+One "step" = one engine iteration on every GPU: E envs x n rollout steps (forward, categorical
+draw, synthetic Atari step, Environment.screen preprocessing into the frame ring), bootstrap
+forward, n-step returns, loss + backward, per-tensor clip, sync RCCL all-reduce of the clipped
+gradients (N > 1) and the RMSProp apply.  Inputs (the HBM-resident RGB frame pool) are on the
+device before the timed region.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Rank 0 prints ONE JSON line (value = all GPUs' env-steps / max-over-ranks wall time), with the
+dominant kernel's roofline (HIP-event timing of that kernel on its live buffers) and the CPU
+baseline (oracle/engine_ref.py on host cores, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'async-rl-tensorflow_amd'))
+sys.path.insert(0, ROOT)
+
+METRIC = json.load(open(os.path.join(ROOT, 'BASELINE.json')))['metric']
+GAMES = {'Pong-v0': (6, 0), 'Breakout-v0': (4, 5), 'SpaceInvaders-v0': (6, 3)}
+
+# algorithmic work per unit (DESIGN.md "Roofline"): FLOP per sample / bytes per env-step
+CONV12_FWD_FLOP = 2 * 400 * 16 * 256 + 2 * 81 * 32 * 256            # 4,603,904
+CONV_BWD_FLOP = 2 * 81 * 32 * 256 * 2 + 2 * 400 * 16 * 256          # 5,931,008
+FC_FWD_FLOP = 2 * 2592 * 256                                        # 1,327,104
+ENV_STEP_BYTES = 210 * 160 * 3 + 84 * 84                            # 107,856
+PEAK_FP32_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix peak (spec)
+PEAK_HBM_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--envs', type=int, default=256, help='envs per GPU (BASELINE config 2: 256)')
+    ap.add_argument('--n-step', type=int, default=5)
+    ap.add_argument('--game', default='Pong-v0', choices=sorted(GAMES))
+    ap.add_argument('--algo', default='a3c', choices=['a3c', 'q'])
+    ap.add_argument('--frames', type=int, default=16384, help='HBM frame pool (16384 = 1.65 GB > L3)')
+    ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--cpu-seconds', type=float, default=12.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-kernel-timing', action='store_true')
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds, game, algo):
+    """oracle/engine_ref.py (numpy restatement of the same iteration) on one host core."""
+    import numpy as np
+    try:
+        from threadpoolctl import threadpool_limits
+        lim = threadpool_limits(1)
+    except Exception:   # pragma: no cover
+        lim = None
+    from oracle.engine_ref import EngineRef
+    from src.initializers import init_params
+    from src.kernels import param_names_shapes
+    A, lives = GAMES[game]
+    E, n = 8, 5 if algo == 'a3c' else 32
+    p = init_params(param_names_shapes(A, algo), seed=123)
+    ref = EngineRef(p, E, n, A, algo, lives, num_frames=16384, seed=123, dtype=np.float32)
+    ref.cache_screens = False
+    ref.reset()
+    t0 = time.perf_counter()
+    iters = 0
+    while True:
+        out = ref.iterate()
+        ref.apply(out['clipped'])
+        iters += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    if lim is not None:
+        lim.unregister() if hasattr(lim, 'unregister') else None
+    return dict(value=round(iters * E * n / el, 2), unit='env-steps/s', cores=1, kind='port',
+                sample=f'oracle/engine_ref.py {algo} iteration (numpy fp32), {E} envs x n={n}, '
+                       f'{iters} iterations in {el:.1f} s, 1 thread, no screen cache')
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit('--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)')
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+
+    from src import _lib
+    from src.engine import Engine
+    from src.initializers import init_params, flatten_host
+    from src.kernels import param_names_shapes
+
+    A, lives = GAMES[args.game]
+    E, n = args.envs, args.n_step
+    eng = Engine(num_envs=E, n_step=n, action_size=A, algo=args.algo, start_lives=lives, num_frames=args.frames,
+                 seed=123, env_id_base=rank * E, world_size=world, use_graph=not args.no_graph)
+    ns = param_names_shapes(A, args.algo)
+    params = flatten_host(ns, eng.offsets, eng.params.numel(), init_params(ns, seed=123))
+    eng.reset(params)     # every rank starts from the same parameters
+    torch.cuda.synchronize()
+
+    exchange = None
+    if world > 1:
+        def exchange(g):
+            dist.all_reduce(g, op=dist.ReduceOp.SUM)   # sync SUM of per-worker-clipped grads
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        eng.iterate(exchange)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.iterate(exchange)
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    loss = eng.loss.cpu().numpy().tolist()
+    finite = bool(torch.isfinite(eng.params).all().item())
+
+    roofline, kernels = None, {}
+    if rank == 0 and not args.no_kernel_timing:
+        ms = {
+            'k_conv12_fwd': eng.time_kernel(_lib.KER_CONV12_FWD, 20),
+            'k_conv_bwd': eng.time_kernel(_lib.KER_CONV_BWD, 10),
+            'k_gemm_f32(fc fwd)+reduce': eng.time_kernel(_lib.KER_FC_FWD, 20),
+            'k_env_step': eng.time_kernel(_lib.KER_ENV_STEP, 20),
+        }
+        count = {'k_conv12_fwd': n + 1, 'k_conv_bwd': 1, 'k_gemm_f32(fc fwd)+reduce': n + 1, 'k_env_step': n}
+        work = {
+            'k_conv12_fwd': ('mfma', CONV12_FWD_FLOP * E),
+            'k_conv_bwd': ('mfma', CONV_BWD_FLOP * n * E),
+            'k_gemm_f32(fc fwd)+reduce': ('mfma', FC_FWD_FLOP * E),
+            'k_env_step': ('hbm', ENV_STEP_BYTES * E),
+        }
+        iter_ms = el / args.steps * 1e3
+        for k in ms:
+            bound, w = work[k]
+            ach = w / (ms[k] * 1e-3) / (1e12 if bound == 'mfma' else 1e9)
+            kernels[k] = dict(avg_ms=round(ms[k], 4), per_iter=count[k],
+                              share=round(ms[k] * count[k] / iter_ms, 3), bound=bound,
+                              achieved=round(ach, 2), unit='TFLOP/s' if bound == 'mfma' else 'GB/s')
+        dom = max(ms, key=lambda k: ms[k] * count[k])
+        bound, w = work[dom]
+        peak = PEAK_FP32_TFLOPS if bound == 'mfma' else PEAK_HBM_GBS
+        traffic = None
+        pmc = os.path.join(ROOT, 'profiles', 'pmc_hbm_bytes.json')
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get(dom.split('(')[0])
+            except Exception:
+                traffic = None
+        roofline = dict(kernel=dom, bound=bound, achieved=kernels[dom]['achieved'], peak=peak,
+                        unit='TFLOP/s' if bound == 'mfma' else 'GB/s',
+                        frac=round(kernels[dom]['achieved'] / peak, 4), traffic=traffic,
+                        work_per_launch=w, work_unit='FLOP' if bound == 'mfma' else 'B')
+
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_seconds, args.game, args.algo)
+        steps_total = world * E * n * args.steps
+        line = {
+            'metric': METRIC, 'value': round(steps_total / el, 1), 'unit': 'env-steps/s', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 4),
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
+            'data': f'synthetic: HBM-resident hashed RGB 210x160x3 frame pool ({args.frames} frames) stepped by '
+                    f'the on-device synthetic Atari env; random-init NIPS A3C conv net',
+            'config': {'workload': f'{args.game}, {E} envs batched per MI355X, n-step={n}, '
+                                   f'{"A3C" if args.algo == "a3c" else "one-step Q"} conv net (nips trunk)',
+                       'game': args.game, 'envs_per_gpu': E, 'n_step': n, 'action_size': A, 'algo': args.algo,
+                       'env_steps_per_step': world * E * n,
+                       'parallelism': f'dp{world} sync all-reduce (RCCL) of per-worker-clipped grads'
+                       if world > 1 else 'dp1', 'hipgraph': not args.no_graph},
+            'roofline': roofline, 'cpu_baseline': cpu, 'kernels': kernels,
+            'final_loss': loss, 'params_finite': finite,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

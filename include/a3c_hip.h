@@ -1,0 +1,239 @@
+/*
+ * a3c_hip.h -- C-ABI of liba3c_hip.so, the MI355X (gfx950) rollout + gradient path of
+ * datavizweb/async-rl-tensorflow re-built as hand-written HIP kernels.
+ *
+ * The reference has no FFI: its boundary is the Python object API.
+ * Each entry point below names the reference interface (file:line under the reference
+ * root) whose arithmetic it replaces; the Python mirror in
+ * async-rl-tensorflow_amd/src/ binds them through ctypes.
+ *
+ * Conventions
+ *  - extern "C", plain pointers and sizes; every pointer is a CALLER-OWNED device buffer
+ *    unless stated.  Nothing here allocates on the hot path; a3c_engine_create is the only
+ *    allocating call (one-time workspace).
+ *  - every call enqueues on the caller's stream (`stream` is a hipStream_t; NULL = legacy
+ *    default stream) and returns an int status: 0 = ok, otherwise a hipError_t value or one
+ *    of the A3C_ERR_* codes; a3c_last_error() gives the message.  No C++ exception crosses
+ *    the ABI.  The Python side raises ValueError / RuntimeError (network.py:21,28,54).
+ *  - no call is re-entrant on the same engine handle.
+ */
+#ifndef A3C_HIP_H
+#define A3C_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define A3C_OK 0
+#define A3C_ERR_INVALID 10001   /* bad argument / unsupported shape            */
+#define A3C_ERR_STATE 10002     /* engine used in the wrong order               */
+
+#define A3C_ALGO_A3C 0          /* policy + value heads (src/network.py:456-490) */
+#define A3C_ALGO_Q 1            /* one-step Q-learning head (src/agent.py:251-254) */
+
+#define A3C_TRUNK_NIPS 0        /* 16/32/256 trunk: agent.py:226-251, network.py:439-448 */
+
+const char* a3c_version(void);
+const char* a3c_last_error(void);
+/* 1 when a gfx950 device is visible (no compute). */
+int a3c_device_ok(void);
+
+/* ----------------------------------------------------------------------------
+ * Network description and flat parameter layout.
+ * Flat fp32 vector in TF variable order (ops.py:21,24,36,38; agent.py:226-252 /
+ * network.py:443-475); each tensor starts at a 64-float (256 B) aligned offset,
+ * padding floats are zero and stay zero.
+ *  a3c : l1_w[8,8,4,16] l1_b l2_w[4,4,16,32] l2_b l4_w[2592,256] l4_b p_w[256,A] p_b q_w[256,1] q_b
+ *  q   : l1_w l1_b l2_w l2_b l3_w[2592,256] l3_b q_w[256,A] q_b
+ * -------------------------------------------------------------------------- */
+typedef struct a3c_net_desc {
+  int algo;            /* A3C_ALGO_*                                       */
+  int trunk;           /* A3C_TRUNK_NIPS                                   */
+  int action_size;     /* A (<= 31)                                        */
+  int history_length;  /* 4 (config.py:22)                                 */
+  int screen_h;        /* 84                                               */
+  int screen_w;        /* 84                                               */
+} a3c_net_desc;
+
+#define A3C_MAX_TENSORS 16
+/* n_tensors, offsets[i], sizes[i] (floats), total padded length. */
+int a3c_param_layout(const a3c_net_desc* net, int* n_tensors, int64_t* offsets, int64_t* sizes,
+                     int64_t* total);
+/* bytes of scratch a3c_forward / a3c_loss_backward need for batch B */
+int a3c_workspace_bytes(const a3c_net_desc* net, int64_t B, int64_t* bytes);
+
+/* ----------------------------------------------------------------------------
+ * K1  Environment.screen (environment.py:95-99): fp64 luminance truncated to u8, then
+ *     Pillow BILINEAR fixed-point resample (scipy.misc.imresize, environment.py:5-8).
+ *     rgb frames [*, in_h, in_w, 3] u8; frame i reads rgb + (frame_idx ? frame_idx[i] : i)
+ *     * in_h*in_w*3 and writes out + i*out_stride ([out_h][out_w] u8).  Bit-exact.
+ * -------------------------------------------------------------------------- */
+int a3c_preprocess_u8(const uint8_t* rgb, const int32_t* frame_idx, int64_t n, int in_h, int in_w,
+                      uint8_t* out, int64_t out_stride, int out_h, int out_w, void* stream);
+
+/* ----------------------------------------------------------------------------
+ * K2  History (history.py:3-27).  hist is [n][L][h*w] u8 (oldest plane first);
+ *     push: if reset_mask && reset_mask[i]: zero (History.reset, :17-18); then shift one
+ *     plane and append screens[i] (History.add, :13-15).
+ *     get: float32 copy, NHWC [n][h][w][L] when nhwc else [n][L][h][w] (History.get, :20-24).
+ * -------------------------------------------------------------------------- */
+int a3c_history_push(uint8_t* hist, const uint8_t* screens, const uint8_t* reset_mask, int64_t n,
+                     int L, int64_t hw, void* stream);
+int a3c_history_get_f32(const uint8_t* hist, int64_t n, int L, int h, int w, int nhwc, float* out,
+                        void* stream);
+
+/* ----------------------------------------------------------------------------
+ * Forward (agent.py:217-254 q-net / network.py:439-479 a3c net, ops.py:4-46).
+ *  states  [B][L][84][84] u8 (frame values; the /255 of agent.py:226 is applied inside)
+ *  act_l1  [B][400][16]  f32 conv1 out (nullable: only needed for a3c_loss_backward)
+ *  act_l2  [B][2592]     f32 conv2 out, (h,w,c) flatten order (agent.py:231-232)
+ *  act_l3  [B][256]      f32 fc out
+ *  z       [B][zs]       f32 head: a3c -> A logits then V at column A; q -> A q-values.
+ *                         zs = a3c_z_stride(net).
+ * -------------------------------------------------------------------------- */
+int a3c_z_stride(const a3c_net_desc* net);
+int a3c_forward(const a3c_net_desc* net, const float* params, const uint8_t* states, int64_t B,
+                float* act_l1, float* act_l2, float* act_l3, float* z, void* workspace,
+                void* stream);
+
+/* ----------------------------------------------------------------------------
+ * K6  action selection.
+ *  mode 0 (a3c, network.py:461-468 softmax + batch_sample): categorical draw
+ *        u = philox(seed; tau, env_ids[i], P_ACTION); first j with fp32 cumsum(pi)[j] > u.
+ *  mode 1 (q, agent.py:141-151): if u01(x0) < eps[i]: x1 % A  else argmax_j q[j]
+ *        (first maximum, tf.argmax agent.py:254).
+ *  env_ids nullable (= i).  eps nullable in mode 0.
+ * -------------------------------------------------------------------------- */
+int a3c_select_action(int mode, const float* z, int64_t B, int zs, int A, const float* eps,
+                      uint64_t seed, int64_t tau, const int32_t* env_ids, int32_t* actions,
+                      void* stream);
+
+/* ----------------------------------------------------------------------------
+ * K7  n-step returns (assets/a3c.png Algorithm S3) over [n][E] in float64:
+ *     R = bootstrap[e] (0 if terminals[n-1]); R <- r_i + gamma*R, reset at terminals.
+ *     TD target (agent.py:186-190): (1-term)*discount*max_a q_next[i][a] + reward[i] (fp64).
+ * -------------------------------------------------------------------------- */
+int a3c_returns(const float* rewards, const uint8_t* terminals, const float* bootstrap, int n,
+                int64_t E, double gamma, float* R, void* stream);
+int a3c_td_target(const float* rewards, const uint8_t* terminals, const float* q_next, int64_t B,
+                  int A, int zs, double discount, float* target, void* stream);
+
+/* ----------------------------------------------------------------------------
+ * K8+K9  loss + backward (network.py:81-94 with the SURVEY §8 A11 fixes / agent.py:306-317).
+ *  target: a3c -> R (n-step return); q -> TD target.
+ *  a3c loss per sample  -log pi(a)*stopgrad(R-V) - beta*H + (R-V)^2/2, summed over B
+ *      (literal_adv != 0: no stop-gradient, network.py:83-84 literal form);
+ *  q   loss mean((target - Q[a])^2) over B (agent.py:313-314).
+ *  grads: flat fp32 (layout of a3c_param_layout), OVERWRITTEN.
+ *  loss_out (device, 4 floats): a3c {policy_sum, value_sum, entropy_sum, total_sum};
+ *                               q {loss, mean_q_acted, 0, 0}.
+ * -------------------------------------------------------------------------- */
+int a3c_loss_backward(const a3c_net_desc* net, const float* params, const uint8_t* states,
+                      int64_t B, const float* act_l1, const float* act_l2, const float* act_l3,
+                      const float* z, const int32_t* actions, const float* target, float beta,
+                      int literal_adv, float* grads, float* loss_out, void* workspace,
+                      void* stream);
+
+/* ----------------------------------------------------------------------------
+ * K10+K11  per-tensor clip_by_norm (agent.py:316-319) + TF ApplyRMSProp
+ *  (main.py:63-65, agent.py:321): ms += (g^2-ms)(1-rho); mom = mom*momentum +
+ *  lr*g/sqrt(ms+eps); w -= mom.  ms must be initialised to 1.0, mom to 0 (TF1 slots).
+ *  clip <= 0 disables clipping.  sumsq_out (nullable, device, n_tensors floats) receives
+ *  the pre-clip squared norms.  workspace >= a3c_optim_workspace_bytes().
+ *  a3c_clip_grads only clips in place (multi-GPU: clip per worker, then all-reduce).
+ * -------------------------------------------------------------------------- */
+int a3c_optim_workspace_bytes(int64_t total, int64_t* bytes);
+int a3c_clip_grads(float* grads, int n_tensors, const int64_t* offsets, const int64_t* sizes,
+                   float clip, float* sumsq_out, void* workspace, void* stream);
+int a3c_clip_rmsprop_apply(float* params, float* ms, float* mom, float* grads, int n_tensors,
+                           const int64_t* offsets, const int64_t* sizes, float lr, float rho,
+                           float momentum, float eps, float clip, float* sumsq_out,
+                           void* workspace, void* stream);
+
+/* K12  target sync (agent.py:342-344) / theta' <- theta (network.py:96-107). */
+int a3c_copy_params(float* dst, const float* src, int64_t n, void* stream);
+
+/* ----------------------------------------------------------------------------
+ * Batched actor-learner engine: E envs per GPU stepped in lock-step on device
+ * (synthetic ALE stand-in, oracle/synthetic_env.py semantics), n-step rollout,
+ * backward, per-tensor clip, RMSProp.  One process per GPU; the multi-GPU gradient
+ * exchange happens between a3c_engine_rollout_grad and a3c_engine_apply (RCCL from the
+ * host, on the same stream).
+ * -------------------------------------------------------------------------- */
+typedef struct a3c_engine a3c_engine;
+
+typedef struct a3c_engine_config {
+  a3c_net_desc net;
+  int num_envs;          /* E per GPU                                              */
+  int n_step;            /* rollout length n (a3c 5; q: train_frequency 32)          */
+  int env_id_base;       /* global id of this GPU's env 0 (rank * E)                 */
+  int world_size;        /* GPUs taking part (lr schedule counts their env-steps)    */
+  int start_lives;       /* 0 Pong, 5 Breakout, 3 SpaceInvaders                      */
+  int random_start;      /* config.py:7 (30)                                          */
+  int action_repeat;     /* config.py:50 (1)                                          */
+  int num_frames;        /* synthetic frame pool size (HBM resident RGB frames)       */
+  int use_graph;         /* capture the rollout+backward into a hipGraph              */
+  uint64_t seed;         /* main.py:336 random_seed (123)                             */
+  double gamma;          /* config.py:9 discount 0.99                                 */
+  float beta;            /* config.py:16 entropy weight 0.01                          */
+  float learning_rate;   /* config.py:11 7e-4                                          */
+  int64_t max_step;      /* config.py:5 8e7                                           */
+  float decay, momentum, epsilon;   /* main.py:64-65: 0.99, 0, 0.1                    */
+  float clip_norm;       /* agent.py:319: 40                                          */
+  int literal_adv;       /* 1: network.py literal un-stopped advantage gradient       */
+  /* q-learning only */
+  float ep_start, ep_end; int64_t ep_end_t, learn_start;  /* config.py:18-25         */
+  int64_t target_q_update_step;   /* config.py:10 (4e4)                               */
+  double discount;                /* config.py:9                                      */
+} a3c_engine_config;
+
+void a3c_engine_config_default(a3c_engine_config* cfg);
+int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out);
+int a3c_engine_destroy(a3c_engine* eng);
+/* fill the frame pool, reset the envs (new_random_game, environment.py:81-86), fill each
+ * history with 4 copies of the first screen (agent.py:37-38) and initialise params
+ * from host memory (nullable -> keep), rms slot = 1, mom = 0. */
+int a3c_engine_reset(a3c_engine* eng, const float* host_params, void* stream);
+/* n rollout steps + bootstrap + loss + backward + per-tensor clip -> grads */
+int a3c_engine_rollout_grad(a3c_engine* eng, void* stream);
+/* RMSProp apply of grads (lr from the device global step) and advance counters */
+int a3c_engine_apply(a3c_engine* eng, void* stream);
+
+/* device pointers owned by the engine (valid until destroy) */
+typedef struct a3c_engine_buffers {
+  float* params; float* target_params; float* ms; float* mom; float* grads;
+  int64_t n_params;
+  uint8_t* frame_ring;     /* [E][R][84*84] u8                                */
+  int ring_slots;
+  int64_t* tau;            /* device: current frame index tau                 */
+  int64_t* global_step;    /* device: env-steps taken by all GPUs             */
+  int32_t* actions;        /* [n][E]                                           */
+  float* rewards;          /* [n][E]                                           */
+  uint8_t* terminals;      /* [n][E]                                           */
+  float* z;                /* [(n+1)][E][zs] (row n = bootstrap forward)       */
+  float* returns;          /* [n][E] R or TD target                            */
+  float* loss;             /* [4]                                              */
+  float* sumsq;            /* [n_tensors] pre-clip squared norms               */
+  float* act_l1; float* act_l2; float* act_l3;  /* [n*E][...]                  */
+  uint8_t* frame_pool;     /* [num_frames][210][160][3]                        */
+  int32_t* env_frame; int32_t* env_lives; uint32_t* env_episode; uint32_t* env_step;
+  uint32_t* env_len;
+  int zs; int n_tensors; int64_t offsets[A3C_MAX_TENSORS]; int64_t sizes[A3C_MAX_TENSORS];
+} a3c_engine_buffers;
+int a3c_engine_get_buffers(a3c_engine* eng, a3c_engine_buffers* out);
+
+/* profiling hook: average device time (ms) of `iters` back-to-back launches of one engine
+ * kernel on its live buffers, bracketed by HIP events on `stream`.  A3C_KER_ENV_STEP
+ * advances the env state (use only after a measurement). */
+#define A3C_KER_CONV12_FWD 0   /* conv1+conv2 forward, B = E (saves conv1 out)          */
+#define A3C_KER_FC_FWD 1       /* fc 2592->256 forward GEMM (+split-K reduce), B = E     */
+#define A3C_KER_ENV_STEP 2     /* env step + Environment.screen into the frame ring      */
+#define A3C_KER_CONV_BWD 3     /* fused conv backward over B = n*E                       */
+int a3c_engine_time_kernel(a3c_engine* eng, int kernel, int iters, void* stream, float* avg_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* A3C_HIP_H */

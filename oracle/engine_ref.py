@@ -1,0 +1,161 @@
+"""CPU replay of one actor-learner iteration (TEST INFRASTRUCTURE ONLY; also bench.py's
+cpu_baseline leg).
+
+Restates, on the synthetic env, the batched form of the reference worker loop:
+  agent.py:52-67 (train: predict -> act -> observe -> new_random_game on terminal)
+  agent.py:141-151 predict (q) / network.py:461-468 + assets/a3c.png (a3c) action draw
+  agent.py:153-167 observe (reward clip, history add, update cadence, target sync)
+  agent.py:169-207 batch_update (TD target) / assets/a3c.png n-step returns (a3c)
+  agent.py:306-321 loss, per-tensor clip_by_norm(40), RMSProp apply (main.py:63-65)
+with E envs in lock-step, the history kept as a ring of frames (history.py:13-24 order).
+"""
+import numpy as np
+
+from . import philox as px
+from . import ref_cpu as R
+from .synthetic_env import SyntheticAtari, pool_frame
+
+EP_END_CHOICES = np.array([0.1, 0.01, 0.5], np.float32)   # main.py:369
+
+
+class EngineRef:
+    def __init__(self, params, num_envs, n_step, action_size, algo='a3c', start_lives=0, num_frames=64,
+                 seed=123, env_id_base=0, world_size=1, random_start=30, action_repeat=1,
+                 gamma=0.99, beta=0.01, learning_rate=0.0007, max_step=80_000_000, decay=0.99,
+                 momentum=0.0, epsilon=0.1, clip_norm=40.0, literal_adv=False, ep_start=1.0,
+                 ep_end_t=4_000_000, learn_start=32, target_q_update_step=40_000, discount=0.99,
+                 dtype=np.float64):
+        self.algo, self.A, self.E, self.n = algo, int(action_size), int(num_envs), int(n_step)
+        self.seed = int(seed)
+        self.k0, self.k1 = px.seed_key(seed)
+        self.env = SyntheticAtari(seed, num_envs, num_frames, action_size, start_lives, random_start,
+                                  action_repeat, env_id_base)
+        self.ids = self.env.ids
+        self.world = int(world_size)
+        self.R = self.n + 4 + (1 if algo == 'q' else 0)
+        self.ring = np.zeros((self.E, self.R, 84, 84), np.uint8)
+        self.tau, self.global_step = 3, 0
+        self.params = {k: np.array(v, np.float32) for k, v in params.items()}
+        self.tparams = {k: v.copy() for k, v in self.params.items()}
+        self.ms = {k: np.ones_like(v) for k, v in self.params.items()}      # TF1 rms slot = 1
+        self.mom = {k: np.zeros_like(v) for k, v in self.params.items()}
+        self.h = dict(gamma=gamma, beta=beta, learning_rate=learning_rate, max_step=max_step, decay=decay,
+                      momentum=momentum, epsilon=epsilon, clip_norm=clip_norm, literal_adv=literal_adv,
+                      ep_start=ep_start, ep_end_t=ep_end_t, learn_start=learn_start,
+                      target_q_update_step=target_q_update_step, discount=discount)
+        self.dtype = dtype
+        x0 = px.philox4x32(self.ids, 0, 0, 11, self.k0, self.k1)[0]
+        self.ep_end = EP_END_CHOICES[x0 % 3]
+        self._screens = {}
+        self.cache_screens = True      # the fixed pool makes screens cacheable; bench turns it off
+
+    # ---- screens of pool frames (cached: the pool is a fixed set) --------------------
+    def screen_of(self, f):
+        f = int(f)
+        if not self.cache_screens:
+            return R.screen(pool_frame(self.seed, f))
+        if f not in self._screens:
+            self._screens[f] = R.screen(pool_frame(self.seed, f))
+        return self._screens[f]
+
+    def reset(self):
+        self.env.new_random_game()
+        for e in range(self.E):
+            s = self.screen_of(self.env.frame[e])
+            for c in range(4):
+                self.ring[e, c % self.R] = s
+        self.tau, self.global_step = 3, 0
+
+    def states(self, tau):
+        """[E,84,84,4] NHWC u8 state s_tau (frames tau-3..tau)."""
+        slots = [(tau - 3 + c) % self.R for c in range(4)]
+        return np.ascontiguousarray(np.transpose(self.ring[:, slots], (0, 2, 3, 1)))
+
+    def _draw(self, z, t):
+        tau = self.tau + t
+        x = px.philox4x32(np.uint32(tau & 0xFFFFFFFF), np.uint32(tau >> 32), self.ids, px.P_ACTION,
+                          self.k0, self.k1)
+        if self.algo == 'a3c':
+            pi, _, _ = R.softmax_stats(z[:, :self.A])
+            return R.sample_categorical(pi.astype(np.float32), px.u01(x[0])), pi
+        eps = self.eps()
+        q = z[:, :self.A].astype(np.float32)
+        greedy = np.argmax(q, axis=1).astype(np.int32)
+        rnd = (x[1] % np.uint32(self.A)).astype(np.int32)
+        return np.where(px.u01(x[0]) < eps, rnd, greedy).astype(np.int32), None
+
+    def eps(self):
+        h = self.h
+        step = float(self.global_step)
+        d = float(h['ep_end_t']) - max(0.0, step - float(h['learn_start']))
+        ee = self.ep_end.astype(np.float64)
+        return (ee + np.maximum(0.0, (float(h['ep_start']) - ee) * d / float(h['ep_end_t']))).astype(np.float32)
+
+    def iterate(self, forced_actions=None):
+        """One iteration; returns a dict of everything the GPU engine exposes."""
+        E, n, A, h = self.E, self.n, self.A, self.h
+        acts = np.zeros((n, E), np.int32)
+        sampled = np.zeros((n, E), np.int32)
+        rewards = np.zeros((n, E), np.float32)
+        terms = np.zeros((n, E), np.uint8)
+        zs, pis, frames = [], [], []
+        for t in range(n):
+            st = self.states(self.tau + t)
+            z = R.forward(self.params, st, self.algo, dtype=self.dtype, keep=False)['z']
+            a, pi = self._draw(z, t)
+            sampled[t] = a
+            acts[t] = a if forced_actions is None else forced_actions[t]
+            zs.append(z)
+            pis.append(pi)
+            frame, reward, term = self.env.act(acts[t], is_training=True)
+            rewards[t] = np.clip(reward, -1.0, 1.0)                      # agent.py:154
+            terms[t] = term
+            frames.append(frame.copy())
+            for e in range(E):
+                self.ring[e, (self.tau + t + 1) % self.R] = self.screen_of(frame[e])
+            if term.any():
+                self.env.new_random_game(term.astype(bool))
+        states = np.concatenate([self.states(self.tau + t) for t in range(n)])      # b = t*E + e
+        B = n * E
+        out = dict(actions=acts, sampled=sampled, rewards=rewards, terminals=terms, z=np.stack(zs),
+                   pi=pis, frames=np.stack(frames))
+        if self.algo == 'a3c':
+            zb = R.forward(self.params, self.states(self.tau + n), 'a3c', dtype=self.dtype, keep=False)['z']
+            Rt = R.nstep_returns(rewards, terms, zb[:, A].astype(np.float32), h['gamma'])
+            target = Rt.astype(np.float32)
+            out['bootstrap_z'] = zb
+        else:
+            nxt = np.concatenate([self.states(self.tau + t + 1) for t in range(n)])
+            qn = R.forward(self.tparams, nxt, 'q', dtype=self.dtype, keep=False)['z']
+            target = R.td_target(rewards.reshape(-1), terms.reshape(-1), qn.astype(np.float32),
+                                 h['discount']).astype(np.float32)
+        out['target'] = target.reshape(n, E)
+        fwd = R.forward(self.params, states, self.algo, dtype=self.dtype)
+        flat_acts = acts.reshape(-1)
+        if self.algo == 'a3c':
+            losses, dz = R.a3c_loss_and_dz(fwd['z'], flat_acts, target.reshape(-1).astype(self.dtype),
+                                           h['beta'], h['literal_adv'])
+        else:
+            loss, dz = R.q_loss_and_dz(fwd['z'], flat_acts, target.reshape(-1).astype(self.dtype))
+            losses = dict(loss=loss, q_mean=fwd['z'][np.arange(B), flat_acts].mean())
+        g = R.backward(self.params, fwd, dz, self.algo)
+        grads = {k: np.asarray(v, np.float32).reshape(self.params[k].shape) for k, v in g.items()}
+        sumsq = {k: np.float32(np.sum(v.astype(np.float64) ** 2)) for k, v in grads.items()}
+        clipped = {k: R.clip_by_norm(v, h['clip_norm']) for k, v in grads.items()}
+        out.update(losses=losses, grads=grads, sumsq=sumsq, clipped=clipped, z_batch=fwd['z'])
+        return out
+
+    def apply(self, clipped):
+        h = self.h
+        inc = self.n * self.E * self.world
+        lr = R.learning_rate(self.global_step + inc, h['max_step'], h['learning_rate'])
+        for k in self.params:
+            R.rmsprop_apply(self.params[k], self.ms[k], self.mom[k], clipped[k].astype(np.float32), lr,
+                            h['decay'], h['momentum'], h['epsilon'])
+        if self.algo == 'q':
+            P = h['target_q_update_step']
+            if (self.global_step + inc + 1) // P != (self.global_step + 1) // P:   # agent.py:166-167
+                self.tparams = {k: v.copy() for k, v in self.params.items()}
+        self.tau += self.n
+        self.global_step += inc
+        return lr
