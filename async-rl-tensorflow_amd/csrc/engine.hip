@@ -20,6 +20,7 @@
 #include "gemm.h"
 
 void a3c_init_once();
+int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s);
 
 struct a3c_engine {
   a3c_engine_config cfg;
@@ -34,6 +35,7 @@ struct a3c_engine {
   EnvBufs env;
   EnvParams envp;
   int32_t* actions;
+  int32_t* frames;         // [n][E] post-act frame index per step
   float* rewards;
   uint8_t* terms;
   float* z;
@@ -49,6 +51,7 @@ struct a3c_engine {
   float* fslab_e; int fsplit_e;
   float* fslab_b; int fsplit_b;
   double* opt_part;
+  float* sched;            // [0] lr, [1] target-sync flag (device)
   TensorTab tt;
   hipGraph_t graph;
   hipGraphExec_t gexec;
@@ -142,14 +145,15 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   ALLOC(e->ring, (int64_t)E * e->R * PLANE);
   ALLOC(e->pool, (int64_t)cfg->num_frames * SCREEN_H * SCREEN_W * 3);
   ALLOC(e->counters, 64);
-  ALLOC(e->env.episode, E * 4);
-  ALLOC(e->env.ep_step, E * 4);
-  ALLOC(e->env.ep_len, E * 4);
-  ALLOC(e->env.lives, E * 4);
-  ALLOC(e->env.frame, E * 4);
-  ALLOC(e->env.reward, E * 4);
-  ALLOC(e->env.terminal, E);
+  ALLOC(e->env.episode, 2 * E * 4);
+  ALLOC(e->env.ep_step, 2 * E * 4);
+  ALLOC(e->env.ep_len, 2 * E * 4);
+  ALLOC(e->env.lives, 2 * E * 4);
+  ALLOC(e->env.frame, 2 * E * 4);
+  ALLOC(e->env.reward, 2 * E * 4);
+  ALLOC(e->env.terminal, 2 * E);
   ALLOC(e->actions, nE * 4);
+  ALLOC(e->frames, nE * 4);
   ALLOC(e->rewards, nE * 4);
   ALLOC(e->terms, nE);
   ALLOC(e->z, (nE + E) * zs * 4);
@@ -171,10 +175,13 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   ALLOC(e->fslab_e, f1 * 4);
   int64_t f2 = a3c_fwd_slab_floats(scrB, &e->fsplit_b);
   ALLOC(e->fslab_b, f2 * 4);
-  ALLOC(e->opt_part, (int64_t)A3C_MAX_TENSORS * SS_BLOCKS * 8);
+  ALLOC(e->opt_part, (int64_t)SS_MAX_BLOCKS * 8);
+  ALLOC(e->sched, 64);
 #undef ALLOC
-  e->tt.n = L.nt;
-  for (int i = 0; i < L.nt; ++i) { e->tt.off[i] = L.off[i]; e->tt.size[i] = L.size[i]; }
+  if (a3c_make_tab(L.nt, L.off, L.size, L.total, &e->tt)) {
+    a3c_engine_destroy(e);
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "tensor table");
+  }
   e->envp.k0 = e->k0; e->envp.k1 = e->k1;
   e->envp.P = cfg->num_frames;
   e->envp.A = L.A;
@@ -211,22 +218,6 @@ __global__ void k_eps(float* __restrict__ eps, const float* __restrict__ ep_end,
   eps[i] = (float)v;
 }
 
-__global__ void k_advance(int64_t* __restrict__ counters, int64_t dtau, int64_t dstep) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    counters[0] += dtau;
-    counters[1] += dstep;
-  }
-}
-
-// target-network sync when the global step passes T with T % P == P-1 (agent.py:165-167)
-__global__ void k_maybe_copy(float* __restrict__ dst, const float* __restrict__ src, int64_t n,
-                             const int64_t* __restrict__ counters, int64_t inc, int64_t period) {
-  const int64_t g0 = counters[1];
-  if ((g0 + inc + 1) / period == (g0 + 1) / period) return;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    dst[i] = src[i];
-}
-
 static StateAddr ring_addr(const a3c_engine* e, int tau_offset) {
   StateAddr sa;
   sa.base = e->ring;
@@ -238,6 +229,25 @@ static StateAddr ring_addr(const a3c_engine* e, int tau_offset) {
   sa.tau_offset = tau_offset;
   sa.tau_ptr = e->counters;
   return sa;
+}
+
+static OptParams opt_params(const a3c_engine* e) {
+  const a3c_engine_config& c = e->cfg;
+  OptParams op = {};
+  op.clip = c.clip_norm;
+  op.sched = e->sched;
+  op.step_ptr = e->counters + 1;
+  op.step_add = e->nE * c.world_size;
+  op.lr0 = c.learning_rate;
+  op.max_step = c.max_step;
+  op.target_period = e->L.algo == A3C_ALGO_Q ? c.target_q_update_step : 0;
+  op.target = e->L.algo == A3C_ALGO_Q ? e->tparams : nullptr;
+  op.counters = e->counters;
+  op.dtau = e->n;
+  op.rho = c.decay;
+  op.momentum = c.momentum;
+  op.eps = c.epsilon;
+  return op;
 }
 
 static int enqueue_rollout_grad(a3c_engine* e, hipStream_t s) {
@@ -260,11 +270,16 @@ static int enqueue_rollout_grad(a3c_engine* e, hipStream_t s) {
     sel.eps = e->eps;
     sel.actions = e->actions + (int64_t)t * E;
     const int64_t o = (int64_t)t * E;
+    sel.env_on = 1;
+    sel.envp = e->envp;
+    sel.envb = e->env;
+    sel.rewards = e->rewards + o;
+    sel.terms = e->terms + o;
+    sel.frames_out = e->frames + o;
     rc = a3c_forward_launch(L, e->params, ring_addr(e, t), E, e->act_l1 + o * C1_P * C1_N, e->act_l2 + o * FLAT,
                             e->act_l3 + o * FC, e->z + o * zs, e->fslab_e, e->fsplit_e, sel, s);
     if (rc) return rc;
-    rc = a3c_env_step_launch(e->envp, e->env, E, e->actions + o, e->rewards + o, e->terms + o, -1.0f, 1.0f,
-                             e->pool, e->ring, e->R, e->counters, t, s);
+    rc = a3c_env_screen_launch(E, e->frames + o, e->pool, e->ring, e->R, e->counters, t, s);
     if (rc) return rc;
   }
   HeadSelect none = {};
@@ -275,8 +290,6 @@ static int enqueue_rollout_grad(a3c_engine* e, hipStream_t s) {
     rc = a3c_forward_launch(L, e->params, ring_addr(e, n), E, nullptr, e->scr_l2, e->scr_l3, e->z + e->nE * zs,
                             e->fslab_e, e->fsplit_e, none, s);
     if (rc) return rc;
-    rc = a3c_returns_launch(e->rewards, e->terms, e->z + e->nE * zs + L.A, zs, n, E, c.gamma, e->R_buf, s);
-    if (rc) return rc;
   } else {
     // target network on s_{t+1} for every transition (agent.py:186)
     none.E = E;
@@ -286,14 +299,24 @@ static int enqueue_rollout_grad(a3c_engine* e, hipStream_t s) {
     rc = a3c_td_target_launch(e->rewards, e->terms, e->zt, e->nE, L.A, zs, c.discount, e->R_buf, s);
     if (rc) return rc;
   }
+  ReturnsArgs ra = {};
+  if (!q) {   // n-step returns computed inside the head backward (assets/a3c.png)
+    ra.rewards = e->rewards; ra.terms = e->terms; ra.boot = e->z + e->nE * zs + L.A; ra.boot_stride = zs;
+    ra.n = n; ra.E = E; ra.gamma = c.gamma; ra.R_out = e->R_buf;
+  }
   rc = a3c_backward_launch(L, e->params, ring_addr(e, 0), e->nE, e->act_l1, e->act_l2, e->act_l3, e->z,
-                           e->actions, e->R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s);
+                           e->actions, e->R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra);
   if (rc) return rc;
-  // per-tensor clip of this worker's gradient (agent.py:319) -- before any cross-GPU exchange
-  OptParams op = {};
-  op.mode = OPT_CLIP;
-  op.clip = c.clip_norm;
-  return a3c_optim_launch(nullptr, nullptr, nullptr, e->grads, e->tt, op, e->opt_part, e->sumsq, true, s);
+  // per-tensor squared norms (+ lr / target-sync schedule from the device step counter)
+  OptParams op = opt_params(e);
+  rc = a3c_sumsq_launch(e->grads, e->tt, op, e->opt_part, s);
+  if (rc) return rc;
+  if (c.world_size > 1) {
+    // multi-GPU: clip this worker's gradient (agent.py:319) before the cross-GPU exchange
+    op.mode = OPT_CLIP;
+    return a3c_apply_launch(nullptr, nullptr, nullptr, e->grads, e->tt, op, e->opt_part, e->sumsq, s);
+  }
+  return 0;
 }
 
 extern "C" int a3c_engine_reset(a3c_engine* e, const float* host_params, void* stream) {
@@ -346,31 +369,15 @@ extern "C" int a3c_engine_rollout_grad(a3c_engine* e, void* stream) {
   return 0;
 }
 
+// RMSProp apply (lr from the schedule computed on device), target sync (q) and the counter
+// advance, all in one launch.  world_size == 1: the per-tensor clip is applied here as well.
 extern "C" int a3c_engine_apply(a3c_engine* e, void* stream) {
   if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_apply", "null");
   hipStream_t s = (hipStream_t)stream;
-  const a3c_engine_config& c = e->cfg;
-  const int64_t inc = e->nE * c.world_size;
-  OptParams op = {};
-  op.mode = OPT_APPLY;
-  op.clip = 0.f;
-  op.step_ptr = e->counters + 1;
-  op.step_add = inc;
-  op.lr0 = c.learning_rate;
-  op.max_step = c.max_step;
-  op.rho = c.decay;
-  op.momentum = c.momentum;
-  op.eps = c.epsilon;
-  int rc = a3c_optim_launch(e->params, e->ms, e->mom, e->grads, e->tt, op, e->opt_part, nullptr, false, s);
-  if (rc) return rc;
-  if (e->L.algo == A3C_ALGO_Q) {
-    hipLaunchKernelGGL(k_maybe_copy, dim3(256), dim3(256), 0, s, e->tparams, e->params, e->L.total, e->counters,
-                       inc, c.target_q_update_step);
-    A3C_CHECK(hipGetLastError());
-  }
-  hipLaunchKernelGGL(k_advance, dim3(1), dim3(64), 0, s, e->counters, (int64_t)e->n, inc);
-  A3C_CHECK(hipGetLastError());
-  return 0;
+  OptParams op = opt_params(e);
+  op.mode = e->cfg.world_size > 1 ? OPT_APPLY : (OPT_CLIP | OPT_APPLY);
+  return a3c_apply_launch(e->params, e->ms, e->mom, e->grads, e->tt, op, e->opt_part,
+                          e->cfg.world_size > 1 ? nullptr : e->sumsq, s);
 }
 
 extern "C" int a3c_engine_get_buffers(a3c_engine* e, a3c_engine_buffers* b) {
@@ -402,16 +409,10 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
     switch (kernel) {
       case A3C_KER_CONV12_FWD:
         return a3c_conv12_launch(L, e->params, ring_addr(e, 0), E, e->act_l1, e->act_l2, s);
-      case A3C_KER_FC_FWD: {
-        GemmArgs g = {};
-        g.A = e->act_l2; g.lda = FLAT; g.B = e->params + L.off[T_FCW]; g.ldb = FC; g.C = e->act_l3; g.ldc = FC;
-        g.M = E; g.N = FC; g.K = FLAT; g.epi = EPI_BIAS_RELU; g.bias = e->params + L.off[T_FCB];
-        g.slab = e->fslab_e; g.nsplit = e->fsplit_e;
-        return a3c_gemm(true, true, g, s);
-      }
+      case A3C_KER_FC_FWD:
+        return a3c_fc_fwd_launch(e->act_l2, e->params + L.off[T_FCW], e->params + L.off[T_FCB], e->act_l3, E, s);
       case A3C_KER_ENV_STEP:
-        return a3c_env_step_launch(e->envp, e->env, E, e->actions, e->rewards, e->terms, -1.0f, 1.0f, e->pool,
-                                   e->ring, e->R, e->counters, 0, s);
+        return a3c_env_screen_launch(E, e->frames, e->pool, e->ring, e->R, e->counters, 0, s);
       case A3C_KER_CONV_BWD: {
         const BwdPlan p = a3c_bwd_plan(L, e->nE);
         return a3c_conv_bwd_launch(L, e->params, ring_addr(e, 0), e->nE, e->act_l1, e->ws + p.dl2, e->ws, s);

@@ -60,6 +60,21 @@ inline int a3c_make_layout(const a3c_net_desc* d, NetLayout* L) {
   return 0;
 }
 
+struct EnvParams {
+  uint32_t k0, k1;
+  int P, A, L0, random_start, action_repeat, env_id_base;
+};
+
+struct EnvBufs {
+  uint32_t* episode;
+  uint32_t* ep_step;
+  uint32_t* ep_len;
+  int32_t* lives;
+  int32_t* frame;
+  float* reward;
+  uint8_t* terminal;
+};
+
 struct HeadSelect {
   int mode;                 // -1 none, 0 categorical (a3c), 1 epsilon-greedy argmax (q)
   uint32_t k0, k1;          // philox key (seed)
@@ -70,6 +85,14 @@ struct HeadSelect {
   int E;
   const float* eps;         // mode 1: per env (index b % E)
   int32_t* actions;         // [B]
+  // fused env step (engine rollout): act() on the drawn action right after predict, as the
+  // reference worker does (agent.py:59-62); env state double-buffered by (tau & 1)
+  int env_on;
+  EnvParams envp;
+  EnvBufs envb;
+  float* rewards;           // [E] observe-clipped reward (agent.py:154)
+  uint8_t* terms;           // [E]
+  int32_t* frames_out;      // [E] post-act frame index (the screen the history gets)
 };
 
 // forward of B states; returns 0 or error

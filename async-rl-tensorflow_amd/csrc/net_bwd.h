@@ -24,15 +24,28 @@ struct FinalizeSegs {
 };
 
 struct BwdPlan {
-  int nwg, per_wg, head_split, fc_split;
-  int64_t dz, dh3, dl2, terms, hgrad, hcol, hslab, fccol, fcslab, cslab, total;  // float offsets
+  int nwg, per_wg, head_split, fc_split, groups;
+  int64_t dz, dh3, dl2, terms, hgrad, hcol, hslab, fccol, fcslab, cslab, cgroup, total;  // float offsets
+};
+
+// optional fused n-step returns in the head backward (engine a3c path)
+struct ReturnsArgs {
+  const float* rewards;      // [n][E] (nullptr: use the explicit target array)
+  const uint8_t* terms;      // [n][E]
+  const float* boot;         // V(s_{t+n}) at boot[e * boot_stride]
+  int64_t boot_stride;
+  int n;
+  int64_t E;
+  double gamma;
+  float* R_out;              // [n*E] the returns (inspection)
 };
 
 BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B);
 int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
                         const float* act_l1, const float* act_l2, const float* act_l3,
                         const float* z, const int32_t* actions, const float* target, float beta,
-                        int literal, float* grads, float* loss_out, float* ws, hipStream_t s);
+                        int literal, float* grads, float* loss_out, float* ws, hipStream_t s,
+                        const ReturnsArgs* ra = nullptr);
 int a3c_returns_launch(const float* rewards, const uint8_t* terms, const float* boot, int64_t boot_stride,
                        int n, int64_t E, double gamma, float* R, hipStream_t s);
 int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float* qn, int64_t B, int A,

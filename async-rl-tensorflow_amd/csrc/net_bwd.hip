@@ -52,13 +52,27 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ z, i
                                                   const float* __restrict__ Wv, float beta,
                                                   int literal, float invB, int64_t B,
                                                   float* __restrict__ dz, float* __restrict__ dh3,
-                                                  float* __restrict__ terms) {
+                                                  float* __restrict__ terms, ReturnsArgs ra) {
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
   const float myz = lane < zs ? z[b * zs + lane] : 0.f;
   const int a = actions[b];
-  const float tgt = target[b];
+  float tgt;
+  if (ra.rewards) {
+    // n-step return of sample (t, e) (assets/a3c.png), float64 like k_returns
+#pragma clang fp contract(off)
+    const int64_t t = b / ra.E, e = b - t * ra.E;
+    double r = (double)ra.boot[e * ra.boot_stride];
+    for (int64_t i = ra.n - 1; i >= t; --i) {
+      if (ra.terms[i * ra.E + e]) r = 0.0;
+      r = (double)ra.rewards[i * ra.E + e] + ra.gamma * r;
+    }
+    tgt = (float)r;
+    if (lane == 0) ra.R_out[b] = tgt;
+  } else {
+    tgt = target[b];
+  }
   float mydz = 0.f, dV = 0.f;
   if (algo == A3C_ALGO_A3C) {
     float l = lane < A ? myz : -INFINITY;
@@ -284,20 +298,19 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
 // ---------------------------------------------------------------------------------------
 // deterministic slab reductions into the flat gradient vector
 // ---------------------------------------------------------------------------------------
-__global__ void k_finalize(FinalizeSegs fs) {
-  const FinalizeSeg sg = fs.s[blockIdx.y];
-  const int64_t n = (int64_t)sg.rows * sg.ncols;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int r = (int)(i / sg.ncols), c = (int)(i - (int64_t)r * sg.ncols);
-    const float* src = sg.src + (int64_t)r * sg.src_ld + sg.col0 + c;
-    float v = 0.f;
-    for (int s = 0; s < sg.nsplit; ++s) v += src[(int64_t)s * sg.split_stride];
-    fs.dst[sg.dst_off + (int64_t)r * sg.dst_ld + c] = v * sg.scale;
-  }
+// pass 1 of the conv-slab reduction: dst[g][i] = sum of slabs s in group g (fixed order)
+__global__ void __launch_bounds__(256) k_slab_group(const float* __restrict__ src, int nsplit, int per,
+                                                    int64_t len, float* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= len) return;
+  const int g = blockIdx.y;
+  const int s0 = g * per, s1 = min(nsplit, s0 + per);
+  float v = 0.f;
+  for (int s = s0; s < s1; ++s) v += src[(int64_t)s * len + i];
+  dst[(int64_t)g * len + i] = v;
 }
 
-__global__ void __launch_bounds__(256) k_loss_reduce(const float* __restrict__ terms, int64_t B,
-                                                     float* __restrict__ out) {
+__device__ void loss_reduce_block(const float* __restrict__ terms, int64_t B, float* __restrict__ out) {
   __shared__ double red[4][256];
   double s[4] = {0, 0, 0, 0};
   for (int64_t b = threadIdx.x; b < B; b += 256)
@@ -313,6 +326,24 @@ __global__ void __launch_bounds__(256) k_loss_reduce(const float* __restrict__ t
     __syncthreads();
   }
   if (threadIdx.x < 4) out[threadIdx.x] = (float)red[threadIdx.x][0];
+}
+
+// pass 2 + small segments; block row fs.n (x == 0) reduces the per-sample loss terms
+__global__ void __launch_bounds__(256) k_finalize(FinalizeSegs fs, const float* __restrict__ terms, int64_t B,
+                                                  float* __restrict__ loss_out) {
+  if ((int)blockIdx.y == fs.n) {
+    if (blockIdx.x == 0 && loss_out) loss_reduce_block(terms, B, loss_out);
+    return;
+  }
+  const FinalizeSeg sg = fs.s[blockIdx.y];
+  const int64_t n = (int64_t)sg.rows * sg.ncols;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / sg.ncols), c = (int)(i - (int64_t)r * sg.ncols);
+    const float* src = sg.src + (int64_t)r * sg.src_ld + sg.col0 + c;
+    float v = 0.f;
+    for (int s = 0; s < sg.nsplit; ++s) v += src[(int64_t)s * sg.split_stride];
+    fs.dst[sg.dst_off + (int64_t)r * sg.dst_ld + c] = v * sg.scale;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -338,6 +369,8 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   p.fccol = take((int64_t)p.fc_split * FC);
   p.fcslab = take(p.fc_split > 1 ? (int64_t)p.fc_split * FLAT * FC : 0);
   p.cslab = take((int64_t)p.nwg * CB_SLAB);
+  p.groups = p.nwg < 16 ? p.nwg : 16;
+  p.cgroup = take((int64_t)p.groups * CB_SLAB);
   p.total = o;
   return p;
 }
@@ -345,7 +378,10 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
 int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
                         const float* act_l1, const float* act_l2, const float* act_l3,
                         const float* z, const int32_t* actions, const float* target, float beta,
-                        int literal, float* grads, float* loss_out, float* ws, hipStream_t s) {
+                        int literal, float* grads, float* loss_out, float* ws, hipStream_t s,
+                        const ReturnsArgs* ra_in) {
+  ReturnsArgs ra = {};
+  if (ra_in) ra = *ra_in;
   if (B <= 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "B must be > 0");
   const BwdPlan p = a3c_bwd_plan(L, B);
   const float* P = params;
@@ -357,7 +393,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
 
   hipLaunchKernelGGL(k_head_bwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, z, L.zs, L.A, L.algo,
                      actions, target, act_l3, P + L.off[T_HW], a3c ? P + L.off[T_VW] : nullptr, beta,
-                     literal, 1.0f / (float)B, B, dz, dh3, terms);
+                     literal, 1.0f / (float)B, B, dz, dh3, terms, ra);
   A3C_CHECK(hipGetLastError());
 
   // head weights: dWh[256][zs] = l3^T dz ; dbh = colsum(dz)
@@ -401,11 +437,16 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     q.src = src; q.split_stride = stride; q.nsplit = nsplit; q.rows = rows; q.src_ld = src_ld;
     q.col0 = col0; q.ncols = ncols; q.dst_off = dst_off; q.dst_ld = dst_ld; q.scale = scale;
   };
-  const float* cs = ws + p.cslab;
-  seg(cs + CB_OFF_W1, CB_SLAB, p.nwg, 1, 0, 0, KC1 * C1_N, L.off[T_L1W], 0, 1.0f / 255.0f);
-  seg(cs + CB_OFF_B1, CB_SLAB, p.nwg, 1, 0, 0, C1_N, L.off[T_L1B], 0, 1.0f);
-  seg(cs + CB_OFF_W2, CB_SLAB, p.nwg, 1, 0, 0, KC2 * C2_N, L.off[T_L2W], 0, 1.0f);
-  seg(cs + CB_OFF_B2, CB_SLAB, p.nwg, 1, 0, 0, C2_N, L.off[T_L2B], 0, 1.0f);
+  // conv slabs: nwg partials -> p.groups partials (pass 1), folded by k_finalize (pass 2)
+  const int per = (p.nwg + p.groups - 1) / p.groups;
+  hipLaunchKernelGGL(k_slab_group, dim3((CB_SLAB + 255) / 256, p.groups), dim3(256), 0, s, ws + p.cslab, p.nwg, per,
+                     (int64_t)CB_SLAB, ws + p.cgroup);
+  A3C_CHECK(hipGetLastError());
+  const float* cs = ws + p.cgroup;
+  seg(cs + CB_OFF_W1, CB_SLAB, p.groups, 1, 0, 0, KC1 * C1_N, L.off[T_L1W], 0, 1.0f / 255.0f);
+  seg(cs + CB_OFF_B1, CB_SLAB, p.groups, 1, 0, 0, C1_N, L.off[T_L1B], 0, 1.0f);
+  seg(cs + CB_OFF_W2, CB_SLAB, p.groups, 1, 0, 0, KC2 * C2_N, L.off[T_L2W], 0, 1.0f);
+  seg(cs + CB_OFF_B2, CB_SLAB, p.groups, 1, 0, 0, C2_N, L.off[T_L2B], 0, 1.0f);
   seg(ws + p.fccol, FC, p.fc_split, 1, 0, 0, FC, L.off[T_FCB], 0, 1.0f);
   seg(ws + p.hgrad, 0, 1, FC, L.zs, 0, L.A, L.off[T_HW], L.A, 1.0f);
   seg(ws + p.hcol, L.zs, p.head_split, 1, 0, 0, L.A, L.off[T_HB], 0, 1.0f);
@@ -413,12 +454,8 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     seg(ws + p.hgrad, 0, 1, FC, L.zs, L.A, 1, L.off[T_VW], 1, 1.0f);
     seg(ws + p.hcol, L.zs, p.head_split, 1, 0, L.A, 1, L.off[T_VB], 0, 1.0f);
   }
-  hipLaunchKernelGGL(k_finalize, dim3(32, fs.n), dim3(256), 0, s, fs);
+  hipLaunchKernelGGL(k_finalize, dim3(32, fs.n + 1), dim3(256), 0, s, fs, terms, B, loss_out);
   A3C_CHECK(hipGetLastError());
-  if (loss_out) {
-    hipLaunchKernelGGL(k_loss_reduce, dim3(1), dim3(256), 0, s, terms, B, loss_out);
-    A3C_CHECK(hipGetLastError());
-  }
   return 0;
 }
 

@@ -14,6 +14,7 @@
 #include "net.h"
 #include "gemm.h"
 #include "net_bwd.h"
+#include "env_dev.h"
 
 #define X8_BYTES (HIST * PLANE)                      // 28224
 #define L1S_BYTES (C1_P * L1S_LD * 4)                // 32000
@@ -156,8 +157,31 @@ __global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, 
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
-  f32x4 h = *(const f32x4*)(h3 + b * FC + 4 * lane);
   float myz = 0.f;
+  const int nout = A + (Wv ? 1 : 0);
+  if (nout <= 8) {
+    // lane = (output o = lane & 7, chunk c = lane >> 3 of 32 features): 8 outputs at once,
+    // then a 3-step butterfly over the 8 chunks
+    const int o = lane & 7, c = lane >> 3;
+    const float* hp = h3 + b * FC + 32 * c;
+    float p = 0.f;
+    if (o < nout) {
+      const bool val = o == A;
+      const float* w = val ? Wv + 32 * c : Wp + (int64_t)(32 * c) * A + o;
+      const int st = val ? 1 : A;
+#pragma unroll 8
+      for (int k = 0; k < 32; ++k) p += hp[k] * w[k * st];
+    }
+    p += __shfl_xor(p, 8, 64);
+    p += __shfl_xor(p, 16, 64);
+    p += __shfl_xor(p, 32, 64);
+    // lane j (< 8) now holds output j in lane j (c == 0 lanes)
+    const float zj = __shfl(p, lane & 7, 64);
+    if (lane < A) myz = zj + bp[lane];
+    else if (Wv && lane == A) myz = zj + bv[0];
+    if (lane < zs) z[b * zs + lane] = myz;
+  } else {
+  f32x4 h = *(const f32x4*)(h3 + b * FC + 4 * lane);
   for (int j = 0; j < A; ++j) {
     const float* w = Wp + (int64_t)(4 * lane) * A + j;
     float p = h[0] * w[0] + h[1] * w[A] + h[2] * w[2 * A] + h[3] * w[3 * A];
@@ -170,9 +194,25 @@ __global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, 
     if (lane == A) myz = p + bv[0];
   }
   if (lane < zs) z[b * zs + lane] = myz;   // padding columns are 0
+  }
   if (sel.mode >= 0) {
     int32_t a = select_from_lanes(myz, lane, A, sel, b);
-    if (lane == 0) sel.actions[b] = a;
+    if (lane == 0) {
+      sel.actions[b] = a;
+      if (sel.env_on) {
+        const int64_t tau = *sel.tau_ptr + sel.tau_add;
+        const int e = (int)b;
+        const int64_t cur = (tau & 1) * (int64_t)sel.E + e, nxt = ((tau + 1) & 1) * (int64_t)sel.E + e;
+        const uint32_t id = (uint32_t)(sel.env_id_base + e);
+        EnvState s = env_load(sel.envb, cur);
+        env_act(s, sel.envp, id, (uint32_t)a, true);
+        sel.rewards[e] = fmaxf(-1.0f, fminf(1.0f, s.reward));   // observe clip, agent.py:154
+        sel.terms[e] = (uint8_t)s.terminal;
+        sel.frames_out[e] = s.frame;
+        if (s.terminal) env_new_random_game(s, sel.envp, id);    // agent.py:66-67
+        env_store(sel.envb, nxt, s);
+      }
+    }
   }
 }
 
@@ -193,6 +233,8 @@ int64_t a3c_fwd_slab_floats(int64_t B, int* split_out) {
   return split > 1 ? (int64_t)split * B * FC : 0;
 }
 
+int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s);
+
 int a3c_forward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
                        float* act_l1, float* act_l2, float* act_l3, float* z, float* slab,
                        int fc_split, const HeadSelect& sel, hipStream_t s) {
@@ -200,14 +242,7 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const StateAddr&
   const float* P = params;
   int rc0 = a3c_conv12_launch(L, P, sa, B, act_l1, act_l2, s);
   if (rc0) return rc0;
-  GemmArgs g = {};
-  g.A = act_l2; g.lda = FLAT;
-  g.B = P + L.off[T_FCW]; g.ldb = FC;
-  g.C = act_l3; g.ldc = FC;
-  g.M = (int)B; g.N = FC; g.K = FLAT;
-  g.epi = EPI_BIAS_RELU; g.bias = P + L.off[T_FCB];
-  g.slab = slab; g.nsplit = fc_split;
-  int rc = a3c_gemm(true, true, g, s);
+  int rc = a3c_fc_fwd_launch(act_l2, P + L.off[T_FCW], P + L.off[T_FCB], act_l3, B, s);
   if (rc) return rc;
   const float* Wv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VW] : nullptr;
   const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
@@ -239,4 +274,79 @@ int a3c_select_launch(const float* z, int64_t B, int zs, int A, const HeadSelect
 void a3c_conv12_set_smem() {
   (void)hipFuncSetAttribute((const void*)k_conv12_fwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize, CONV12_SMEM);
   (void)hipFuncSetAttribute((const void*)k_conv12_fwd<false>, hipFuncAttributeMaxDynamicSharedMemorySize, CONV12_SMEM);
+}
+
+// ---------------------------------------------------------------------------------------
+// fc layer of the rollout (agent.py:251 / network.py:447): l3 = relu(l2 @ W + b) for a
+// skinny batch (M = E states, N = 256, K = 2592).  One workgroup per 16x16 output tile, the
+// 4 waves split K four ways on v_mfma_f32_16x16x4_f32 and meet in LDS: no split-K slab, no
+// second launch.  Operands stream from L2 straight to registers (A as 16-byte rows, B as
+// 64-byte row segments); K is walked in 16-wide chunks with the next chunk prefetched.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_fc_fwd(const float* __restrict__ A, const float* __restrict__ W,
+                                                const float* __restrict__ bias, float* __restrict__ C, int M) {
+  __shared__ f32x4 red[3][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i16 = lane & 15, j4 = lane >> 4;
+  const int m0 = blockIdx.y * 16, n0 = blockIdx.x * 16;
+  const int m = min(m0 + i16, M - 1);
+  constexpr int KW = FLAT / 4;                    // 648 per wave
+  constexpr int NCH = KW / 16;                    // 40 chunks of 16 (+ 8 left)
+  constexpr int D = 8;                            // chunks in flight per wave (register ring)
+  const float* a = A + (int64_t)m * FLAT + wid * KW + 4 * j4;
+  const float* b = W + (int64_t)(wid * KW + 4 * j4) * FC + n0 + i16;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 ra[D];
+  float rb[D][4];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    ra[d] = *(const f32x4*)(a + 16 * d);
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) rb[d][c4] = b[(int64_t)(16 * d + c4) * FC];
+  }
+  for (int c0 = 0; c0 < NCH; c0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][c4], rb[d][c4], acc, 0, 0, 0);
+      const int cn = c0 + d + D;                  // refill this slot with chunk cn
+      if (cn < NCH) {
+        ra[d] = *(const f32x4*)(a + 16 * cn);
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) rb[d][c4] = b[(int64_t)(16 * cn + c4) * FC];
+      }
+    }
+  }
+  // tail: 8 = KW - 16*NCH values per wave -> lane groups j4 < 2 carry them, others add zeros
+  {
+    const bool live = j4 < 2;
+    const float* at = A + (int64_t)m * FLAT + wid * KW + 16 * NCH + 4 * (j4 & 1);
+    const float* bt = W + (int64_t)(wid * KW + 16 * NCH + 4 * (j4 & 1)) * FC + n0 + i16;
+    f32x4 x = *(const f32x4*)at;
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(live ? x[c4] : 0.f, live ? bt[c4 * FC] : 0.f, acc, 0, 0, 0);
+  }
+  if (wid > 0) red[wid - 1][lane] = acc;
+  __syncthreads();
+  if (wid == 0) {
+    acc += red[0][lane];
+    acc += red[1][lane];
+    acc += red[2][lane];
+    const int n = n0 + i16;
+    const float bb = bias[n];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + 4 * j4 + r;
+      if (row < M) C[(int64_t)row * FC + n] = fmaxf(acc[r] + bb, 0.f);
+    }
+  }
+}
+
+int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s) {
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(k_fc_fwd, dim3(FC / 16, (unsigned)((M + 15) / 16)), dim3(256), 0, s, A, W, bias, C, (int)M);
+  A3C_CHECK(hipGetLastError());
+  return 0;
 }

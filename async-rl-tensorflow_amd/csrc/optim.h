@@ -2,26 +2,41 @@
 #include "a3c_common.h"
 #include "../../include/a3c_hip.h"
 
-#define SS_BLOCKS 64
+#define SS_CHUNK 4096          // elements per sum-of-squares partial block
+#define SS_MAX_BLOCKS 1024     // partial slots (>= sum over tensors of ceil(size / SS_CHUNK))
 enum { OPT_CLIP = 1, OPT_APPLY = 2 };
 
 struct TensorTab {
   int n;
   int64_t off[A3C_MAX_TENSORS];
   int64_t size[A3C_MAX_TENSORS];
+  int pb_first[A3C_MAX_TENSORS];   // first partial block of tensor t
+  int pb_count[A3C_MAX_TENSORS];   // partial blocks of tensor t
+  int nblocks;
+  int64_t total;                   // padded flat length (multiple of 4): the apply pass covers [0, total)
 };
 
 struct OptParams {
   int mode;              // OPT_CLIP | OPT_APPLY
   float clip;            // <= 0: no clipping
-  float lr;              // used when step_ptr == nullptr
-  const int64_t* step_ptr;  // device global step: lr = (max_step - step + 1)/max_step * lr0 (agent.py:393-395)
+  float lr;              // used when sched == nullptr
+  // schedule (engine): the sum-of-squares kernel computes, from the device global step,
+  //   sched[0] = lr = (max_step - step + 1)/max_step * lr0              (agent.py:393-395)
+  //   sched[1] = 1 if a target sync falls in (step, step + step_add]    (agent.py:165-167)
+  float* sched;
+  const int64_t* step_ptr;
   int64_t step_add;
   double lr0;
   int64_t max_step;
+  int64_t target_period;  // 0: no target network
+  float* target;          // apply: params also written here when sched[1] != 0
+  int64_t* counters;      // apply: block 0 advances counters[0] += dtau, counters[1] += step_add
+  int64_t dtau;
   float rho, momentum, eps;
 };
 
-int a3c_optim_launch(float* w, float* ms, float* mom, float* grads, const TensorTab& tt, OptParams op,
-                     double* part, float* sumsq_out, bool compute_sumsq, hipStream_t s);
+int a3c_make_tab(int n, const int64_t* off, const int64_t* size, int64_t total, TensorTab* tt);
+int a3c_sumsq_launch(const float* grads, const TensorTab& tt, const OptParams& op, double* part, hipStream_t s);
+int a3c_apply_launch(float* w, float* ms, float* mom, float* grads, const TensorTab& tt, const OptParams& op,
+                     const double* part, float* sumsq_out, hipStream_t s);
 int a3c_fill_launch(float* p, int64_t n, float v, hipStream_t s);

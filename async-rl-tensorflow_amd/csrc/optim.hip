@@ -1,81 +1,145 @@
 // K10 per-tensor clip_by_norm (agent.py:316-319) + K11 TF ApplyRMSProp (main.py:63-65,
 // agent.py:321) + K12 parameter copy (agent.py:342-344, network.py:96-107).
 //
-// Two launches: k_sumsq_partial (fixed-shape per-tensor partial sums of squares in fp64,
-// deterministic order) then k_clip_apply (every block folds the partials into the per-tensor
-// scales in LDS, then a grid-stride pass clips and/or applies RMSProp).  All element math is
-// written with contraction off so it matches the numpy oracle bit for bit on equal grads.
+// k_sumsq: one partial sum of squares (fp64, fixed order) per SS_CHUNK elements of each tensor,
+//          blocks proportional to tensor size; block 0 also evaluates the lr schedule and the
+//          target-sync decision from the device step counter.
+// k_apply: every block folds the partials into the per-tensor clip scales in LDS, then one
+//          float4 pass over the flat vector clips and/or applies RMSProp (and the target copy);
+//          block 0 advances the engine counters at the end (nothing in this launch reads them).
+// Element math is written with contraction off so it matches the numpy oracle bit for bit on
+// equal gradients.
 #include "optim.h"
 
-__global__ void __launch_bounds__(256) k_sumsq_partial(const float* __restrict__ g, TensorTab tt,
-                                                       double* __restrict__ part) {
-  __shared__ double red[256];
-  const int t = blockIdx.y;
-  const float* p = g + tt.off[t];
-  const int64_t n = tt.size[t];
-  double s = 0.0;
-  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += (int64_t)SS_BLOCKS * 256) {
-    double v = (double)p[j];
-    s += v * v;
+int a3c_make_tab(int n, const int64_t* off, const int64_t* size, int64_t total, TensorTab* tt) {
+  if (n <= 0 || n > A3C_MAX_TENSORS || !off || !size || (total & 3)) return -1;
+  tt->n = n;
+  int nb = 0;
+  int64_t end = 0;
+  for (int i = 0; i < n; ++i) {
+    if ((off[i] & 3) || size[i] < 0 || off[i] < end) return -1;
+    tt->off[i] = off[i];
+    tt->size[i] = size[i];
+    tt->pb_first[i] = nb;
+    tt->pb_count[i] = (int)((size[i] + SS_CHUNK - 1) / SS_CHUNK);
+    nb += tt->pb_count[i];
+    end = off[i] + size[i];
   }
+  if (nb > SS_MAX_BLOCKS || end > total) return -1;
+  tt->nblocks = nb;
+  tt->total = total;
+  return 0;
+}
+
+__global__ void __launch_bounds__(256) k_sumsq(const float* __restrict__ g, TensorTab tt, OptParams op,
+                                               double* __restrict__ part) {
+  __shared__ double red[256];
+  int t = 0;
+  while (t + 1 < tt.n && (int)blockIdx.x >= tt.pb_first[t + 1]) ++t;
+  const int64_t c = blockIdx.x - tt.pb_first[t];
+  const int64_t beg = c * SS_CHUNK;
+  const int64_t end = min(tt.size[t], beg + (int64_t)SS_CHUNK);
+  const float* p = g + tt.off[t];
+  double s = 0.0;
+  // tensor offsets are 4-aligned, chunk starts are 4096-aligned: float4 body + scalar tail
+  const int64_t end4 = beg + ((end - beg) & ~(int64_t)3);
+  for (int64_t j = beg + 4 * threadIdx.x; j < end4; j += 4 * 256) {
+    f32x4 v = *(const f32x4*)(p + j);
+    s += (double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3];
+  }
+  for (int64_t j = end4 + threadIdx.x; j < end; j += 256) s += (double)p[j] * p[j];
   red[threadIdx.x] = s;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) part[t * SS_BLOCKS + blockIdx.x] = red[0];
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = red[0];
+    if (blockIdx.x == 0 && op.sched && op.step_ptr) {
+      const int64_t g0 = *op.step_ptr;
+      const double step = (double)(g0 + op.step_add);
+      op.sched[0] = (float)((double)(op.max_step - step + 1.0) / (double)op.max_step * op.lr0);
+      int copy = 0;
+      if (op.target_period > 0)
+        copy = (g0 + op.step_add + 1) / op.target_period != (g0 + 1) / op.target_period;
+      op.sched[1] = copy ? 1.0f : 0.0f;
+    }
+  }
 }
 
-__global__ void __launch_bounds__(256) k_clip_apply(float* __restrict__ w, float* __restrict__ ms,
-                                                    float* __restrict__ mom, float* __restrict__ grads,
-                                                    TensorTab tt, const double* __restrict__ part,
-                                                    OptParams op, float* __restrict__ sumsq_out) {
+__global__ void __launch_bounds__(256) k_apply(float* __restrict__ w, float* __restrict__ ms,
+                                               float* __restrict__ mom, float* __restrict__ grads,
+                                               TensorTab tt, const double* __restrict__ part, OptParams op,
+                                               float* __restrict__ sumsq_out) {
 #pragma clang fp contract(off)
   __shared__ float cm[A3C_MAX_TENSORS];
-  __shared__ float s_lr;
+  __shared__ float s_lr, s_copy;
+  __shared__ double red[4][A3C_MAX_TENSORS];
+  // per-tensor fold of the partials: wave w sums tensors t = w, w+4, ... with all 64 lanes
+  {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int t = wv; t < tt.n; t += 4) {
+      double v = 0.0;
+      for (int b = lane; b < tt.pb_count[t]; b += 64) v += part[tt.pb_first[t] + b];
+      v = wave_sum_d(v);
+      if (lane == 0) red[0][t] = v;
+    }
+  }
+  __syncthreads();
   if (threadIdx.x < tt.n) {
-    double ss = 0.0;
-    for (int b = 0; b < SS_BLOCKS; ++b) ss += part[threadIdx.x * SS_BLOCKS + b];
+    const double ss = red[0][threadIdx.x];
     const float ssf = (float)ss;
     if (blockIdx.x == 0 && sumsq_out) sumsq_out[threadIdx.x] = ssf;
     float m = 1.0f;
-    if (op.clip > 0.f) {
+    if (op.clip > 0.f && (op.mode & OPT_CLIP)) {
       const float inv = ssf > 0.f ? 1.0f / sqrtf(ssf) : INFINITY;
-      m = fminf(inv, 1.0f / op.clip);
+      m = fminf(inv, 1.0f / op.clip);      // tf.clip_by_norm: t * clip * min(rsqrt(ss), 1/clip)
     }
     cm[threadIdx.x] = m;
   }
   if (threadIdx.x == 0) {
-    float lr = op.lr;
-    if (op.step_ptr) {
-      const double step = (double)(*op.step_ptr + op.step_add);
-      lr = (float)((double)(op.max_step - step + 1.0) / (double)op.max_step * op.lr0);
-    }
-    s_lr = lr;
+    s_lr = op.sched ? op.sched[0] : op.lr;
+    s_copy = (op.sched && op.target) ? op.sched[1] : 0.f;
   }
   __syncthreads();
   const float lr = s_lr;
+  const bool copy = s_copy != 0.f;
+  const bool clip = op.clip > 0.f && (op.mode & OPT_CLIP);
+  const bool apply = op.mode & OPT_APPLY;
   const float one_m_rho = 1.0f - op.rho;
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t gstride = (int64_t)gridDim.x * blockDim.x;
-  for (int t = 0; t < tt.n; ++t) {
-    const int64_t off = tt.off[t], n = tt.size[t];
-    const float c = cm[t];
-    for (int64_t j = gid; j < n; j += gstride) {
-      float g = grads[off + j];
-      if (op.clip > 0.f && (op.mode & OPT_CLIP)) g = (g * op.clip) * c;
-      if (op.mode & OPT_APPLY) {
-        float m2 = ms[off + j];
-        m2 = m2 + (g * g - m2) * one_m_rho;
-        float mo = mom[off + j] * op.momentum + (g * lr) / sqrtf(m2 + op.eps);
-        ms[off + j] = m2;
-        mom[off + j] = mo;
-        w[off + j] = w[off + j] - mo;
-      } else {
-        grads[off + j] = g;
-      }
+  const int64_t n4 = tt.total >> 2;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = 4 * q;
+    int t = 0;
+    while (t + 1 < tt.n && i >= tt.off[t + 1]) ++t;     // padding after tensor t has zero grads
+    f32x4 g = *(const f32x4*)(grads + i);
+    if (clip) {
+      const float c = cm[t];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) g[k] = (g[k] * op.clip) * c;
     }
+    if (apply) {
+      f32x4 m2 = *(const f32x4*)(ms + i);
+      f32x4 mo = *(const f32x4*)(mom + i);
+      f32x4 wv = *(const f32x4*)(w + i);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        m2[k] = m2[k] + (g[k] * g[k] - m2[k]) * one_m_rho;
+        mo[k] = mo[k] * op.momentum + (g[k] * lr) / sqrtf(m2[k] + op.eps);
+        wv[k] = wv[k] - mo[k];
+      }
+      *(f32x4*)(ms + i) = m2;
+      *(f32x4*)(mom + i) = mo;
+      *(f32x4*)(w + i) = wv;
+      if (copy) *(f32x4*)(op.target + i) = wv;
+    } else {
+      *(f32x4*)(grads + i) = g;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && op.counters) {
+    op.counters[0] += op.dtau;
+    op.counters[1] += op.step_add;
   }
 }
 
@@ -84,14 +148,19 @@ __global__ void k_fill(float* __restrict__ p, int64_t n, float v) {
   if (i < n) p[i] = v;
 }
 
-int a3c_optim_launch(float* w, float* ms, float* mom, float* grads, const TensorTab& tt, OptParams op,
-                     double* part, float* sumsq_out, bool compute_sumsq, hipStream_t s) {
-  if (tt.n <= 0 || tt.n > A3C_MAX_TENSORS) return a3c_set_error(A3C_ERR_INVALID, "optim", "bad tensor table");
-  if (compute_sumsq) {
-    hipLaunchKernelGGL(k_sumsq_partial, dim3(SS_BLOCKS, tt.n), dim3(256), 0, s, grads, tt, part);
-    A3C_CHECK(hipGetLastError());
-  }
-  hipLaunchKernelGGL(k_clip_apply, dim3(256), dim3(256), 0, s, w, ms, mom, grads, tt, part, op, sumsq_out);
+int a3c_sumsq_launch(const float* grads, const TensorTab& tt, const OptParams& op, double* part, hipStream_t s) {
+  hipLaunchKernelGGL(k_sumsq, dim3(tt.nblocks), dim3(256), 0, s, grads, tt, op, part);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+int a3c_apply_launch(float* w, float* ms, float* mom, float* grads, const TensorTab& tt, const OptParams& op,
+                     const double* part, float* sumsq_out, hipStream_t s) {
+  int64_t n4 = tt.total >> 2;
+  int blocks = (int)((n4 + 255) / 256);
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_apply, dim3(blocks), dim3(256), 0, s, w, ms, mom, grads, tt, part, op, sumsq_out);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
@@ -107,26 +176,28 @@ int a3c_fill_launch(float* p, int64_t n, float v, hipStream_t s) {
 extern "C" int a3c_optim_workspace_bytes(int64_t total, int64_t* bytes) {
   (void)total;
   if (!bytes) return a3c_set_error(A3C_ERR_INVALID, "a3c_optim_workspace_bytes", "null");
-  *bytes = (int64_t)A3C_MAX_TENSORS * SS_BLOCKS * sizeof(double);
+  *bytes = (int64_t)SS_MAX_BLOCKS * sizeof(double);
   return 0;
 }
 
-static int make_tab(int n, const int64_t* off, const int64_t* size, TensorTab* tt) {
-  if (n <= 0 || n > A3C_MAX_TENSORS || !off || !size) return -1;
-  tt->n = n;
-  for (int i = 0; i < n; ++i) { tt->off[i] = off[i]; tt->size[i] = size[i]; }
-  return 0;
+static int64_t tab_total(int n, const int64_t* off, const int64_t* size) {
+  int64_t e = 0;
+  for (int i = 0; i < n; ++i) e = off[i] + size[i] > e ? off[i] + size[i] : e;
+  return (e + 3) & ~(int64_t)3;
 }
 
 extern "C" int a3c_clip_grads(float* grads, int n_tensors, const int64_t* offsets, const int64_t* sizes,
                               float clip, float* sumsq_out, void* workspace, void* stream) {
   TensorTab tt;
-  if (!grads || !workspace || make_tab(n_tensors, offsets, sizes, &tt))
-    return a3c_set_error(A3C_ERR_INVALID, "a3c_clip_grads", "bad argument");
+  if (!grads || !workspace || !offsets || !sizes || n_tensors <= 0 || n_tensors > A3C_MAX_TENSORS ||
+      a3c_make_tab(n_tensors, offsets, sizes, tab_total(n_tensors, offsets, sizes), &tt))
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_clip_grads", "bad argument (offsets must be 4-aligned, ascending)");
   OptParams op = {};
   op.mode = OPT_CLIP; op.clip = clip;
-  return a3c_optim_launch(nullptr, nullptr, nullptr, grads, tt, op, (double*)workspace, sumsq_out, true,
-                          (hipStream_t)stream);
+  hipStream_t s = (hipStream_t)stream;
+  int rc = a3c_sumsq_launch(grads, tt, op, (double*)workspace, s);
+  if (rc) return rc;
+  return a3c_apply_launch(nullptr, nullptr, nullptr, grads, tt, op, (double*)workspace, sumsq_out, s);
 }
 
 extern "C" int a3c_clip_rmsprop_apply(float* params, float* ms, float* mom, float* grads, int n_tensors,
@@ -134,12 +205,15 @@ extern "C" int a3c_clip_rmsprop_apply(float* params, float* ms, float* mom, floa
                                       float momentum, float eps, float clip, float* sumsq_out,
                                       void* workspace, void* stream) {
   TensorTab tt;
-  if (!params || !ms || !mom || !grads || !workspace || make_tab(n_tensors, offsets, sizes, &tt))
-    return a3c_set_error(A3C_ERR_INVALID, "a3c_clip_rmsprop_apply", "bad argument");
+  if (!params || !ms || !mom || !grads || !workspace || !offsets || !sizes || n_tensors <= 0 ||
+      n_tensors > A3C_MAX_TENSORS || a3c_make_tab(n_tensors, offsets, sizes, tab_total(n_tensors, offsets, sizes), &tt))
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_clip_rmsprop_apply", "bad argument (offsets must be 4-aligned, ascending)");
   OptParams op = {};
   op.mode = OPT_CLIP | OPT_APPLY; op.clip = clip; op.lr = lr; op.rho = rho; op.momentum = momentum; op.eps = eps;
-  return a3c_optim_launch(params, ms, mom, grads, tt, op, (double*)workspace, sumsq_out, true,
-                          (hipStream_t)stream);
+  hipStream_t s = (hipStream_t)stream;
+  int rc = a3c_sumsq_launch(grads, tt, op, (double*)workspace, s);
+  if (rc) return rc;
+  return a3c_apply_launch(params, ms, mom, grads, tt, op, (double*)workspace, sumsq_out, s);
 }
 
 extern "C" int a3c_copy_params(float* dst, const float* src, int64_t n, void* stream) {

@@ -1,34 +1,106 @@
 // K1 Environment.screen + K2 History kernels and their C-ABI entry points.
+#include <cstdlib>
 #include "preprocess_dev.h"
+#include "screen_atari.h"
 #include "../../include/a3c_hip.h"
 
+// grid (parts, n): workgroup (q, i) produces output band q of frame i
 __global__ void __launch_bounds__(256) k_preprocess(const uint8_t* __restrict__ rgb,
                                                     const int32_t* __restrict__ frame_idx,
                                                     uint8_t* __restrict__ out, int64_t out_stride,
                                                     PreGeom g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int64_t i = blockIdx.x;
+  const int64_t i = blockIdx.y;
   const int64_t fb = (int64_t)g.in_h * g.in_w * 3;
   const int64_t f = frame_idx ? (int64_t)frame_idx[i] : i;
-  a3c_preprocess_block(rgb + f * fb, out + i * out_stride, g, smem);
+  a3c_preprocess_part(rgb + f * fb, out + i * out_stride, g, blockIdx.x, smem);
+}
+
+// specialised Atari geometry: grid (84/ROWS bands, n)
+template <int ROWS>
+__global__ void __launch_bounds__(256) k_screen_atari(const uint8_t* __restrict__ rgb,
+                                                      const int32_t* __restrict__ frame_idx,
+                                                      uint8_t* __restrict__ out, int64_t out_stride) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int64_t i = blockIdx.y;
+  const int64_t f = frame_idx ? (int64_t)frame_idx[i] : i;
+  atari::screen_band<ROWS>(rgb + f * (atari::IH * atari::IW * 3), out + i * out_stride, blockIdx.x, smem);
+}
+
+template <int ROWS>
+static void launch_atari(const uint8_t* rgb, const int32_t* idx, int64_t n, uint8_t* out, int64_t stride, hipStream_t s) {
+  hipLaunchKernelGGL(k_screen_atari<ROWS>, dim3((atari::OH + ROWS - 1) / ROWS, (unsigned)n), dim3(256),
+                     atari::Smem<ROWS>::BYTES, s, rgb, idx, out, stride);
+}
+
+// luminance step of Environment.screen alone (environment.py:97-98), the exact integer form the
+// Atari kernel uses: out[i] = truncated fp64 0.2126 R + 0.7152 G + 0.0722 B of pixel i
+__global__ void k_luminance(const uint8_t* __restrict__ rgb, int64_t npix, uint8_t* __restrict__ out) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x)
+    out[p] = (uint8_t)atari::lum_exact(rgb[3 * p], rgb[3 * p + 1], rgb[3 * p + 2]);
+}
+
+extern "C" int a3c_luminance_u8(const uint8_t* rgb, int64_t npix, uint8_t* out, void* stream) {
+  if (!rgb || !out || npix < 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_luminance_u8", "bad argument");
+  if (npix == 0) return 0;
+  hipLaunchKernelGGL(k_luminance, dim3(4096), dim3(256), 0, (hipStream_t)stream, rgb, npix, out);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+int a3c_screen_rows() {
+  static int rows = [] {
+    const char* v = getenv("A3C_PRE_ROWS");    // tuning knob (tools/microbench_preprocess.py); default 14
+    int r = v ? atoi(v) : 14;
+    return (r == 7 || r == 12 || r == 14 || r == 21 || r == 28 || r == 42) ? r : 14;
+  }();
+  return rows;
+}
+
+int a3c_launch_screen_atari(const uint8_t* rgb, const int32_t* idx, int64_t n, uint8_t* out, int64_t stride,
+                            hipStream_t s) {
+  switch (a3c_screen_rows()) {
+    case 7: launch_atari<7>(rgb, idx, n, out, stride, s); break;
+    case 21: launch_atari<21>(rgb, idx, n, out, stride, s); break;
+    case 28: launch_atari<28>(rgb, idx, n, out, stride, s); break;
+    case 42: launch_atari<42>(rgb, idx, n, out, stride, s); break;
+    case 12: launch_atari<12>(rgb, idx, n, out, stride, s); break;
+    default: launch_atari<14>(rgb, idx, n, out, stride, s); break;
+  }
+  A3C_CHECK(hipGetLastError());
+  return 0;
 }
 
 int a3c_launch_preprocess(const uint8_t* rgb, const int32_t* frame_idx, int64_t n, const PreGeom& g,
                           uint8_t* out, int64_t out_stride, hipStream_t s) {
   if (n <= 0) return 0;
+  if (g.in_h == atari::IH && g.in_w == atari::IW && g.out_h == atari::OH && g.out_w == atari::OW &&
+      (((uintptr_t)rgb) & 15) == 0 && n <= 65535)
+    return a3c_launch_screen_atari(rgb, frame_idx, n, out, out_stride, s);
   size_t sm = a3c_pre_smem_bytes(g);
   if (sm > 160 * 1024) return a3c_set_error(A3C_ERR_INVALID, "a3c_preprocess_u8", "frame too large for LDS");
-  hipLaunchKernelGGL(k_preprocess, dim3((unsigned)n), dim3(256), sm, s, rgb, frame_idx, out, out_stride, g);
+  if (n > 65535) {   // grid.y limit: chunk
+    for (int64_t o = 0; o < n; o += 65535) {
+      int64_t m = n - o < 65535 ? n - o : 65535;
+      int rc = a3c_launch_preprocess(frame_idx ? rgb : rgb + o * (int64_t)g.in_h * g.in_w * 3,
+                                     frame_idx ? frame_idx + o : nullptr, m, g, out + o * out_stride, out_stride, s);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  hipLaunchKernelGGL(k_preprocess, dim3(g.parts, (unsigned)n), dim3(256), sm, s, rgb, frame_idx, out, out_stride, g);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
 
+// output bands per frame for the standalone C-ABI path (A3C_PRE_PARTS overrides: tuning knob)
 PreGeom a3c_make_geom(int in_h, int in_w, int out_h, int out_w) {
-  PreGeom g;
-  g.in_h = in_h; g.in_w = in_w; g.out_h = out_h; g.out_w = out_w;
-  g.kh = a3c_pillow_ksize(in_w, out_w);
-  g.kv = a3c_pillow_ksize(in_h, out_h);
-  return g;
+  static int parts = [] {
+    const char* v = getenv("A3C_PRE_PARTS");
+    int p = v ? atoi(v) : 8;
+    return p > 0 ? p : 8;
+  }();
+  return a3c_make_geom_parts(in_h, in_w, out_h, out_w, parts);
 }
 
 extern "C" int a3c_preprocess_u8(const uint8_t* rgb, const int32_t* frame_idx, int64_t n, int in_h,

@@ -1,0 +1,180 @@
+// K1 specialised for the Atari geometry 210x160 RGB -> 84x84 (environment.py:49-53 with
+// config.py:38-39): Pillow's BILINEAR coefficients are generated at compile time (constexpr
+// restatement of precompute_coeffs/normalize_coeffs_8bpc, IEEE double, no contraction), every
+// tap loop has a fixed length (zero weights past a row's count, reads clamped in bounds), and
+// the luminance uses an exact integer form:
+//   numpy's fp64  0.2126 R + 0.7152 G + 0.0722 B  truncated  ==  floor((2126R + 7152G + 722B) / 10^4)
+// whenever the integer sum is not a multiple of 10^4 (the fp64 rounding error, < 1e-13, cannot
+// cross an integer that lies >= 1e-4 away); multiples of 10^4 take the fp64 expression itself.
+// Exhaustively checked over all 2^24 RGB values against the reference's table
+// (tests/test_gpu_kernels.py::test_preprocess_full_luminance_table).
+#pragma once
+#include "preprocess_dev.h"
+
+namespace atari {
+
+constexpr int IH = 210, IW = 160, OH = 84, OW = 84;
+
+template <int IN, int OUT>
+struct Coef {
+  static constexpr double scale = (double)(float)IN / (double)OUT;
+  static constexpr double filterscale = scale < 1.0 ? 1.0 : scale;
+  static constexpr double support = 1.0 * filterscale;
+  static constexpr int K = ((int)support + ((double)(int)support < support ? 1 : 0)) * 2 + 1;
+  int xmin[OUT];
+  int cnt[OUT];
+  int k[OUT][K];
+  constexpr Coef() : xmin(), cnt(), k() {
+    for (int xx = 0; xx < OUT; ++xx) {
+      const double center = 0.0 + (xx + 0.5) * scale;
+      const double ss = 1.0 / filterscale;
+      int lo = (int)(center - support + 0.5);
+      if (lo < 0) lo = 0;
+      int hi = (int)(center + support + 0.5);
+      if (hi > IN) hi = IN;
+      const int n = hi - lo;
+      double ww = 0.0;
+      for (int x = 0; x < n; ++x) ww += tap(x, lo, center, ss);
+      for (int x = 0; x < K; ++x) {
+        double w = 0.0;
+        if (x < n) {
+          w = tap(x, lo, center, ss);
+          if (ww != 0.0) w = w / ww;
+        }
+        const double v = w * (double)(1 << A3C_PRECISION_BITS);
+        k[xx][x] = w < 0 ? (int)(-0.5 + v) : (int)(0.5 + v);
+      }
+      xmin[xx] = lo;
+      cnt[xx] = n;
+    }
+  }
+  static constexpr double tap(int x, int lo, double center, double ss) {
+    double t = ((double)(x + lo) - center + 0.5) * ss;
+    if (t < 0.0) t = -t;
+    return t < 1.0 ? 1.0 - t : 0.0;
+  }
+};
+
+constexpr Coef<IW, OW> kH{};
+constexpr Coef<IH, OH> kV{};
+constexpr int KH = Coef<IW, OW>::K;   // 5
+constexpr int KV = Coef<IH, OH>::K;   // 7
+
+__constant__ Coef<IW, OW> cH = kH;
+__constant__ Coef<IH, OH> cV = kV;
+
+// source rows [y0, y1) of output band [yy0, yy0 + rows)
+constexpr int band_y0(int yy0) { return kV.xmin[yy0]; }
+constexpr int band_y1(int yy0, int rows) { return kV.xmin[yy0 + rows - 1] + kV.cnt[yy0 + rows - 1]; }
+template <int ROWS>
+constexpr int max_src_rows() {
+  int m = 0;
+  for (int b = 0; b * ROWS < OH; ++b) {
+    const int r = (b + 1) * ROWS <= OH ? ROWS : OH - b * ROWS;
+    const int s = band_y1(b * ROWS, r) - band_y0(b * ROWS);
+    m = s > m ? s : m;
+  }
+  return m;
+}
+
+// exact truncated fp64 luminance (see header)
+__device__ inline uint32_t lum_exact(uint32_t r, uint32_t g, uint32_t b) {
+  const uint32_t y = 2126u * r + 7152u * g + 722u * b;       // < 2^22
+  const uint32_t q = (uint32_t)(((uint64_t)y * 3518437209ull) >> 45);   // y / 10000 (exact for y < 2^32/..)
+  if (q * 10000u == y) return a3c_lum(r, g, b);               // exact multiple: fp64 decides
+  return q;
+}
+
+template <int ROWS>
+struct Smem {
+  static constexpr int SR = max_src_rows<ROWS>();
+  static constexpr int RAW = SR * IW * 3;                      // multiple of 16 (IW*3 = 480)
+  static constexpr int GRAY = SR * IW;                         // multiple of 16
+  static constexpr int TMP = ((SR * OW + 15) / 16) * 16;
+  static constexpr int BYTES = RAW + GRAY + TMP;
+};
+
+// One workgroup (256 threads) produces output rows [band*ROWS, band*ROWS + ROWS) of one frame.
+template <int ROWS>
+__device__ inline void screen_band(const uint8_t* __restrict__ rgb, uint8_t* __restrict__ out, int band,
+                                   uint8_t* smem) {
+  using S = Smem<ROWS>;
+  const int tid = threadIdx.x;
+  const int yy0 = band * ROWS;
+  const int rows = (yy0 + ROWS <= OH) ? ROWS : OH - yy0;
+  const int y0 = cV.xmin[yy0];
+  const int y1 = cV.xmin[yy0 + rows - 1] + cV.cnt[yy0 + rows - 1];
+  uint8_t* raw = smem;
+  uint8_t* gray = smem + S::RAW;
+  uint8_t* tmp = gray + S::GRAY;
+
+  // ---- stage source rows [y0, y1): 16-byte coalesced loads, all issued before any store ----
+  const uint4* s4 = (const uint4*)(rgb + y0 * IW * 3);
+  const int n16 = (y1 - y0) * (IW * 3 / 16);
+  constexpr int PER = (S::RAW / 16 + 255) / 256;
+  uint4 r[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) r[j] = s4[min(tid + 256 * j, n16 - 1)];   // clamped: always a valid load
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (tid + 256 * j < n16) ((uint4*)raw)[tid + 256 * j] = r[j];
+  __syncthreads();
+
+  // ---- luminance, 16 pixels (48 B) per thread-iteration ----
+  const int nunit = (y1 - y0) * (IW / 16);
+  for (int u = tid; u < nunit; u += 256) {
+    const uint4* r4 = (const uint4*)(raw + 48 * u);
+    const uint4 a = r4[0], b = r4[1], c = r4[2];
+    const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+    uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const int i0 = 3 * p, i1 = 3 * p + 1, i2 = 3 * p + 2;
+      const uint32_t rr = (w[i0 >> 2] >> (8 * (i0 & 3))) & 255u;
+      const uint32_t gg = (w[i1 >> 2] >> (8 * (i1 & 3))) & 255u;
+      const uint32_t bb = (w[i2 >> 2] >> (8 * (i2 & 3))) & 255u;
+      o[p >> 2] |= lum_exact(rr, gg, bb) << (8 * (p & 3));
+    }
+    *(uint4*)(gray + 16 * u) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  __syncthreads();
+
+  // ---- horizontal pass: thread -> (column, row phase); the column's taps stay in registers ----
+  const int srows = y1 - y0;
+  if (tid < 3 * OW) {
+    const int xx = tid % OW, rp = tid / OW;
+    const int x0 = cH.xmin[xx];
+    int kk[KH], off[KH];
+#pragma unroll
+    for (int x = 0; x < KH; ++x) {
+      kk[x] = cH.k[xx][x];
+      off[x] = min(x0 + x, IW - 1);          // weight is 0 past the row's count
+    }
+    for (int rr = rp; rr < srows; rr += 3) {
+      const uint8_t* s = gray + rr * IW;
+      int acc = 1 << (A3C_PRECISION_BITS - 1);
+#pragma unroll
+      for (int x = 0; x < KH; ++x) acc += (int)s[off[x]] * kk[x];
+      tmp[rr * OW + xx] = a3c_clip8(acc);
+    }
+  }
+  __syncthreads();
+
+  // ---- vertical pass for the band ----
+  if (tid < 3 * OW) {
+    const int xx = tid % OW, rp = tid / OW;
+    for (int yy = rp; yy < rows; yy += 3) {
+      const int Y = yy0 + yy;
+      const int b0 = cV.xmin[Y] - y0;
+      int acc = 1 << (A3C_PRECISION_BITS - 1);
+#pragma unroll
+      for (int y = 0; y < KV; ++y) {
+        const int ry = min(b0 + y, srows - 1);
+        acc += (int)tmp[ry * OW + xx] * cV.k[Y][y];
+      }
+      out[Y * OW + xx] = a3c_clip8(acc);
+    }
+  }
+}
+
+}  // namespace atari

@@ -61,6 +61,7 @@ SIGNATURES = {
     'a3c_workspace_bytes': (c_int, [ctypes.POINTER(NetDesc), c_i64, ctypes.POINTER(c_i64)]),
     'a3c_preprocess_u8': (c_int, [c_void_p, c_void_p, c_i64, c_int, c_int, c_void_p, c_i64, c_int, c_int,
                                   c_void_p]),
+    'a3c_luminance_u8': (c_int, [c_void_p, c_i64, c_void_p, c_void_p]),
     'a3c_history_push': (c_int, [c_void_p, c_void_p, c_void_p, c_i64, c_int, c_i64, c_void_p]),
     'a3c_history_get_f32': (c_int, [c_void_p, c_i64, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     'a3c_z_stride': (c_int, [ctypes.POINTER(NetDesc)]),

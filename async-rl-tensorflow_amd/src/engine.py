@@ -88,11 +88,21 @@ class Engine:
         self.act_l2 = _view(b.act_l2, (n * E, 2592), torch.float32)
         self.act_l3 = _view(b.act_l3, (n * E, 256), torch.float32)
         self.frame_pool = _view(b.frame_pool, (int(cfg.num_frames), 210, 160, 3), torch.uint8)
-        self.env_frame = _view(b.env_frame, (E,), torch.int32)
-        self.env_lives = _view(b.env_lives, (E,), torch.int32)
-        self.env_episode = _view(b.env_episode, (E,), torch.int32)
-        self.env_step = _view(b.env_step, (E,), torch.int32)
-        self.env_len = _view(b.env_len, (E,), torch.int32)
+        # env state is double-buffered by step parity: the current state lives at tau & 1
+        self._env = {'frame': _view(b.env_frame, (2, E), torch.int32),
+                     'lives': _view(b.env_lives, (2, E), torch.int32),
+                     'episode': _view(b.env_episode, (2, E), torch.int32),
+                     'ep_step': _view(b.env_step, (2, E), torch.int32),
+                     'ep_len': _view(b.env_len, (2, E), torch.int32)}
+
+    def env_field(self, name):
+        """Current synthetic-env state field [E] (frame, lives, episode, ep_step, ep_len)."""
+        tau = int(self.counters[0].item())
+        return self._env[name][tau & 1]
+
+    @property
+    def env_frame(self):
+        return self.env_field('frame')
 
     def close(self):
         if getattr(self, '_h', None):

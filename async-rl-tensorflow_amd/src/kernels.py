@@ -46,6 +46,14 @@ def preprocess(rgb, frame_idx=None, out_hw=(IMG, IMG), out=None):
     return out
 
 
+def luminance(rgb):
+    """environment.py:97-98 alone: [...,3] u8 -> [...] u8 (exact integer form of the fp64 sum)."""
+    _dev(rgb, torch.uint8, 'rgb')
+    out = torch.empty(rgb.shape[:-1], dtype=torch.uint8, device=rgb.device)
+    check(lib().a3c_luminance_u8(ptr(rgb), out.numel(), ptr(out), stream_handle()), 'a3c_luminance_u8')
+    return out
+
+
 def history_push(hist, screens, reset_mask=None):
     """History.add (+ History.reset when reset_mask) on [n,L,h,w] u8 histories, in place."""
     _dev(hist, torch.uint8, 'hist')

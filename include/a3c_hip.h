@@ -73,6 +73,10 @@ int a3c_workspace_bytes(const a3c_net_desc* net, int64_t B, int64_t* bytes);
 int a3c_preprocess_u8(const uint8_t* rgb, const int32_t* frame_idx, int64_t n, int in_h, int in_w,
                       uint8_t* out, int64_t out_stride, int out_h, int out_w, void* stream);
 
+/* luminance step alone (environment.py:97-98): out[i] = uint8(fp64 0.2126R+0.7152G+0.0722B)
+ * for npix RGB pixels, in the exact integer form the Atari screen kernel uses. */
+int a3c_luminance_u8(const uint8_t* rgb, int64_t npix, uint8_t* out, void* stream);
+
 /* ----------------------------------------------------------------------------
  * K2  History (history.py:3-27).  hist is [n][L][h*w] u8 (oldest plane first);
  *     push: if reset_mask && reset_mask[i]: zero (History.reset, :17-18); then shift one
@@ -225,11 +229,11 @@ typedef struct a3c_engine_buffers {
 int a3c_engine_get_buffers(a3c_engine* eng, a3c_engine_buffers* out);
 
 /* profiling hook: average device time (ms) of `iters` back-to-back launches of one engine
- * kernel on its live buffers, bracketed by HIP events on `stream`.  A3C_KER_ENV_STEP
- * advances the env state (use only after a measurement). */
+ * kernel on its live buffers, bracketed by HIP events on `stream` (idempotent: each
+ * relaunch recomputes the same outputs). */
 #define A3C_KER_CONV12_FWD 0   /* conv1+conv2 forward, B = E (saves conv1 out)          */
 #define A3C_KER_FC_FWD 1       /* fc 2592->256 forward GEMM (+split-K reduce), B = E     */
-#define A3C_KER_ENV_STEP 2     /* env step + Environment.screen into the frame ring      */
+#define A3C_KER_ENV_STEP 2     /* Environment.screen of the post-act frames into the ring */
 #define A3C_KER_CONV_BWD 3     /* fused conv backward over B = n*E                       */
 int a3c_engine_time_kernel(a3c_engine* eng, int kernel, int iters, void* stream, float* avg_ms);
 

@@ -82,7 +82,6 @@ def test_engine_matches_oracle(algo, A, E, n, lives):
         assert agree >= 0.98, agree
         assert np.array_equal(eng.rewards.cpu().numpy(), out['rewards'])
         assert np.array_equal(eng.terminals.cpu().numpy(), out['terminals'])
-        assert np.array_equal(eng.env_frame.cpu().numpy(), ref.env.frame.astype(np.int32))
         gr = eng.frame_ring.cpu().numpy()
         bad = [(e, sl, int((gr[e, sl] != ref.ring[e, sl]).sum())) for e in range(E) for sl in range(R)
                if not np.array_equal(gr[e, sl], ref.ring[e, sl])]
@@ -99,14 +98,19 @@ def test_engine_matches_oracle(algo, A, E, n, lives):
             assert abs(loss[0] - out['losses']['loss']) <= 1e-4 * max(1.0, abs(out['losses']['loss']))
         ss = eng.sumsq.cpu().numpy()
         G = unflat(eng, ns, eng.grads)
+        # single GPU: the per-tensor clip is fused into apply, so after rollout_grad the buffer
+        # holds the raw gradient and sumsq its squared norms
         # backward arithmetic on the GPU's own activations (same ReLU masks): 1e-4
         g_same = gpu_act_grads(eng, ref, algo, A, n, E, ns, tgt)
         for i, (name, _) in enumerate(ns):
-            assert rel_l2(G[name], Rc.clip_by_norm(g_same[name], 40.0)) < 1e-4, (it, name)
-            assert np.isclose(ss[i], np.sum(g_same[name].astype(np.float64) ** 2), rtol=2e-4), (it, name)
+            assert rel_l2(G[name], g_same[name]) < 1e-4, (it, name)
             # fully independent fp64 oracle: ReLU-mask flips allowed
-            assert rel_l2(G[name], out['clipped'][name]) < 2e-2, (it, name)
+            assert rel_l2(G[name], out['grads'][name]) < 2e-2, (it, name)
         eng.apply()
+        torch.cuda.synchronize()
+        ss = eng.sumsq.cpu().numpy()
+        for i, (name, _) in enumerate(ns):
+            assert np.isclose(ss[i], np.sum(G[name].astype(np.float64) ** 2), rtol=1e-5), (it, name)
         # the oracle optimizer consumes the same-mask gradients so the two parameter
         # trajectories stay comparable at 1e-5 over iterations
         ref.apply({k: Rc.clip_by_norm(v, 40.0) for k, v in g_same.items()})
@@ -117,6 +121,9 @@ def test_engine_matches_oracle(algo, A, E, n, lives):
             assert d <= 1e-5 * max(1.0, np.abs(ref.params[name]).max()), (it, name, d)
         cnt = eng.counters.cpu().numpy()
         assert cnt[0] == ref.tau and cnt[1] == ref.global_step
+        for f, ref_v in (('frame', ref.env.frame), ('lives', ref.env.lives), ('episode', ref.env.episode),
+                         ('ep_step', ref.env.ep_step), ('ep_len', ref.env.ep_len)):
+            assert np.array_equal(eng.env_field(f).cpu().numpy(), ref_v.astype(np.int32)), f
         if algo == 'q':
             T = unflat(eng, ns, eng.target_params)
             for name, _ in ns:

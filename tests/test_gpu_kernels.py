@@ -67,6 +67,14 @@ def test_preprocess_full_luminance_table(K, screen_golden):
     assert hashlib.sha256(out.tobytes()).hexdigest() == str(screen_golden['lum_sha256'])
 
 
+def test_luminance_exact_integer_form_all_rgb(K, screen_golden):
+    """The Atari screen kernel's integer luminance over all 2^24 RGB triples == the reference table."""
+    rgb = np.arange(1 << 24, dtype=np.uint32)
+    fr = np.stack([(rgb >> 16) & 255, (rgb >> 8) & 255, rgb & 255], -1).astype(np.uint8)
+    out = K.luminance(cu(fr)).cpu().numpy()
+    assert hashlib.sha256(out.tobytes()).hexdigest() == str(screen_golden['lum_sha256'])
+
+
 def test_preprocess_gather_stride_and_unaligned(K):
     rng = np.random.default_rng(5)
     pool = rng.integers(0, 256, (7, 210, 160, 3), dtype=np.uint8)
