@@ -1,0 +1,153 @@
+"""main.py:1-98 on MI355X.  Same flags; ``--job_name``/``--ps_hosts``/``--worker_hosts`` are
+accepted but the TF ps/worker cluster is replaced by one process per GPU under torchrun
+(torch.distributed, backend nccl = RCCL), see src/distributed.py.
+
+  --mode agent   the reference's per-step Q-learning Agent loop (agent.py:52-139), one env per
+                 process, drop-in API (src/agent.py);
+  --mode engine  the batched MI355X actor-learner (num_envs envs per GPU, n-step rollout +
+                 gradient + exchange + RMSProp per iteration, src/engine.py).
+
+  python main.py --mode engine --env_name Pong-v0 --iterations 1000
+  python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 main.py --mode engine
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import numpy as np    # noqa: E402
+import torch          # noqa: E402
+
+
+def str2bool(v):
+  return str(v).lower() in ('1', 'true', 'yes', 'y', 't')
+
+
+def parse_flags(argv=None):
+  p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+  # Model
+  p.add_argument('--model', default='m1')
+  p.add_argument('--dueling', type=str2bool, default=False)
+  p.add_argument('--double_q', type=str2bool, default=False)
+  # Environment
+  p.add_argument('--env_name', default='Breakout-v0')
+  p.add_argument('--action_repeat', type=int, default=1)
+  # Optimizer
+  p.add_argument('--decay', type=float, default=0.99)
+  p.add_argument('--epsilon', type=float, default=0.1)
+  p.add_argument('--momentum', type=float, default=0.0)
+  p.add_argument('--beta', type=float, default=0.01)
+  # Distributed (accepted for compatibility; torchrun provides RANK/WORLD_SIZE)
+  p.add_argument('--ps_hosts', default='0.0.0.0:2222')
+  p.add_argument('--worker_hosts', default='0.0.0.0:2223,0.0.0.0:2224')
+  p.add_argument('--job_name', default='')
+  p.add_argument('--task_index', type=int, default=0)
+  # Misc
+  p.add_argument('--gpu_fraction', default='1/1')
+  p.add_argument('--display', type=str2bool, default=False)
+  p.add_argument('--is_train', type=str2bool, default=True)
+  p.add_argument('--random_seed', type=int, default=123)
+  # MI355X engine
+  p.add_argument('--mode', choices=['agent', 'engine'], default='engine')
+  p.add_argument('--algo', choices=['a3c', 'q'], default='a3c')
+  p.add_argument('--n_step', type=int, default=5)
+  p.add_argument('--num_envs', type=int, default=256)
+  p.add_argument('--num_frames', type=int, default=16384)
+  p.add_argument('--iterations', type=int, default=1000)
+  p.add_argument('--max_step', type=int, default=None)
+  p.add_argument('--log_every', type=int, default=100)
+  p.add_argument('--logdir', default='./logs')
+  return p.parse_args(argv)
+
+
+def run_engine(config, flags):
+  from src import distributed as D
+  from src.engine import Engine
+  from src.environment import game_spec
+  rank, world, local = D.init_from_env()
+  torch.cuda.set_device(local)
+  A, lives = game_spec(config.env_name)
+  E = flags.num_envs
+  opts = dict(gamma=config.discount, discount=config.discount, beta=config.beta, learning_rate=config.learning_rate,
+              max_step=config.max_step, decay=config.decay, momentum=config.momentum, epsilon=config.epsilon,
+              clip_norm=config.clip_norm, literal_adv=int(config.literal_adv), ep_start=config.ep_start,
+              ep_end=config.ep_end, ep_end_t=config.ep_end_t, learn_start=config.learn_start,
+              target_q_update_step=config.target_q_update_step, random_start=config.random_start,
+              action_repeat=config.action_repeat)
+  eng = Engine(num_envs=E, n_step=flags.n_step, action_size=A, algo=flags.algo, start_lives=lives,
+               num_frames=flags.num_frames, seed=flags.random_seed, env_id_base=rank * E, world_size=world, **opts)
+  eng.reset()
+  D.broadcast_params(eng.params, src=0)
+  if flags.algo == 'q':
+    eng.target_params.copy_(eng.params)
+  xch = D.GradExchange() if world > 1 else None
+  torch.cuda.synchronize()
+  t0 = time.time()
+  log = None
+  if rank == 0:
+    os.makedirs(flags.logdir, exist_ok=True)
+    log = open(os.path.join(flags.logdir, 'engine.jsonl'), 'a')
+  for it in range(flags.iterations):
+    eng.iterate(exchange=xch)
+    if rank == 0 and (it + 1) % flags.log_every == 0:
+      loss = eng.loss.tolist()
+      torch.cuda.synchronize()
+      dt = time.time() - t0
+      rec = dict(iteration=it + 1, global_step=int(eng.counters[1].item()),
+                 env_steps_per_sec=(it + 1) * E * flags.n_step * world / dt,
+                 loss_policy=loss[0], loss_value=loss[1], entropy=loss[2], loss_total=loss[3],
+                 mean_return=float(eng.returns.mean().item()), reward_sum=float(eng.rewards.sum().item()))
+      print(json.dumps(rec), flush=True)
+      log.write(json.dumps(rec) + '\n')
+  torch.cuda.synchronize()
+  if log:
+    log.close()
+  return eng
+
+
+def run_agent(config, flags):
+  from src import distributed as D
+  from src.agent import Agent, Supervisor
+  from src.environment import GymEnvironment
+  from src.optim import RMSPropOptimizer
+  rank, world, local = D.init_from_env()
+  torch.cuda.set_device(local)
+  random.seed(flags.random_seed + rank)
+  env = GymEnvironment(config)
+  optimizer = RMSPropOptimizer(None, decay=0.99, momentum=0, epsilon=0.1)     # main.py:64-65
+  agent = Agent(config, env, optimizer)
+  agent.ep_end = random.sample([0.1, 0.01, 0.5], 1)[0]                        # main.py:68
+  if world > 1:
+    D.broadcast_params(agent.params, src=0)
+  print(agent.model_dir)
+  is_chief = rank == 0
+  sv = Supervisor(is_chief=is_chief, logdir=os.path.join(flags.logdir, agent.model_dir), agent=agent)
+  agent.update_target_q_network()
+  if flags.is_train:
+    (agent.train_with_summary if is_chief else agent.train)(sv, is_chief)
+  else:
+    agent.play(sv, is_chief)
+  return agent
+
+
+def main(argv=None):
+  flags = parse_flags(argv)
+  random.seed(flags.random_seed)
+  np.random.seed(flags.random_seed)
+  from config import get_config
+  config = get_config(flags)
+  config.cnn_format = 'NHWC'                       # main.py:45
+  if flags.max_step is not None:
+    config.max_step = flags.max_step
+  config.algo, config.n_step, config.num_envs = flags.algo, flags.n_step, flags.num_envs
+  if flags.mode == 'engine':
+    return run_engine(config, flags)
+  return run_agent(config, flags)
+
+
+if __name__ == '__main__':
+  main()

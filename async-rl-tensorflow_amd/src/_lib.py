@@ -81,7 +81,17 @@ SIGNATURES = {
     'a3c_clip_rmsprop_apply': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, ctypes.POINTER(c_i64),
                                        ctypes.POINTER(c_i64), c_float, c_float, c_float, c_float, c_float,
                                        c_void_p, c_void_p, c_void_p]),
+    'a3c_conv2d_forward': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 11 + [c_void_p]),
+    'a3c_conv2d_backward': (c_int, [c_void_p] * 6 + [c_int] * 10 + [c_void_p]),
+    'a3c_matmul': (c_int, [c_void_p, c_i64, c_i64, c_void_p, c_i64, c_i64, c_void_p, c_i64, c_int, c_int, c_int,
+                           c_void_p, c_int, c_int, c_void_p]),
     'a3c_copy_params': (c_int, [c_void_p, c_void_p, c_i64, c_void_p]),
+    'a3c_env_create': (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_u64, c_int, ctypes.POINTER(c_void_p)]),
+    'a3c_env_destroy': (c_int, [c_void_p]),
+    'a3c_env_new_game': (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    'a3c_env_act': (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'a3c_env_screen': (c_int, [c_void_p, c_void_p, c_i64, c_void_p]),
+    'a3c_env_buffers': (c_int, [c_void_p] + [ctypes.POINTER(c_void_p)] * 7),
     'a3c_engine_config_default': (None, [ctypes.POINTER(EngineConfig)]),
     'a3c_engine_create': (c_int, [ctypes.POINTER(EngineConfig), ctypes.POINTER(c_void_p)]),
     'a3c_engine_destroy': (c_int, [c_void_p]),

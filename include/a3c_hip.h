@@ -156,8 +156,42 @@ int a3c_clip_rmsprop_apply(float* params, float* ms, float* mom, float* grads, i
                            float momentum, float eps, float clip, float* sumsq_out,
                            void* workspace, void* stream);
 
+/* ----------------------------------------------------------------------------
+ * Generic layer ops (ops.py:4-46 drop-ins, any shape; off the hot path).
+ *  conv2d VALID, weights [kh,kw,cin,cout] (ops.py:16-21), x NHWC [N,H,W,C] or NCHW [N,C,H,W]
+ *  (nhwc flag), y likewise; bias nullable; relu = activation_fn tf.nn.relu (ops.py:27-28).
+ *  backward: dx (nullable) / dw, db (nullable) -- OVERWRITTEN.
+ *  matmul: C[m][n] (+)= sum_k A[m*sam+k*sak] * B[k*sbk+n*sbn] (+bias[n]) (relu) -- linear
+ *  (ops.py:41-46) and its gradients through the strides.
+ * -------------------------------------------------------------------------- */
+int a3c_conv2d_forward(const float* x, const float* w, const float* b, float* y, int N, int H, int W, int C,
+                       int KH, int KW, int SH, int SW, int OC, int nhwc, int relu, void* stream);
+int a3c_conv2d_backward(const float* x, const float* w, const float* dy, float* dx, float* dw, float* db, int N,
+                        int H, int W, int C, int KH, int KW, int SH, int SW, int OC, int nhwc, void* stream);
+int a3c_matmul(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn, float* C,
+               int64_t ldc, int M, int N, int K, const float* bias, int relu, int accumulate, void* stream);
+
 /* K12  target sync (agent.py:342-344) / theta' <- theta (network.py:96-107). */
 int a3c_copy_params(float* dst, const float* src, int64_t n, void* stream);
+
+/* ----------------------------------------------------------------------------
+ * Batched synthetic Atari env (gym/ALE is absent): the Environment / GymEnvironment interface
+ * of environment.py:14-106 for E envs on device (dynamics: oracle/synthetic_env.py).
+ *  new_game(random=0): environment.py:74-79; random=1: new_random_game :81-86 (mask nullable)
+ *  act: GymEnvironment.act :124-142 (simple=1: SimpleGymEnvironment.act :148-152); outputs
+ *       reward / terminal / frame index per env (each nullable), state updated in place
+ *  screen: Environment.screen :95-99 of every env's current frame -> out + e*out_stride
+ * -------------------------------------------------------------------------- */
+typedef struct a3c_env a3c_env;
+int a3c_env_create(int num_envs, int action_size, int start_lives, int random_start, int action_repeat,
+                   int num_frames, uint64_t seed, int env_id_base, a3c_env** out);
+int a3c_env_destroy(a3c_env* env);
+int a3c_env_new_game(a3c_env* env, const uint8_t* mask, int random, void* stream);
+int a3c_env_act(a3c_env* env, const int32_t* actions, int is_training, int simple, float* rewards,
+                uint8_t* terminals, int32_t* frames, void* stream);
+int a3c_env_screen(a3c_env* env, uint8_t* out, int64_t out_stride, void* stream);
+int a3c_env_buffers(a3c_env* env, uint8_t** pool, int32_t** frame, int32_t** lives, uint32_t** episode,
+                    uint32_t** ep_step, float** reward, uint8_t** terminal);
 
 /* ----------------------------------------------------------------------------
  * Batched actor-learner engine: E envs per GPU stepped in lock-step on device

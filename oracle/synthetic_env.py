@@ -132,6 +132,11 @@ class SyntheticAtari:
         self.reward = cum.astype(np.float32)
         return self.frame.copy(), self.reward.copy(), self.terminal.copy()
 
+    def simple_act(self, action):
+        """SimpleGymEnvironment.act, environment.py:148-152 (one raw step, no life-loss handling)."""
+        self._step(action, np.ones(self.E, bool))
+        return self.frame.copy(), self.reward.copy(), self.terminal.copy()
+
     def screens_rgb(self, frames=None):
         frames = self.frame if frames is None else frames
         return np.stack([pool_frame(self.seed, int(f)) for f in frames])

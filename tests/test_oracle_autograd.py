@@ -1,0 +1,85 @@
+"""Cross-check the oracle's hand-written forward/backward (oracle/ref_cpu.py) against torch CPU
+autograd in float64 -- an independent implementation of the same TF semantics:
+conv2d VALID NHWC with [kh,kw,cin,cout] weights (ops.py:21-28), flatten in (h,w,c) order
+(agent.py:231-232), linear x@W+b (ops.py:41), the A3C losses with the SURVEY §8 A11 fixes and
+the Q-learning MSE (agent.py:310-314).  The TF reference itself cannot run here (no TF), so this
+is what pins the network/loss arithmetic ("parity unpinned" against a reference execution)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ref_cpu as R
+
+
+def torch_forward(p, states, algo):
+    x = torch.as_tensor(states, dtype=torch.float64).permute(0, 3, 1, 2) / 255.0    # NHWC -> NCHW
+    T = {k: torch.as_tensor(v, dtype=torch.float64).requires_grad_(True) for k, v in p.items()}
+    w1 = T['l1_w'].permute(3, 2, 0, 1)          # [kh,kw,cin,cout] -> [cout,cin,kh,kw]
+    w2 = T['l2_w'].permute(3, 2, 0, 1)
+    h = F.relu(F.conv2d(x, w1, T['l1_b'], stride=4))
+    h = F.relu(F.conv2d(h, w2, T['l2_b'], stride=2))
+    flat = h.permute(0, 2, 3, 1).reshape(h.shape[0], -1)     # (h,w,c) order
+    fc = 'l4' if algo == 'a3c' else 'l3'
+    h3 = F.relu(flat @ T[fc + '_w'] + T[fc + '_b'])
+    if algo == 'a3c':
+        z = torch.cat([h3 @ T['p_w'] + T['p_b'], h3 @ T['q_w'] + T['q_b']], dim=1)
+    else:
+        z = h3 @ T['q_w'] + T['q_b']
+    return T, z
+
+
+@pytest.mark.parametrize('algo,A,literal', [('a3c', 6, False), ('a3c', 4, True), ('q', 6, False)])
+def test_oracle_backward_matches_torch_autograd(algo, A, literal):
+    rng = np.random.default_rng(11)
+    B = 5
+    from make_goldens import frame_from_spec  # noqa: F401  (conftest path check)
+    shapes = R.param_shapes(A, algo)
+    p = R.init_params(shapes, seed=3, stddev=0.08)
+    for k in p:
+        if k.endswith('_b'):
+            p[k] = (rng.standard_normal(p[k].shape) * 0.05).astype(np.float32)
+    states = rng.integers(0, 256, (B, 84, 84, 4), dtype=np.uint8)
+    actions = rng.integers(0, A, B)
+    target = rng.standard_normal(B)
+    fwd = R.forward(p, states, algo)
+    T, z = torch_forward(p, states, algo)
+    np.testing.assert_allclose(z.detach().numpy(), fwd['z'], rtol=1e-10, atol=1e-12)
+    beta = 0.01
+    if algo == 'a3c':
+        losses, dz = R.a3c_loss_and_dz(fwd['z'], actions, target, beta, literal)
+        logits, V = z[:, :A], z[:, A]
+        logpi = F.log_softmax(logits, dim=1)
+        pi = logpi.exp()
+        H = -(pi * logpi).sum(1)
+        adv = torch.as_tensor(target) - V
+        lp_a = logpi[torch.arange(B), torch.as_tensor(actions)]
+        pol = -(lp_a * (adv if literal else adv.detach())) - beta * H
+        loss = (pol + 0.5 * adv * adv).sum()
+        assert np.isclose(loss.item(), losses['total'], rtol=1e-12)
+        assert np.isclose((-(lp_a * adv) - beta * H).sum().item(), losses['policy'], rtol=1e-12)
+    else:
+        l, dz = R.q_loss_and_dz(fwd['z'], actions, target)
+        q_a = z[torch.arange(B), torch.as_tensor(actions)]
+        loss = ((torch.as_tensor(target) - q_a) ** 2).mean()
+        assert np.isclose(loss.item(), l, rtol=1e-12)
+    loss.backward()
+    g = R.backward(p, fwd, dz, algo)
+    for k in p:
+        np.testing.assert_allclose(g[k].reshape(p[k].shape), T[k].grad.numpy(), rtol=1e-9, atol=1e-12,
+                                   err_msg=k)
+
+
+def test_rmsprop_differs_from_torch_default_as_documented():
+    """torch.optim.RMSprop (eps outside sqrt, square_avg init 0) is NOT TF's ApplyRMSProp: the
+    oracle follows TF (rms init 1.0, eps inside sqrt) -- guard against silently swapping them."""
+    w = np.array([0.5], np.float32)
+    ms, mom = np.ones(1, np.float32), np.zeros(1, np.float32)
+    R.rmsprop_apply(w, ms, mom, np.array([2.0], np.float32), 0.1, 0.99, 0.0, 0.1)
+    tw = torch.tensor([0.5], requires_grad=True)
+    opt = torch.optim.RMSprop([tw], lr=0.1, alpha=0.99, eps=0.1)
+    tw.grad = torch.tensor([2.0])
+    opt.step()
+    assert not np.isclose(w[0], tw.item(), rtol=1e-3)
+    exp = 0.5 - 0.1 * 2.0 / np.sqrt(1.0 + (4.0 - 1.0) * 0.01 + 0.1)
+    assert np.isclose(w[0], exp, rtol=1e-6)
