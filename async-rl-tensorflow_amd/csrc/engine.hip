@@ -22,6 +22,24 @@
 void a3c_init_once();
 int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s);
 
+// Per-rollout buffers.  Sync mode has one slot whose params are the live parameters and whose
+// tau is the live frame counter.  Overlap mode (cfg.overlap = 1) has two: rollout k fills slot
+// k & 1 with its own parameter snapshot and tau while the backward + apply of rollout k-1 (slot
+// (k-1) & 1) runs on the caller's stream -- A3C's stale-parameter asynchrony at a fixed
+// staleness of one update.
+struct Slot {
+  float* P;                // params the rollout (and its backward) use
+  int64_t* tau;            // tau at rollout start (sync: the live counter)
+  int32_t* actions;        // [n][E]
+  int32_t* frames;         // [n][E] post-act frame index per step
+  float* rewards;          // [n][E]
+  uint8_t* terms;          // [n][E]
+  float* z;                // [(n+1)][E][zs]
+  float* R_buf;            // [n][E] returns / TD targets
+  float *act_l1, *act_l2, *act_l3;
+  float *scr_l2, *scr_l3;  // bootstrap / target forward scratch
+};
+
 struct a3c_engine {
   a3c_engine_config cfg;
   NetLayout L;
@@ -34,16 +52,10 @@ struct a3c_engine {
   int64_t* counters;  // [0] tau, [1] global step
   EnvBufs env;
   EnvParams envp;
-  int32_t* actions;
-  int32_t* frames;         // [n][E] post-act frame index per step
-  float* rewards;
-  uint8_t* terms;
-  float* z;
-  float* R_buf;
+  int overlap, nslot;
+  Slot slot[2];
   float* loss;
   float* sumsq;
-  float *act_l1, *act_l2, *act_l3;
-  float *scr_l2, *scr_l3;  // bootstrap / target forward scratch
   float* zt;               // q: target-net q values [nE][zs]
   float* eps;              // q: per env epsilon
   float* ep_end;           // q: per env final epsilon
@@ -53,9 +65,15 @@ struct a3c_engine {
   double* opt_part;
   float* sched;            // [0] lr, [1] target-sync flag (device)
   TensorTab tt;
-  hipGraph_t graph;
-  hipGraphExec_t gexec;
-  bool captured;
+  // sync: one graph (rollout + grad); overlap: rollout and grad graphs per slot
+  hipGraph_t graph[5];
+  hipGraphExec_t gexec[5];
+  bool captured[5];
+  // overlap pipeline
+  hipStream_t rs;          // rollout stream
+  hipEvent_t ev_start, ev_snap[2], ev_roll[2];
+  int64_t iter;            // rollouts issued since reset
+  bool grad_ready;         // the last rollout_grad call computed a gradient
   bool reset_done;
 };
 
@@ -78,6 +96,7 @@ extern "C" void a3c_engine_config_default(a3c_engine_config* c) {
   c->net.screen_w = 84;
   c->num_envs = 256;
   c->n_step = 5;
+  c->overlap = 0;
   c->env_id_base = 0;
   c->world_size = 1;
   c->start_lives = 0;
@@ -105,9 +124,17 @@ extern "C" void a3c_engine_config_default(a3c_engine_config* c) {
 
 extern "C" int a3c_engine_destroy(a3c_engine* e) {
   if (!e) return 0;
-  if (e->captured) {
-    (void)hipGraphExecDestroy(e->gexec);
-    (void)hipGraphDestroy(e->graph);
+  if (e->rs) (void)hipStreamSynchronize(e->rs);
+  for (int i = 0; i < 5; ++i)
+    if (e->captured[i]) {
+      (void)hipGraphExecDestroy(e->gexec[i]);
+      (void)hipGraphDestroy(e->graph[i]);
+    }
+  if (e->rs) (void)hipStreamDestroy(e->rs);
+  if (e->ev_start) (void)hipEventDestroy(e->ev_start);
+  for (int k = 0; k < 2; ++k) {
+    if (e->ev_snap[k]) (void)hipEventDestroy(e->ev_snap[k]);
+    if (e->ev_roll[k]) (void)hipEventDestroy(e->ev_roll[k]);
   }
   for (void* p : e->allocs) (void)hipFree(p);
   delete e;
@@ -121,7 +148,8 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "oom");
   e->cfg = *cfg;
   if (a3c_make_layout(&cfg->net, &e->L) || cfg->num_envs < 1 || cfg->n_step < 1 || cfg->n_step > 64 ||
-      cfg->num_frames < 1 || cfg->random_start < 1 || cfg->action_repeat < 1 || cfg->world_size < 1) {
+      cfg->num_frames < 1 || cfg->random_start < 1 || cfg->action_repeat < 1 || cfg->world_size < 1 ||
+      (cfg->overlap && cfg->net.algo != A3C_ALGO_A3C)) {
     delete e;
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "bad config");
   }
@@ -129,7 +157,10 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   const NetLayout& L = e->L;
   e->E = cfg->num_envs;
   e->n = cfg->n_step;
-  e->R = e->n + HIST + (cfg->net.algo == A3C_ALGO_Q ? 1 : 0);
+  e->overlap = cfg->overlap ? 1 : 0;
+  e->nslot = e->overlap ? 2 : 1;
+  // ring: the states of one rollout (frames tau-3 .. tau+n); overlap keeps two rollouts' frames
+  e->R = (e->overlap ? 2 * e->n : e->n) + HIST + (cfg->net.algo == A3C_ALGO_Q ? 1 : 0);
   e->nE = (int64_t)e->n * e->E;
   e->k0 = (uint32_t)cfg->seed;
   e->k1 = (uint32_t)(cfg->seed >> 32);
@@ -152,20 +183,30 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   ALLOC(e->env.frame, 2 * E * 4);
   ALLOC(e->env.reward, 2 * E * 4);
   ALLOC(e->env.terminal, 2 * E);
-  ALLOC(e->actions, nE * 4);
-  ALLOC(e->frames, nE * 4);
-  ALLOC(e->rewards, nE * 4);
-  ALLOC(e->terms, nE);
-  ALLOC(e->z, (nE + E) * zs * 4);
-  ALLOC(e->R_buf, nE * 4);
   ALLOC(e->loss, 64);
   ALLOC(e->sumsq, A3C_MAX_TENSORS * 4);
-  ALLOC(e->act_l1, nE * C1_P * C1_N * 4);
-  ALLOC(e->act_l2, nE * FLAT * 4);
-  ALLOC(e->act_l3, nE * FC * 4);
   const int64_t scrB = cfg->net.algo == A3C_ALGO_Q ? nE : E;
-  ALLOC(e->scr_l2, scrB * FLAT * 4);
-  ALLOC(e->scr_l3, scrB * FC * 4);
+  for (int k = 0; k < e->nslot; ++k) {
+    Slot& sl = e->slot[k];
+    if (e->overlap) {
+      ALLOC(sl.P, L.total * 4);
+      ALLOC(sl.tau, 64);
+    } else {
+      sl.P = e->params;
+      sl.tau = e->counters;
+    }
+    ALLOC(sl.actions, nE * 4);
+    ALLOC(sl.frames, nE * 4);
+    ALLOC(sl.rewards, nE * 4);
+    ALLOC(sl.terms, nE);
+    ALLOC(sl.z, (nE + E) * zs * 4);
+    ALLOC(sl.R_buf, nE * 4);
+    ALLOC(sl.act_l1, nE * C1_P * C1_N * 4);
+    ALLOC(sl.act_l2, nE * FLAT * 4);
+    ALLOC(sl.act_l3, nE * FC * 4);
+    ALLOC(sl.scr_l2, scrB * FLAT * 4);
+    ALLOC(sl.scr_l3, scrB * FC * 4);
+  }
   ALLOC(e->zt, scrB * zs * 4);
   ALLOC(e->eps, E * 4);
   ALLOC(e->ep_end, E * 4);
@@ -181,6 +222,17 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   if (a3c_make_tab(L.nt, L.off, L.size, L.total, &e->tt)) {
     a3c_engine_destroy(e);
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "tensor table");
+  }
+  if (e->overlap) {
+    bool ok = hipStreamCreateWithFlags(&e->rs, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&e->ev_start, hipEventDisableTiming) == hipSuccess;
+    for (int k = 0; k < 2 && ok; ++k)
+      ok = hipEventCreateWithFlags(&e->ev_snap[k], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&e->ev_roll[k], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+      a3c_engine_destroy(e);
+      return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "stream/event creation failed");
+    }
   }
   e->envp.k0 = e->k0; e->envp.k1 = e->k1;
   e->envp.P = cfg->num_frames;
@@ -218,7 +270,7 @@ __global__ void k_eps(float* __restrict__ eps, const float* __restrict__ ep_end,
   eps[i] = (float)v;
 }
 
-static StateAddr ring_addr(const a3c_engine* e, int tau_offset) {
+static StateAddr ring_addr(const a3c_engine* e, int tau_offset, const int64_t* tau_ptr) {
   StateAddr sa;
   sa.base = e->ring;
   sa.env_stride = (int64_t)e->R * PLANE;
@@ -227,9 +279,11 @@ static StateAddr ring_addr(const a3c_engine* e, int tau_offset) {
   sa.R = e->R;
   sa.L = HIST;
   sa.tau_offset = tau_offset;
-  sa.tau_ptr = e->counters;
+  sa.tau_ptr = tau_ptr;
   return sa;
 }
+
+__global__ void k_advance_tau(int64_t* counters, int n) { counters[0] += n; }
 
 static OptParams opt_params(const a3c_engine* e) {
   const a3c_engine_config& c = e->cfg;
@@ -243,14 +297,16 @@ static OptParams opt_params(const a3c_engine* e) {
   op.target_period = e->L.algo == A3C_ALGO_Q ? c.target_q_update_step : 0;
   op.target = e->L.algo == A3C_ALGO_Q ? e->tparams : nullptr;
   op.counters = e->counters;
-  op.dtau = e->n;
+  op.dtau = e->overlap ? 0 : e->n;   // overlap: the rollout advances tau itself
   op.rho = c.decay;
   op.momentum = c.momentum;
   op.eps = c.epsilon;
   return op;
 }
 
-static int enqueue_rollout_grad(a3c_engine* e, hipStream_t s) {
+// n env steps of every env (forward + action draw + env act fused into the head, then the
+// Environment.screen of the new frames into the ring) and the bootstrap forward.
+static int enqueue_rollout(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
   const NetLayout& L = e->L;
   const int E = e->E, n = e->n, zs = L.zs;
@@ -268,44 +324,63 @@ static int enqueue_rollout_grad(a3c_engine* e, hipStream_t s) {
     sel.tau_ptr = e->counters; sel.tau_add = t;
     sel.env_ids = nullptr; sel.env_id_base = c.env_id_base; sel.E = E;
     sel.eps = e->eps;
-    sel.actions = e->actions + (int64_t)t * E;
     const int64_t o = (int64_t)t * E;
+    sel.actions = sl.actions + o;
     sel.env_on = 1;
+    sel.par_E = E;
     sel.envp = e->envp;
     sel.envb = e->env;
-    sel.rewards = e->rewards + o;
-    sel.terms = e->terms + o;
-    sel.frames_out = e->frames + o;
-    rc = a3c_forward_launch(L, e->params, ring_addr(e, t), E, e->act_l1 + o * C1_P * C1_N, e->act_l2 + o * FLAT,
-                            e->act_l3 + o * FC, e->z + o * zs, e->fslab_e, e->fsplit_e, sel, s);
+    sel.rewards = sl.rewards + o;
+    sel.terms = sl.terms + o;
+    sel.frames_out = sl.frames + o;
+    rc = a3c_forward_launch(L, sl.P, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
+                            sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, e->fslab_e, e->fsplit_e, sel, s);
     if (rc) return rc;
-    rc = a3c_env_screen_launch(E, e->frames + o, e->pool, e->ring, e->R, e->counters, t, s);
+    rc = a3c_env_screen_launch(E, sl.frames + o, e->pool, e->ring, e->R, e->counters, t, s);
     if (rc) return rc;
   }
-  HeadSelect none = {};
-  none.mode = -1;
-  none.E = E;
   if (!q) {
     // bootstrap V(s_{t+n}) with the same parameters (assets/a3c.png)
-    rc = a3c_forward_launch(L, e->params, ring_addr(e, n), E, nullptr, e->scr_l2, e->scr_l3, e->z + e->nE * zs,
-                            e->fslab_e, e->fsplit_e, none, s);
-    if (rc) return rc;
-  } else {
-    // target network on s_{t+1} for every transition (agent.py:186)
+    HeadSelect none = {};
+    none.mode = -1;
     none.E = E;
-    rc = a3c_forward_launch(L, e->tparams, ring_addr(e, 1), e->nE, nullptr, e->scr_l2, e->scr_l3, e->zt,
+    rc = a3c_forward_launch(L, sl.P, ring_addr(e, n, e->counters), E, nullptr, sl.scr_l2, sl.scr_l3,
+                            sl.z + e->nE * zs, e->fslab_e, e->fsplit_e, none, s);
+    if (rc) return rc;
+  }
+  if (e->overlap) {
+    hipLaunchKernelGGL(k_advance_tau, dim3(1), dim3(1), 0, s, e->counters, n);
+    A3C_CHECK(hipGetLastError());
+  }
+  return 0;
+}
+
+// returns / TD target, loss + backward over the slot's n*E samples, per-tensor norms (+ the
+// per-worker clip when gradients are exchanged across GPUs).
+static int enqueue_grad(a3c_engine* e, const Slot& sl, hipStream_t s) {
+  const a3c_engine_config& c = e->cfg;
+  const NetLayout& L = e->L;
+  const int E = e->E, n = e->n, zs = L.zs;
+  const bool q = L.algo == A3C_ALGO_Q;
+  int rc;
+  if (q) {
+    // target network on s_{t+1} for every transition (agent.py:186)
+    HeadSelect none = {};
+    none.mode = -1;
+    none.E = E;
+    rc = a3c_forward_launch(L, e->tparams, ring_addr(e, 1, sl.tau), e->nE, nullptr, sl.scr_l2, sl.scr_l3, e->zt,
                             e->fslab_b, e->fsplit_b, none, s);
     if (rc) return rc;
-    rc = a3c_td_target_launch(e->rewards, e->terms, e->zt, e->nE, L.A, zs, c.discount, e->R_buf, s);
+    rc = a3c_td_target_launch(sl.rewards, sl.terms, e->zt, e->nE, L.A, zs, c.discount, sl.R_buf, s);
     if (rc) return rc;
   }
   ReturnsArgs ra = {};
   if (!q) {   // n-step returns computed inside the head backward (assets/a3c.png)
-    ra.rewards = e->rewards; ra.terms = e->terms; ra.boot = e->z + e->nE * zs + L.A; ra.boot_stride = zs;
-    ra.n = n; ra.E = E; ra.gamma = c.gamma; ra.R_out = e->R_buf;
+    ra.rewards = sl.rewards; ra.terms = sl.terms; ra.boot = sl.z + e->nE * zs + L.A; ra.boot_stride = zs;
+    ra.n = n; ra.E = E; ra.gamma = c.gamma; ra.R_out = sl.R_buf;
   }
-  rc = a3c_backward_launch(L, e->params, ring_addr(e, 0), e->nE, e->act_l1, e->act_l2, e->act_l3, e->z,
-                           e->actions, e->R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra);
+  rc = a3c_backward_launch(L, sl.P, ring_addr(e, 0, sl.tau), e->nE, sl.act_l1, sl.act_l2, sl.act_l3, sl.z,
+                           sl.actions, sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra);
   if (rc) return rc;
   // per-tensor squared norms (+ lr / target-sync schedule from the device step counter)
   OptParams op = opt_params(e);
@@ -316,6 +391,43 @@ static int enqueue_rollout_grad(a3c_engine* e, hipStream_t s) {
     op.mode = OPT_CLIP;
     return a3c_apply_launch(nullptr, nullptr, nullptr, e->grads, e->tt, op, e->opt_part, e->sumsq, s);
   }
+  return 0;
+}
+
+static int enqueue_rollout_grad(a3c_engine* e, hipStream_t s) {
+  int rc = enqueue_rollout(e, e->slot[0], s);
+  return rc ? rc : enqueue_grad(e, e->slot[0], s);
+}
+
+// Graph gi (0: sync rollout+grad; 1, 2: rollout of slot 0, 1; 3, 4: grad of slot 0, 1) is
+// captured on first use (what: 0 rollout+grad, 1 rollout, 2 grad) and launched on s.
+static int run_graph(a3c_engine* e, int gi, int what, int slot, hipStream_t s) {
+  if (gi < 0 || gi >= 5) return a3c_set_error(A3C_ERR_INVALID, "run_graph", "graph index");
+  auto enqueue = [&](hipStream_t cs) -> int {
+    if (what == 0) return enqueue_rollout_grad(e, cs);
+    if (what == 1) return enqueue_rollout(e, e->slot[slot], cs);
+    return enqueue_grad(e, e->slot[slot], cs);
+  };
+  if (!e->cfg.use_graph) return enqueue(s);
+  if (!e->captured[gi]) {
+    hipStream_t cs;
+    A3C_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    A3C_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue(cs);
+    hipGraph_t g;
+    hipError_t st = hipStreamEndCapture(cs, &g);
+    (void)hipStreamDestroy(cs);
+    if (rc) return rc;
+    if (st != hipSuccess) return a3c_set_error((int)st, "a3c_engine_rollout_grad", "capture failed");
+    st = hipGraphInstantiate(&e->gexec[gi], g, nullptr, nullptr, 0);
+    if (st != hipSuccess) {
+      (void)hipGraphDestroy(g);
+      return a3c_set_error((int)st, "a3c_engine_rollout_grad", "instantiate failed");
+    }
+    e->graph[gi] = g;
+    e->captured[gi] = true;
+  }
+  A3C_CHECK(hipGraphLaunch(e->gexec[gi], s));
   return 0;
 }
 
@@ -338,6 +450,8 @@ extern "C" int a3c_engine_reset(a3c_engine* e, const float* host_params, void* s
   if (rc) return rc;
   rc = a3c_env_init_launch(e->envp, e->env, e->E, e->pool, e->ring, e->R, e->counters, s);
   if (rc) return rc;
+  e->iter = 0;
+  e->grad_ready = false;
   e->reset_done = true;
   return 0;
 }
@@ -346,56 +460,73 @@ extern "C" int a3c_engine_rollout_grad(a3c_engine* e, void* stream) {
   if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_rollout_grad", "null");
   if (!e->reset_done) return a3c_set_error(A3C_ERR_STATE, "a3c_engine_rollout_grad", "call a3c_engine_reset first");
   hipStream_t s = (hipStream_t)stream;
-  if (!e->cfg.use_graph) return enqueue_rollout_grad(e, s);
-  if (!e->captured) {
-    hipStream_t cs;
-    A3C_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-    A3C_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue_rollout_grad(e, cs);
-    hipGraph_t g;
-    hipError_t st = hipStreamEndCapture(cs, &g);
-    (void)hipStreamDestroy(cs);
-    if (rc) return rc;
-    if (st != hipSuccess) return a3c_set_error((int)st, "a3c_engine_rollout_grad", "capture failed");
-    st = hipGraphInstantiate(&e->gexec, g, nullptr, nullptr, 0);
-    if (st != hipSuccess) {
-      (void)hipGraphDestroy(g);
-      return a3c_set_error((int)st, "a3c_engine_rollout_grad", "instantiate failed");
-    }
-    e->graph = g;
-    e->captured = true;
+  if (!e->overlap) {
+    int rc = run_graph(e, 0, 0, 0, s);
+    e->grad_ready = rc == 0;
+    return rc;
   }
-  A3C_CHECK(hipGraphLaunch(e->gexec, s));
+  // overlap: rollout k (slot p) on the engine's rollout stream, after everything the caller
+  // enqueued so far (in steady state: the apply of rollout k-2, whose parameters it snapshots);
+  // the backward of rollout k-1 (slot p^1) on the caller's stream, after that rollout and after
+  // rollout k has taken its parameter snapshot (the caller's apply rewrites the parameters).
+  const int p = (int)(e->iter & 1);
+  const Slot& sl = e->slot[p];
+  A3C_CHECK(hipEventRecord(e->ev_start, s));
+  A3C_CHECK(hipStreamWaitEvent(e->rs, e->ev_start, 0));
+  A3C_CHECK(hipMemcpyAsync(sl.P, e->params, e->L.total * 4, hipMemcpyDeviceToDevice, e->rs));
+  A3C_CHECK(hipMemcpyAsync(sl.tau, e->counters, 8, hipMemcpyDeviceToDevice, e->rs));
+  A3C_CHECK(hipEventRecord(e->ev_snap[p], e->rs));
+  int rc = run_graph(e, 1 + p, 1, p, e->rs);
+  if (rc) return rc;
+  A3C_CHECK(hipEventRecord(e->ev_roll[p], e->rs));
+  e->grad_ready = false;
+  if (e->iter >= 1) {
+    A3C_CHECK(hipStreamWaitEvent(s, e->ev_roll[p ^ 1], 0));
+    A3C_CHECK(hipStreamWaitEvent(s, e->ev_snap[p], 0));
+    rc = run_graph(e, 3 + (p ^ 1), 2, p ^ 1, s);
+    if (rc) return rc;
+    e->grad_ready = true;
+  }
+  e->iter += 1;
   return 0;
 }
+
+extern "C" int a3c_engine_grad_ready(a3c_engine* e) { return e && e->grad_ready ? 1 : 0; }
 
 // RMSProp apply (lr from the schedule computed on device), target sync (q) and the counter
 // advance, all in one launch.  world_size == 1: the per-tensor clip is applied here as well.
 extern "C" int a3c_engine_apply(a3c_engine* e, void* stream) {
   if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_apply", "null");
   hipStream_t s = (hipStream_t)stream;
+  if (!e->grad_ready) return 0;          // overlap pipeline still filling: nothing to apply
   OptParams op = opt_params(e);
   op.mode = e->cfg.world_size > 1 ? OPT_APPLY : (OPT_CLIP | OPT_APPLY);
   return a3c_apply_launch(e->params, e->ms, e->mom, e->grads, e->tt, op, e->opt_part,
                           e->cfg.world_size > 1 ? nullptr : e->sumsq, s);
 }
 
-extern "C" int a3c_engine_get_buffers(a3c_engine* e, a3c_engine_buffers* b) {
-  if (!e || !b) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_get_buffers", "null");
+extern "C" int a3c_engine_slot_buffers(a3c_engine* e, int slot, a3c_engine_buffers* b) {
+  if (!e || !b || slot < 0 || slot >= e->nslot)
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_slot_buffers", "bad argument");
+  const Slot& sl = e->slot[slot];
   memset(b, 0, sizeof(*b));
   b->params = e->params; b->target_params = e->tparams; b->ms = e->ms; b->mom = e->mom; b->grads = e->grads;
   b->n_params = e->L.total;
   b->frame_ring = e->ring; b->ring_slots = e->R;
   b->tau = e->counters; b->global_step = e->counters + 1;
-  b->actions = e->actions; b->rewards = e->rewards; b->terminals = e->terms;
-  b->z = e->z; b->returns = e->R_buf; b->loss = e->loss; b->sumsq = e->sumsq;
-  b->act_l1 = e->act_l1; b->act_l2 = e->act_l2; b->act_l3 = e->act_l3;
+  b->actions = sl.actions; b->rewards = sl.rewards; b->terminals = sl.terms;
+  b->z = sl.z; b->returns = sl.R_buf; b->loss = e->loss; b->sumsq = e->sumsq;
+  b->act_l1 = sl.act_l1; b->act_l2 = sl.act_l2; b->act_l3 = sl.act_l3;
   b->frame_pool = e->pool;
   b->env_frame = e->env.frame; b->env_lives = e->env.lives; b->env_episode = e->env.episode;
   b->env_step = e->env.ep_step; b->env_len = e->env.ep_len;
   b->zs = e->L.zs; b->n_tensors = e->L.nt;
   for (int i = 0; i < e->L.nt; ++i) { b->offsets[i] = e->L.off[i]; b->sizes[i] = e->L.size[i]; }
   return 0;
+}
+
+extern "C" int a3c_engine_get_buffers(a3c_engine* e, a3c_engine_buffers* b) {
+  return a3c_engine_slot_buffers(e, 0, b);
 }
 
 // ---- profiling hook: average duration of one engine kernel, HIP events on the caller's stream ----
@@ -405,17 +536,19 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
   hipStream_t s = (hipStream_t)stream;
   const NetLayout& L = e->L;
   const int E = e->E;
+  const Slot& sl = e->slot[0];
+  if (e->rs) A3C_CHECK(hipStreamSynchronize(e->rs));
   auto launch = [&]() -> int {
     switch (kernel) {
       case A3C_KER_CONV12_FWD:
-        return a3c_conv12_launch(L, e->params, ring_addr(e, 0), E, e->act_l1, e->act_l2, s);
+        return a3c_conv12_launch(L, e->params, ring_addr(e, 0, e->counters), E, sl.act_l1, sl.act_l2, s);
       case A3C_KER_FC_FWD:
-        return a3c_fc_fwd_launch(e->act_l2, e->params + L.off[T_FCW], e->params + L.off[T_FCB], e->act_l3, E, s);
+        return a3c_fc_fwd_launch(sl.act_l2, e->params + L.off[T_FCW], e->params + L.off[T_FCB], sl.act_l3, E, s);
       case A3C_KER_ENV_STEP:
-        return a3c_env_screen_launch(E, e->frames, e->pool, e->ring, e->R, e->counters, 0, s);
+        return a3c_env_screen_launch(E, sl.frames, e->pool, e->ring, e->R, e->counters, 0, s);
       case A3C_KER_CONV_BWD: {
         const BwdPlan p = a3c_bwd_plan(L, e->nE);
-        return a3c_conv_bwd_launch(L, e->params, ring_addr(e, 0), e->nE, e->act_l1, e->ws + p.dl2, e->ws, s);
+        return a3c_conv_bwd_launch(L, e->params, ring_addr(e, 0, e->counters), e->nE, sl.act_l1, e->ws + p.dl2, e->ws, s);
       }
       default:
         return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_time_kernel", "unknown kernel id");

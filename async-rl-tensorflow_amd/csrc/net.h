@@ -88,6 +88,8 @@ struct HeadSelect {
   // fused env step (engine rollout): act() on the drawn action right after predict, as the
   // reference worker does (agent.py:59-62); env state double-buffered by (tau & 1)
   int env_on;
+  int par_E;                // env-state parity stride (all envs of the engine); envb is
+                            // pre-offset to this launch's first env
   EnvParams envp;
   EnvBufs envb;
   float* rewards;           // [E] observe-clipped reward (agent.py:154)

@@ -202,7 +202,7 @@ __global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, 
       if (sel.env_on) {
         const int64_t tau = *sel.tau_ptr + sel.tau_add;
         const int e = (int)b;
-        const int64_t cur = (tau & 1) * (int64_t)sel.E + e, nxt = ((tau + 1) & 1) * (int64_t)sel.E + e;
+        const int64_t cur = (tau & 1) * (int64_t)sel.par_E + e, nxt = ((tau + 1) & 1) * (int64_t)sel.par_E + e;
         const uint32_t id = (uint32_t)(sel.env_id_base + e);
         EnvState s = env_load(sel.envb, cur);
         env_act(s, sel.envp, id, (uint32_t)a, true);

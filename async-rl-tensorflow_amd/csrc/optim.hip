@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(256) k_apply(float* __restrict__ w, float* __r
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && op.counters) {
-    op.counters[0] += op.dtau;
+    if (op.dtau) op.counters[0] += op.dtau;   // overlap mode: the rollout owns tau
     op.counters[1] += op.step_add;
   }
 }

@@ -36,7 +36,7 @@ class EngineConfig(ctypes.Structure):
                 ('max_step', c_i64), ('decay', c_float), ('momentum', c_float), ('epsilon', c_float),
                 ('clip_norm', c_float), ('literal_adv', c_int), ('ep_start', c_float),
                 ('ep_end', c_float), ('ep_end_t', c_i64), ('learn_start', c_i64),
-                ('target_q_update_step', c_i64), ('discount', c_double)]
+                ('target_q_update_step', c_i64), ('discount', c_double), ('overlap', c_int)]
 
 
 class EngineBuffers(ctypes.Structure):
@@ -99,6 +99,8 @@ SIGNATURES = {
     'a3c_engine_rollout_grad': (c_int, [c_void_p, c_void_p]),
     'a3c_engine_apply': (c_int, [c_void_p, c_void_p]),
     'a3c_engine_get_buffers': (c_int, [c_void_p, ctypes.POINTER(EngineBuffers)]),
+    'a3c_engine_slot_buffers': (c_int, [c_void_p, c_int, ctypes.POINTER(EngineBuffers)]),
+    'a3c_engine_grad_ready': (c_int, [c_void_p]),
     'a3c_engine_time_kernel': (c_int, [c_void_p, c_int, c_int, c_void_p, ctypes.POINTER(c_float)]),
 }
 

@@ -6,6 +6,11 @@ target-net forward, returns, loss + backward, per-tensor clip, then the optional
 gradient exchange (``exchange`` callback, e.g. an RCCL all-reduce) and the RMSProp apply.
 It replaces the per-worker loop of agent.py:52-67 (+ observe/batch_update :153-207) and the
 parameter-server apply of main.py:60-66.
+
+``overlap=True`` pipelines the engine: rollout k runs on an engine-owned stream with the
+parameters after update k-2 while the backward, exchange and apply of rollout k-1 run on the
+caller's stream (A3C's stale-parameter asynchrony at a fixed staleness of one update).  Rollout
+k's buffers are ``slot(k & 1)``.
 """
 import ctypes
 
@@ -38,7 +43,7 @@ def _view(ptr, shape, dtype):
 
 class Engine:
     def __init__(self, num_envs=256, n_step=5, action_size=6, algo='a3c', start_lives=0, num_frames=1024,
-                 seed=123, env_id_base=0, world_size=1, use_graph=True, **overrides):
+                 seed=123, env_id_base=0, world_size=1, use_graph=True, overlap=False, **overrides):
         _lib.require_device()
         cfg = _lib.EngineConfig()
         lib().a3c_engine_config_default(ctypes.byref(cfg))
@@ -51,6 +56,8 @@ class Engine:
         cfg.env_id_base = int(env_id_base)
         cfg.world_size = int(world_size)
         cfg.use_graph = 1 if use_graph else 0
+        cfg.overlap = 1 if overlap else 0
+        self.overlap = bool(overlap)
         for k, v in overrides.items():
             if not hasattr(cfg, k):
                 raise ValueError(f'unknown engine option {k}')
@@ -77,16 +84,11 @@ class Engine:
         self.frame_ring = _view(b.frame_ring, (E, b.ring_slots, 84, 84), torch.uint8)
         self.ring_slots = int(b.ring_slots)
         self.counters = _view(b.tau, (2,), torch.int64)
-        self.actions = _view(b.actions, (n, E), torch.int32)
-        self.rewards = _view(b.rewards, (n, E), torch.float32)
-        self.terminals = _view(b.terminals, (n, E), torch.uint8)
-        self.z = _view(b.z, (n + 1, E, self.zs), torch.float32)
-        self.returns = _view(b.returns, (n, E), torch.float32)
         self.loss = _view(b.loss, (4,), torch.float32)
         self.sumsq = _view(b.sumsq, (b.n_tensors,), torch.float32)
-        self.act_l1 = _view(b.act_l1, (n * E, 6400), torch.float32)
-        self.act_l2 = _view(b.act_l2, (n * E, 2592), torch.float32)
-        self.act_l3 = _view(b.act_l3, (n * E, 256), torch.float32)
+        self._slots = [self._slot_views(k) for k in range(2 if self.overlap else 1)]
+        for k, v in self._slots[0].items():
+            setattr(self, k, v)
         self.frame_pool = _view(b.frame_pool, (int(cfg.num_frames), 210, 160, 3), torch.uint8)
         # env state is double-buffered by step parity: the current state lives at tau & 1
         self._env = {'frame': _view(b.env_frame, (2, E), torch.int32),
@@ -94,6 +96,23 @@ class Engine:
                      'episode': _view(b.env_episode, (2, E), torch.int32),
                      'ep_step': _view(b.env_step, (2, E), torch.int32),
                      'ep_len': _view(b.env_len, (2, E), torch.int32)}
+
+    def _slot_views(self, k):
+        b = _lib.EngineBuffers()
+        check(lib().a3c_engine_slot_buffers(self._h, k, ctypes.byref(b)), 'a3c_engine_slot_buffers')
+        E, n = self.E, self.n
+        return dict(actions=_view(b.actions, (n, E), torch.int32),
+                    rewards=_view(b.rewards, (n, E), torch.float32),
+                    terminals=_view(b.terminals, (n, E), torch.uint8),
+                    z=_view(b.z, (n + 1, E, self.zs), torch.float32),
+                    returns=_view(b.returns, (n, E), torch.float32),
+                    act_l1=_view(b.act_l1, (n * E, 6400), torch.float32),
+                    act_l2=_view(b.act_l2, (n * E, 2592), torch.float32),
+                    act_l3=_view(b.act_l3, (n * E, 256), torch.float32))
+
+    def slot(self, k):
+        """Rollout buffers of slot k (overlap: rollout i lives in slot i & 1)."""
+        return self._slots[k]
 
     def env_field(self, name):
         """Current synthetic-env state field [E] (frame, lives, episode, ep_step, ep_len)."""
@@ -133,8 +152,14 @@ class Engine:
     def apply(self):
         check(lib().a3c_engine_apply(self._h, _lib.stream_handle()), 'a3c_engine_apply')
 
+    @property
+    def grad_ready(self):
+        return bool(lib().a3c_engine_grad_ready(self._h))
+
     def iterate(self, exchange=None):
         self.rollout_grad()
+        if not self.grad_ready:          # overlap pipeline filling: no gradient yet
+            return
         if exchange is not None:
             exchange(self.grads)
         self.apply()

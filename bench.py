@@ -47,6 +47,8 @@ def parse():
     ap.add_argument('--algo', default='a3c', choices=['a3c', 'q'])
     ap.add_argument('--frames', type=int, default=16384, help='HBM frame pool (16384 = 1.65 GB > L3)')
     ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--overlap', type=int, default=1, choices=[0, 1],
+                    help='1: rollout k overlaps backward+apply of rollout k-1 (stale-1 async A3C)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
@@ -110,7 +112,8 @@ def main():
     A, lives = GAMES[args.game]
     E, n = args.envs, args.n_step
     eng = Engine(num_envs=E, n_step=n, action_size=A, algo=args.algo, start_lives=lives, num_frames=args.frames,
-                 seed=123, env_id_base=rank * E, world_size=world, use_graph=not args.no_graph)
+                 seed=123, env_id_base=rank * E, world_size=world, use_graph=not args.no_graph,
+                 overlap=bool(args.overlap))
     ns = param_names_shapes(A, args.algo)
     params = flatten_host(ns, eng.offsets, eng.params.numel(), init_params(ns, seed=123))
     eng.reset(params)     # every rank starts from the same parameters
@@ -147,15 +150,15 @@ def main():
         ms = {
             'k_conv12_fwd': eng.time_kernel(_lib.KER_CONV12_FWD, 20),
             'k_conv_bwd': eng.time_kernel(_lib.KER_CONV_BWD, 10),
-            'k_gemm_f32(fc fwd)+reduce': eng.time_kernel(_lib.KER_FC_FWD, 20),
-            'k_env_step': eng.time_kernel(_lib.KER_ENV_STEP, 20),
+            'k_fc_fwd': eng.time_kernel(_lib.KER_FC_FWD, 20),
+            'k_env_screen': eng.time_kernel(_lib.KER_ENV_STEP, 20),
         }
-        count = {'k_conv12_fwd': n + 1, 'k_conv_bwd': 1, 'k_gemm_f32(fc fwd)+reduce': n + 1, 'k_env_step': n}
+        count = {'k_conv12_fwd': n + 1, 'k_conv_bwd': 1, 'k_fc_fwd': n + 1, 'k_env_screen': n}
         work = {
             'k_conv12_fwd': ('mfma', CONV12_FWD_FLOP * E),
             'k_conv_bwd': ('mfma', CONV_BWD_FLOP * n * E),
-            'k_gemm_f32(fc fwd)+reduce': ('mfma', FC_FWD_FLOP * E),
-            'k_env_step': ('hbm', ENV_STEP_BYTES * E),
+            'k_fc_fwd': ('mfma', FC_FWD_FLOP * E),
+            'k_env_screen': ('hbm', ENV_STEP_BYTES * E),
         }
         iter_ms = el / args.steps * 1e3
         for k in ms:
@@ -167,11 +170,14 @@ def main():
         dom = max(ms, key=lambda k: ms[k] * count[k])
         bound, w = work[dom]
         peak = PEAK_FP32_TFLOPS if bound == 'mfma' else PEAK_HBM_GBS
+        # HBM bytes per launch from the committed PMC passes (tools/profile_round.sh):
+        # (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 FETCH_SIZE correction per MI355X_MICROARCH.md
         traffic = None
         pmc = os.path.join(ROOT, 'profiles', 'pmc_hbm_bytes.json')
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get(dom.split('(')[0])
+                t = json.load(open(pmc))['hbm_bytes_per_launch'].get(dom)
+                traffic = None if t is None else int(round(t))
             except Exception:
                 traffic = None
         roofline = dict(kernel=dom, bound=bound, achieved=kernels[dom]['achieved'], peak=peak,
@@ -197,7 +203,10 @@ def main():
                        'game': args.game, 'envs_per_gpu': E, 'n_step': n, 'action_size': A, 'algo': args.algo,
                        'env_steps_per_step': world * E * n,
                        'parallelism': f'dp{world} sync all-reduce (RCCL) of per-worker-clipped grads'
-                       if world > 1 else 'dp1', 'hipgraph': not args.no_graph},
+                       if world > 1 else 'dp1', 'hipgraph': not args.no_graph,
+                       'update': 'overlap: rollout k uses params after update k-2 (A3C stale-1 async), '
+                                 'backward+apply of k-1 concurrent' if args.overlap else
+                                 'synchronous: rollout -> backward -> apply'},
             'roofline': roofline, 'cpu_baseline': cpu, 'kernels': kernels,
             'final_loss': loss, 'params_finite': finite,
         }

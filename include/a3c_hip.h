@@ -225,6 +225,10 @@ typedef struct a3c_engine_config {
   float ep_start, ep_end; int64_t ep_end_t, learn_start;  /* config.py:18-25         */
   int64_t target_q_update_step;   /* config.py:10 (4e4)                               */
   double discount;                /* config.py:9                                      */
+  int overlap;        /* 1 (a3c only): rollout k runs on an engine stream while the backward +
+                        apply of rollout k-1 run on the caller's stream; rollout k uses the
+                        parameters after update k-2 (A3C stale-parameter asynchrony, fixed
+                        staleness 1).  0: synchronous rollout -> grad -> apply.          */
 } a3c_engine_config;
 
 void a3c_engine_config_default(a3c_engine_config* cfg);
@@ -236,8 +240,12 @@ int a3c_engine_destroy(a3c_engine* eng);
 int a3c_engine_reset(a3c_engine* eng, const float* host_params, void* stream);
 /* n rollout steps + bootstrap + loss + backward + per-tensor clip -> grads */
 int a3c_engine_rollout_grad(a3c_engine* eng, void* stream);
-/* RMSProp apply of grads (lr from the device global step) and advance counters */
+/* RMSProp apply of grads (lr from the device global step) and advance counters.
+ * overlap: a no-op until the pipeline holds a gradient (first call after reset). */
 int a3c_engine_apply(a3c_engine* eng, void* stream);
+/* 1 if the last a3c_engine_rollout_grad produced a gradient (always, unless overlap and it
+ * was the first call after reset) -- exchange / apply only then. */
+int a3c_engine_grad_ready(a3c_engine* eng);
 
 /* device pointers owned by the engine (valid until destroy) */
 typedef struct a3c_engine_buffers {
@@ -261,6 +269,9 @@ typedef struct a3c_engine_buffers {
   int zs; int n_tensors; int64_t offsets[A3C_MAX_TENSORS]; int64_t sizes[A3C_MAX_TENSORS];
 } a3c_engine_buffers;
 int a3c_engine_get_buffers(a3c_engine* eng, a3c_engine_buffers* out);
+/* same, with the rollout buffers (actions .. act_l3) of slot 0 or 1 (overlap: rollout k
+ * writes slot k & 1); get_buffers == slot 0 */
+int a3c_engine_slot_buffers(a3c_engine* eng, int slot, a3c_engine_buffers* out);
 
 /* profiling hook: average device time (ms) of `iters` back-to-back launches of one engine
  * kernel on its live buffers, bracketed by HIP events on `stream` (idempotent: each

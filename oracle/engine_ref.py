@@ -145,7 +145,9 @@ class EngineRef:
         out.update(losses=losses, grads=grads, sumsq=sumsq, clipped=clipped, z_batch=fwd['z'])
         return out
 
-    def apply(self, clipped):
+    def apply(self, clipped, advance_tau=True):
+        """RMSProp apply (+ q target sync).  advance_tau=False: the caller advances tau at
+        rollout time (the engine's overlap pipeline, where rollout k+1 precedes apply k)."""
         h = self.h
         inc = self.n * self.E * self.world
         lr = R.learning_rate(self.global_step + inc, h['max_step'], h['learning_rate'])
@@ -156,6 +158,7 @@ class EngineRef:
             P = h['target_q_update_step']
             if (self.global_step + inc + 1) // P != (self.global_step + 1) // P:   # agent.py:166-167
                 self.tparams = {k: v.copy() for k, v in self.params.items()}
-        self.tau += self.n
+        if advance_tau:
+            self.tau += self.n
         self.global_step += inc
         return lr

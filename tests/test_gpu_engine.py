@@ -29,7 +29,7 @@ def build(algo, A, E, n, lives, seed, frames=48, use_graph=True, scale=4.0, **kw
     p = init_params(ns, seed=seed, stddev=0.02 * scale)
     eng.reset(flatten_host(ns, eng.offsets, eng.params.numel(), p))
     ref = EngineRef(p, E, n, A, algo, lives, frames, seed, **{k: v for k, v in kw.items() if k in
-                                                              ('target_q_update_step',)})
+                                                              ('target_q_update_step', 'learning_rate')})
     ref.reset()
     return eng, ref, ns
 
@@ -152,3 +152,82 @@ def test_engine_bench_shape_runs():
     assert torch.isfinite(eng.loss).all()
     acts = eng.actions.cpu().numpy()
     assert acts.min() >= 0 and acts.max() < 6
+
+
+# ------------------------------------------------------------------ overlap (stale-1) pipeline
+def _same_act_grads(slot, planes, P, algo, A, n, E, tgt):
+    """oracle backward of one rollout on the engine's saved activations of that rollout's slot."""
+    B = n * E
+    l1 = slot['act_l1'].cpu().numpy().astype(np.float64).reshape(B, 20, 20, 16)
+    l2 = slot['act_l2'].cpu().numpy().astype(np.float64)
+    zw = A + 1 if algo == 'a3c' else A
+    z = slot['z'].cpu().numpy()[:n].reshape(B, -1)[:, :zw].astype(np.float64)
+    fwd = dict(z=z, h3=slot['act_l3'].cpu().numpy().astype(np.float64), flat=l2,
+               acts=[Rc.states_nhwc(planes).astype(np.float64) / 255.0, l1, l2.reshape(B, 9, 9, 32)])
+    acts = slot['actions'].cpu().numpy().reshape(-1)
+    losses, dz = Rc.a3c_loss_and_dz(z, acts, tgt.reshape(-1).astype(np.float64), 0.01)
+    g = Rc.backward(P, fwd, dz, algo)
+    return losses, {k: np.asarray(v, np.float32).reshape(P[k].shape) for k, v in g.items()}
+
+
+def test_overlap_with_zero_lr_equals_sync():
+    """With learning_rate 0 staleness is invisible: the pipelined engine must reproduce the
+    synchronous engine's rollouts, losses and gradients bit for bit, one call later."""
+    s, _, _ = build('a3c', 6, 16, 5, 0, seed=31, learning_rate=0.0)
+    o, _, _ = build('a3c', 6, 16, 5, 0, seed=31, learning_rate=0.0, overlap=True)
+    assert o.ring_slots == 2 * 5 + 4 and s.ring_slots == 5 + 4
+    o.iterate()
+    torch.cuda.synchronize()
+    assert not o.grad_ready
+    for k in range(1, 5):
+        s.iterate()
+        o.iterate()
+        torch.cuda.synchronize()
+        assert o.grad_ready
+        prev = o.slot((k - 1) & 1)
+        assert torch.equal(prev['actions'], s.actions), k
+        assert torch.equal(prev['rewards'], s.rewards), k
+        assert torch.equal(prev['returns'], s.returns), k
+        assert torch.equal(o.grads, s.grads), k
+        assert torch.equal(o.loss, s.loss), k
+        assert torch.equal(o.params, s.params), k
+    assert int(o.counters[0].item()) == int(s.counters[0].item()) + 5     # one rollout ahead
+    assert int(o.counters[1].item()) == int(s.counters[1].item())
+
+
+def test_overlap_stale_semantics_match_oracle():
+    """Rollout k uses the parameters after update k-2 (staleness 1): replay that order on the
+    oracle with the engine's own actions and activations; parameters agree at 1e-5."""
+    A, E, n = 6, 8, 5
+    eng, ref, ns = build('a3c', A, E, n, 0, seed=77, overlap=True, learning_rate=3e-3)
+    hist = []                  # per rollout: (oracle params used, planes, oracle out)
+    for k in range(5):
+        eng.iterate()
+        torch.cuda.synchronize()
+        sl = eng.slot(k & 1)
+        Pk = {kk: v.copy() for kk, v in ref.params.items()}
+        out = ref.iterate(forced_actions=sl['actions'].cpu().numpy())
+        planes = np.concatenate([np.transpose(ref.states(ref.tau + t), (0, 3, 1, 2)) for t in range(n)])
+        ref.tau += n                                    # the rollout owns tau in overlap mode
+        assert np.array_equal(sl['rewards'].cpu().numpy(), out['rewards']), k
+        assert np.array_equal(sl['terminals'].cpu().numpy(), out['terminals']), k
+        agree = (sl['actions'].cpu().numpy() == out['sampled']).mean()
+        assert agree >= 0.98, (k, agree)
+        hist.append((Pk, planes, out))
+        if k == 0:
+            assert not eng.grad_ready
+            continue
+        Pp, planes_p, out_p = hist[k - 1]
+        slp = eng.slot((k - 1) & 1)
+        tgt = slp['returns'].cpu().numpy()
+        np.testing.assert_allclose(tgt, out_p['target'], rtol=1e-5, atol=1e-5)
+        losses, g_same = _same_act_grads(slp, planes_p, Pp, 'a3c', A, n, E, tgt)
+        loss = eng.loss.cpu().numpy()
+        for i, key in enumerate(('policy', 'value', 'entropy', 'total')):
+            assert abs(loss[i] - losses[key]) <= 1e-4 * max(1.0, abs(losses[key])), (k, key)
+        ref.apply({kk: Rc.clip_by_norm(v, 40.0) for kk, v in g_same.items()}, advance_tau=False)
+        P = unflat(eng, ns, eng.params)
+        for name, _ in ns:
+            d = np.abs(P[name] - ref.params[name]).max()
+            assert d <= 1e-5 * max(1.0, np.abs(ref.params[name]).max()), (k, name, d)
+        assert int(eng.counters[1].item()) == ref.global_step
