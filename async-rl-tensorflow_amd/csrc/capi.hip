@@ -55,10 +55,9 @@ extern "C" int a3c_workspace_bytes(const a3c_net_desc* net, int64_t B, int64_t* 
   NetLayout L;
   if (a3c_make_layout(net, &L) || B < 0 || !bytes)
     return a3c_set_error(A3C_ERR_INVALID, "a3c_workspace_bytes", "bad argument");
-  int split = 1;
-  int64_t f = a3c_fwd_slab_floats(B > 0 ? B : 1, &split);
+  // forward: the bf16-split conv1 weights; backward: its plan (they never run at once)
   BwdPlan p = a3c_bwd_plan(L, B > 0 ? B : 1);
-  int64_t m = f > p.total ? f : p.total;
+  int64_t m = p.total > W1S_ELEMS / 2 ? p.total : W1S_ELEMS / 2;
   *bytes = m * (int64_t)sizeof(float) + 256;
   return 0;
 }
@@ -87,14 +86,15 @@ extern "C" int a3c_forward(const a3c_net_desc* net, const float* params, const u
     return a3c_set_error(A3C_ERR_INVALID, "a3c_forward", "bad argument");
   if (B == 0) return 0;
   a3c_init_once();
-  int split = 1;
-  int64_t sf = a3c_fwd_slab_floats(B, &split);
-  if (sf && !workspace) return a3c_set_error(A3C_ERR_INVALID, "a3c_forward", "workspace required");
+  if (!workspace) return a3c_set_error(A3C_ERR_INVALID, "a3c_forward", "workspace required");
   HeadSelect sel = {};
   sel.mode = -1;
   sel.E = 1;
-  return a3c_forward_launch(L, params, contiguous_states(states, B), B, act_l1, act_l2, act_l3, z,
-                            sf ? align_ws(workspace) : nullptr, split, sel, (hipStream_t)stream);
+  uint16_t* w1s = (uint16_t*)align_ws(workspace);
+  int rc = a3c_split_w1_launch(params + L.off[T_L1W], w1s, (hipStream_t)stream);
+  if (rc) return rc;
+  return a3c_forward_launch(L, params, w1s, contiguous_states(states, B), B, act_l1, act_l2, act_l3, z, sel,
+                            (hipStream_t)stream);
 }
 
 extern "C" int a3c_select_action(int mode, const float* z, int64_t B, int zs, int A, const float* eps,

@@ -38,6 +38,7 @@ struct Slot {
   float* R_buf;            // [n][E] returns / TD targets
   float *act_l1, *act_l2, *act_l3;
   float *scr_l2, *scr_l3;  // bootstrap / target forward scratch
+  uint16_t* w1s;           // conv1 weights of P split into bf16 terms (net_fwd.hip)
 };
 
 struct a3c_engine {
@@ -57,11 +58,10 @@ struct a3c_engine {
   float* loss;
   float* sumsq;
   float* zt;               // q: target-net q values [nE][zs]
+  uint16_t* w1s_t;         // q: split conv1 weights of the target network
   float* eps;              // q: per env epsilon
   float* ep_end;           // q: per env final epsilon
   float* ws;               // backward workspace
-  float* fslab_e; int fsplit_e;
-  float* fslab_b; int fsplit_b;
   double* opt_part;
   float* sched;            // [0] lr, [1] target-sync flag (device)
   TensorTab tt;
@@ -206,16 +206,14 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     ALLOC(sl.act_l3, nE * FC * 4);
     ALLOC(sl.scr_l2, scrB * FLAT * 4);
     ALLOC(sl.scr_l3, scrB * FC * 4);
+    ALLOC(sl.w1s, W1S_ELEMS * 2);
   }
+  ALLOC(e->w1s_t, W1S_ELEMS * 2);
   ALLOC(e->zt, scrB * zs * 4);
   ALLOC(e->eps, E * 4);
   ALLOC(e->ep_end, E * 4);
   BwdPlan bp = a3c_bwd_plan(L, nE);
   ALLOC(e->ws, bp.total * 4);
-  int64_t f1 = a3c_fwd_slab_floats(E, &e->fsplit_e);
-  ALLOC(e->fslab_e, f1 * 4);
-  int64_t f2 = a3c_fwd_slab_floats(scrB, &e->fsplit_b);
-  ALLOC(e->fslab_b, f2 * 4);
   ALLOC(e->opt_part, (int64_t)SS_MAX_BLOCKS * 8);
   ALLOC(e->sched, 64);
 #undef ALLOC
@@ -311,7 +309,8 @@ static int enqueue_rollout(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const NetLayout& L = e->L;
   const int E = e->E, n = e->n, zs = L.zs;
   const bool q = L.algo == A3C_ALGO_Q;
-  int rc;
+  int rc = a3c_split_w1_launch(sl.P + L.off[T_L1W], sl.w1s, s);   // params are fixed for the rollout
+  if (rc) return rc;
   if (q) {
     hipLaunchKernelGGL(k_eps, dim3((E + 255) / 256), dim3(256), 0, s, e->eps, e->ep_end, E, e->counters,
                        c.ep_start, c.ep_end_t, c.learn_start);
@@ -333,8 +332,8 @@ static int enqueue_rollout(a3c_engine* e, const Slot& sl, hipStream_t s) {
     sel.rewards = sl.rewards + o;
     sel.terms = sl.terms + o;
     sel.frames_out = sl.frames + o;
-    rc = a3c_forward_launch(L, sl.P, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
-                            sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, e->fslab_e, e->fsplit_e, sel, s);
+    rc = a3c_forward_launch(L, sl.P, sl.w1s, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
+                            sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s);
     if (rc) return rc;
     rc = a3c_env_screen_launch(E, sl.frames + o, e->pool, e->ring, e->R, e->counters, t, s);
     if (rc) return rc;
@@ -344,8 +343,8 @@ static int enqueue_rollout(a3c_engine* e, const Slot& sl, hipStream_t s) {
     HeadSelect none = {};
     none.mode = -1;
     none.E = E;
-    rc = a3c_forward_launch(L, sl.P, ring_addr(e, n, e->counters), E, nullptr, sl.scr_l2, sl.scr_l3,
-                            sl.z + e->nE * zs, e->fslab_e, e->fsplit_e, none, s);
+    rc = a3c_forward_launch(L, sl.P, sl.w1s, ring_addr(e, n, e->counters), E, nullptr, sl.scr_l2, sl.scr_l3,
+                            sl.z + e->nE * zs, none, s);
     if (rc) return rc;
   }
   if (e->overlap) {
@@ -357,7 +356,16 @@ static int enqueue_rollout(a3c_engine* e, const Slot& sl, hipStream_t s) {
 
 // returns / TD target, loss + backward over the slot's n*E samples, per-tensor norms (+ the
 // per-worker clip when gradients are exchanged across GPUs).
+static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s);
 static int enqueue_grad(a3c_engine* e, const Slot& sl, hipStream_t s) {
+  // overlap: the backward shares CUs with the next rollout -> the small-LDS conv backward
+  a3c_conv_bwd_set_compact(e->overlap != 0);
+  int rc = enqueue_grad_impl(e, sl, s);
+  a3c_conv_bwd_set_compact(false);
+  return rc;
+}
+
+static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
   const NetLayout& L = e->L;
   const int E = e->E, n = e->n, zs = L.zs;
@@ -368,8 +376,10 @@ static int enqueue_grad(a3c_engine* e, const Slot& sl, hipStream_t s) {
     HeadSelect none = {};
     none.mode = -1;
     none.E = E;
-    rc = a3c_forward_launch(L, e->tparams, ring_addr(e, 1, sl.tau), e->nE, nullptr, sl.scr_l2, sl.scr_l3, e->zt,
-                            e->fslab_b, e->fsplit_b, none, s);
+    rc = a3c_split_w1_launch(e->tparams + L.off[T_L1W], e->w1s_t, s);
+    if (rc) return rc;
+    rc = a3c_forward_launch(L, e->tparams, e->w1s_t, ring_addr(e, 1, sl.tau), e->nE, nullptr, sl.scr_l2,
+                            sl.scr_l3, e->zt, none, s);
     if (rc) return rc;
     rc = a3c_td_target_launch(sl.rewards, sl.terms, e->zt, e->nE, L.A, zs, c.discount, sl.R_buf, s);
     if (rc) return rc;
@@ -538,16 +548,22 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
   const int E = e->E;
   const Slot& sl = e->slot[0];
   if (e->rs) A3C_CHECK(hipStreamSynchronize(e->rs));
+  if (kernel == A3C_KER_CONV12_FWD) {
+    int rc0 = a3c_split_w1_launch(e->params + L.off[T_L1W], sl.w1s, s);
+    if (rc0) return rc0;
+  }
   auto launch = [&]() -> int {
     switch (kernel) {
       case A3C_KER_CONV12_FWD:
-        return a3c_conv12_launch(L, e->params, ring_addr(e, 0, e->counters), E, sl.act_l1, sl.act_l2, s);
+        return a3c_conv12_launch(L, e->params, sl.w1s, ring_addr(e, 0, e->counters), E, sl.act_l1, sl.act_l2, s);
       case A3C_KER_FC_FWD:
         return a3c_fc_fwd_launch(sl.act_l2, e->params + L.off[T_FCW], e->params + L.off[T_FCB], sl.act_l3, E, s);
       case A3C_KER_ENV_STEP:
         return a3c_env_screen_launch(E, sl.frames, e->pool, e->ring, e->R, e->counters, 0, s);
       case A3C_KER_CONV_BWD: {
         const BwdPlan p = a3c_bwd_plan(L, e->nE);
+        a3c_conv_bwd_set_compact(e->overlap != 0);
+        struct Reset { ~Reset() { a3c_conv_bwd_set_compact(false); } } reset_compact;
         return a3c_conv_bwd_launch(L, e->params, ring_addr(e, 0, e->counters), e->nE, sl.act_l1, e->ws + p.dl2, e->ws, s);
       }
       default:

@@ -98,10 +98,12 @@ struct HeadSelect {
 };
 
 // forward of B states; returns 0 or error
-int a3c_forward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
-                       float* act_l1, float* act_l2, float* act_l3, float* z, float* slab,
-                       int fc_split, const HeadSelect& sel, hipStream_t s);
-int64_t a3c_fwd_slab_floats(int64_t B, int* split_out);
+// w1s: conv1 weights split into bf16 terms (a3c_split_w1_launch, W1S_ELEMS u16)
+int a3c_forward_launch(const NetLayout& L, const float* params, const uint16_t* w1s, const StateAddr& sa,
+                       int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
+                       hipStream_t s);
+#define W1S_ELEMS (C1_K * 3 * 64 * 8)   // 12288 bf16
+int a3c_split_w1_launch(const float* W1, uint16_t* w1s, hipStream_t s);
 
 // stage the HIST u8 planes of state b into LDS (HIST x 441 uint4)
 __device__ inline void stage_state(const StateAddr& sa, int64_t b, int64_t tau0, uint8_t* x8) {

@@ -53,7 +53,9 @@ int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float
 int a3c_select_launch(const float* z, int64_t B, int zs, int A, const HeadSelect& sel, hipStream_t s);
 void a3c_conv12_set_smem();
 void a3c_conv_bwd_set_smem();
-int a3c_conv12_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, float* act_l1,
-                      float* act_l2, hipStream_t s);
+bool a3c_conv_bwd_compact();
+void a3c_conv_bwd_set_compact(bool v);
+int a3c_conv12_launch(const NetLayout& L, const float* P, const uint16_t* w1s, const StateAddr& sa, int64_t B,
+                      float* act_l1, float* act_l2, hipStream_t s);
 int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,
                         const float* dl2, float* ws, hipStream_t s);

@@ -134,21 +134,46 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ z, i
 #define CB_L1 (C1_P * CB_L1_LD * 4)          // 32000
 #define CB_DL2_LD 36
 #define CB_DL2 (C2_Q * CB_DL2_LD * 4)        // 11664
-#define CB_DL1_LD 16
-#define CB_DL1 (C1_P * CB_DL1_LD * 4)        // 25600
-#define CB_SMEM (CB_X8 + CB_L1 + CB_DL2 + CB_DL1 + 4 * 64 * 4)
+#define CB_L1ST (C1_P * C1_N * 4)            // 25600: linear DMA staging of l1
+#define CB_DL2ST (FLAT * 4)                  // 10368: linear DMA staging of dl2
+// LDS: x8[2] | l1 stage | dl2 stage | l1s (dl1 written in place) | dl2s | red
+#define CB_SMEM_DMA (2 * CB_X8 + CB_L1ST + CB_DL2ST + CB_L1 + CB_DL2 + 4 * 64 * 4)   // 137104
+// compact variant (no prefetch): x8 | l1s | dl2s | red -- leaves LDS for co-resident rollout
+// kernels when the backward overlaps the next rollout (engine overlap mode)
+#define CB_SMEM_COMPACT (CB_X8 + CB_L1 + CB_DL2 + 4 * 64 * 4)                          // 72912
 
+// one 16-byte-per-lane global -> LDS DMA wave-instruction: lane l's 16 bytes land at
+// lds_base + 16 l (lds_base wave-uniform), no VGPR destination
+__device__ inline void glds16(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// the 4 waves DMA `nbytes` (multiple of 16) from g to LDS dst in 1 KiB wave-instructions
+__device__ inline void glds_copy(const uint8_t* g, uint8_t* dst, int nbytes, int wid, int lane) {
+  for (int c = wid; c * 1024 < nbytes; c += 4) {
+    const int off = c * 1024 + lane * 16;
+    if (off < nbytes) glds16(g + off, dst + c * 1024);
+  }
+}
+
+// workgroup barrier that keeps LDS-DMA loads in flight (retires LDS ops only)
+__device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <bool DMA>
 __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int per_wg,
                                                   const float* __restrict__ act_l1,
                                                   const float* __restrict__ dl2,
                                                   const float* __restrict__ W2,
                                                   float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* x8 = smem;
-  float* l1s = (float*)(smem + CB_X8);
-  float* dl2s = (float*)(smem + CB_X8 + CB_L1);
-  float* dl1s = (float*)(smem + CB_X8 + CB_L1 + CB_DL2);
-  float* red = (float*)(smem + CB_X8 + CB_L1 + CB_DL2 + CB_DL1);   // [4 waves][64]
+  uint8_t* x8buf = smem;                                             // [DMA ? 2 : 1][CB_X8]
+  uint8_t* l1st = smem + (DMA ? 2 : 1) * CB_X8;
+  uint8_t* dl2st = l1st + (DMA ? CB_L1ST : 0);
+  float* l1s = (float*)(dl2st + (DMA ? CB_DL2ST : 0));
+  float* dl2s = (float*)((uint8_t*)l1s + CB_L1);
+  float* dl1s = l1s;                                                 // dl1 overwrites l1 in place
+  float* red = (float*)((uint8_t*)dl2s + CB_DL2);                    // [4 waves][64]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int i16 = lane & 15, j4 = lane >> 4;
   const int64_t tau0 = sa.tau_ptr ? *sa.tau_ptr : 0;
@@ -179,18 +204,45 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
   }
   float db1acc = 0.f, db2acc = 0.f;
 
+  // Operands of sample b+1 (x planes, l1, dl2: 64 KB) are DMA'd global -> LDS while sample b
+  // computes: x8 is double-buffered; l1 / dl2 land in linear staging buffers and are copied into
+  // the padded (bank-spread) layouts at the top of the next sample.
+  auto issue = [&](int64_t bb, uint8_t* x8dst) {
+#pragma unroll
+    for (int c = 0; c < HIST; ++c) glds_copy(state_plane(sa, bb, c, tau0), x8dst + c * PLANE, PLANE, wid, lane);
+    glds_copy((const uint8_t*)(act_l1 + bb * C1_P * C1_N), l1st, CB_L1ST, wid, lane);
+    glds_copy((const uint8_t*)(dl2 + bb * FLAT), dl2st, CB_DL2ST, wid, lane);
+  };
+  if (DMA && b0 < b1) issue(b0, x8buf);
+
   for (int64_t b = b0; b < b1; ++b) {
-    __syncthreads();   // previous sample done with LDS
-    stage_state(sa, b, tau0, x8);
-    for (int i = tid; i < C1_P * 4; i += 256) {     // l1 [400][16] -> stride 20
-      int p = i >> 2, q4 = i & 3;
-      *(f32x4*)(l1s + p * CB_L1_LD + 4 * q4) = *(const f32x4*)(act_l1 + (b * C1_P + p) * C1_N + 4 * q4);
+    uint8_t* x8 = x8buf + (DMA ? ((b - b0) & 1) * CB_X8 : 0);
+    if constexpr (DMA) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA for sample b landed
+      __syncthreads();                                    // ... and every wave's; sample b-1 done
+      for (int i = tid; i < C1_P * 4; i += 256) {         // l1 [400][16] -> stride 20
+        const int p = i >> 2, q4 = i & 3;
+        *(f32x4*)(l1s + p * CB_L1_LD + 4 * q4) = ((const f32x4*)l1st)[i];
+      }
+      for (int i = tid; i < C2_Q * 8; i += 256) {         // dl2 [81][32] -> stride 36
+        const int q = i >> 3, q4 = i & 7;
+        *(f32x4*)(dl2s + q * CB_DL2_LD + 4 * q4) = ((const f32x4*)dl2st)[i];
+      }
+      __syncthreads();                                    // staging buffers free again
+      if (b + 1 < b1) issue(b + 1, x8buf + ((b + 1 - b0) & 1) * CB_X8);
+    } else {
+      __syncthreads();                                    // previous sample done with LDS
+      stage_state(sa, b, tau0, x8);
+      for (int i = tid; i < C1_P * 4; i += 256) {
+        const int p = i >> 2, q4 = i & 3;
+        *(f32x4*)(l1s + p * CB_L1_LD + 4 * q4) = *(const f32x4*)(act_l1 + (b * C1_P + p) * C1_N + 4 * q4);
+      }
+      for (int i = tid; i < C2_Q * 8; i += 256) {
+        const int q = i >> 3, q4 = i & 7;
+        *(f32x4*)(dl2s + q * CB_DL2_LD + 4 * q4) = *(const f32x4*)(dl2 + b * FLAT + q * C2_N + 4 * q4);
+      }
+      __syncthreads();
     }
-    for (int i = tid; i < C2_Q * 8; i += 256) {     // dl2 [81][32] -> stride 36
-      int q = i >> 3, q4 = i & 7;
-      *(f32x4*)(dl2s + q * CB_DL2_LD + 4 * q4) = *(const f32x4*)(dl2 + b * FLAT + q * C2_N + 4 * q4);
-    }
-    __syncthreads();
 
     // ---- (a) dW2[(kh,kw,ci)][n] += sum_q l1[2oy+kh][2ox+kw][ci] * dl2[q][n] ----
     for (int s = 0; s < (C2_Q + 3) / 4; ++s) {
@@ -209,6 +261,8 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
         accW2[t][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bq1, accW2[t][1], 0, 0, 0);
       }
     }
+
+    lds_barrier();   // every wave done reading l1 in (a): (b) overwrites it with dl1
 
     // ---- (b) dl1 for parity class (py,px): 100 positions in 7 M-tiles of 16 ----
     for (int mt = 0; mt < 7; ++mt) {
@@ -239,7 +293,7 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
           const int yy = 2 * (pr / 10) + py, xx = 2 * (pr % 10) + px;
           const int p = yy * C1_O + xx;
           const float g = l1s[p * CB_L1_LD + i16] > 0.f ? acc[r] : 0.f;
-          dl1s[p * CB_DL1_LD + i16] = g;
+          dl1s[p * CB_L1_LD + i16] = g;
           db1acc += g;
         }
       }
@@ -250,7 +304,7 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
       for (int q = 0; q < C2_Q; ++q) s2 += dl2s[q * CB_DL2_LD + tid];
       db2acc += s2;
     }
-    __syncthreads();
+    lds_barrier();   // dl1 complete (the DMA for sample b+1 stays in flight)
 
     // ---- (c) dW1[(kh,kw,cin)][n] += sum_p x[cin][4oy+kh][4ox+kw] * dl1[p][n]  (x unscaled) ----
     int koff[4];
@@ -265,7 +319,7 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
       const int p = 4 * s + j4;
       const int oy = p / C1_O, ox = p - oy * C1_O;
       const int base = (C1_S * oy) * IMG + C1_S * ox;
-      const float bv = dl1s[p * CB_DL1_LD + i16];
+      const float bv = dl1s[p * CB_L1_LD + i16];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         accW1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)x8[base + koff[t]], bv, accW1[t], 0, 0, 0);
@@ -459,10 +513,21 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   return 0;
 }
 
+// variant choice: the compact kernel when the backward shares the GPU with a concurrent rollout
+// (engine overlap mode), the LDS-DMA prefetching one otherwise.  Thread-local switch set by the
+// engine around its enqueue calls (captured into the graphs).
+static thread_local bool t_conv_bwd_compact = false;
+bool a3c_conv_bwd_compact() { return t_conv_bwd_compact; }
+void a3c_conv_bwd_set_compact(bool v) { t_conv_bwd_compact = v; }
+
 int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,
                         const float* dl2, float* ws, hipStream_t s) {
   const BwdPlan p = a3c_bwd_plan(L, B);
-  hipLaunchKernelGGL(k_conv_bwd, dim3((unsigned)p.nwg), dim3(256), CB_SMEM, s, sa, B, p.per_wg, act_l1,
+  if (a3c_conv_bwd_compact())
+    hipLaunchKernelGGL(k_conv_bwd<false>, dim3((unsigned)p.nwg), dim3(256), CB_SMEM_COMPACT, s, sa, B, p.per_wg, act_l1,
+                       dl2, P + L.off[T_L2W], ws + p.cslab);
+  else
+  hipLaunchKernelGGL(k_conv_bwd<true>, dim3((unsigned)p.nwg), dim3(256), CB_SMEM_DMA, s, sa, B, p.per_wg, act_l1,
                      dl2, P + L.off[T_L2W], ws + p.cslab);
   A3C_CHECK(hipGetLastError());
   return 0;
@@ -487,5 +552,7 @@ int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float
 }
 
 void a3c_conv_bwd_set_smem() {
-  (void)hipFuncSetAttribute((const void*)k_conv_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, CB_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_SMEM_DMA);
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            CB_SMEM_COMPACT);
 }

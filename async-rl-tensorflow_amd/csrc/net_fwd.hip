@@ -16,51 +16,108 @@
 #include "net_bwd.h"
 #include "env_dev.h"
 
-#define X8_BYTES (HIST * PLANE)                      // 28224
+#define XB_BYTES (HIST * PLANE * 2)                  // 56448: state planes as bf16
 #define L1S_BYTES (C1_P * L1S_LD * 4)                // 32000
-#define CONV12_SMEM (X8_BYTES + L1S_BYTES)
+#define CONV12_SMEM (XB_BYTES + L1S_BYTES)           // 88448
 
+// ---------------------------------------------------------------------------------------
+// conv1 weights as three bf16 terms.  A u8 pixel is exact in bf16, so conv1 runs on the bf16
+// matrix cores (16x16x32, 16x the fp32 MFMA rate) as x * (w_hi + w_mid + w_lo): the three
+// round-to-nearest bf16 terms carry w to ~2^-24 relative and every product is exact in the
+// fp32 accumulator -- fp32 accuracy for 3 MFMAs instead of 8 fp32 ones per 32-deep K step.
+// Fragment-ordered buffer w1s[kh][term][lane][j] (bf16): lane l = (cin g = l>>4, cout i = l&15)
+// holds B[k = 8g + j][i] = W1[kh][kw = j][cin = g][cout = i] (ops.py:21 layout).
+// ---------------------------------------------------------------------------------------
+__device__ inline uint32_t bf16_rn_bits(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+__global__ void __launch_bounds__(256) k_split_w1(const float* __restrict__ W1, uint16_t* __restrict__ w1s) {
+#pragma clang fp contract(off)
+  const int t = blockIdx.x * 256 + threadIdx.x;            // (kh, lane, j): 8 * 64 * 8
+  if (t >= C1_K * 64 * 8) return;
+  const int kh = t >> 9, lane = (t >> 3) & 63, j = t & 7;
+  const int g = lane >> 4, i = lane & 15;
+  const float w = W1[((kh * C1_K + j) * HIST + g) * C1_N + i];
+  const uint32_t h = bf16_rn_bits(w);
+  const float r1 = w - __uint_as_float(h << 16);
+  const uint32_t m = bf16_rn_bits(r1);
+  const float r2 = r1 - __uint_as_float(m << 16);
+  const uint32_t l = bf16_rn_bits(r2);
+  w1s[((kh * 3 + 0) * 64 + lane) * 8 + j] = (uint16_t)h;
+  w1s[((kh * 3 + 1) * 64 + lane) * 8 + j] = (uint16_t)m;
+  w1s[((kh * 3 + 2) * 64 + lane) * 8 + j] = (uint16_t)l;
+}
+
+int a3c_split_w1_launch(const float* W1, uint16_t* w1s, hipStream_t s) {
+  hipLaunchKernelGGL(k_split_w1, dim3(C1_K * 64 * 8 / 256), dim3(256), 0, s, W1, w1s);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+// 8 waves per state.  The 4 u8 planes are staged into LDS as bf16 (exact); conv1 = 25 M-tiles
+// of 16 positions x K = 256 (8 steps of (kh; cin x kw 0..7)) on v_mfma_f32_16x16x32_bf16 with the
+// three weight terms; conv1 + relu to LDS (and HBM when the backward needs it); conv2 (4x4/2,
+// 16->32, K = 256) in fp32 MFMA from LDS, 12 (M-tile, N-tile) pairs over the 8 waves.
 template <bool SAVE_L1>
-__global__ void __launch_bounds__(256) k_conv12_fwd(StateAddr sa, int64_t B,
-                                                    const float* __restrict__ W1,
+__global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
+                                                    const uint16_t* __restrict__ w1s,
                                                     const float* __restrict__ b1,
                                                     const float* __restrict__ W2,
                                                     const float* __restrict__ b2,
                                                     float* __restrict__ act_l1,
                                                     float* __restrict__ act_l2) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* x8 = smem;
-  float* l1s = (float*)(smem + X8_BYTES);
+  uint16_t* xb = (uint16_t*)smem;
+  float* l1s = (float*)(smem + XB_BYTES);
   const int64_t b = blockIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i16 = lane & 15, j4 = lane >> 4;
   const int64_t tau0 = sa.tau_ptr ? *sa.tau_ptr : 0;
 
-  stage_state(sa, b, tau0, x8);
-
-  // conv1 weights: lane (k-sub j4 = cin, col i16 = cout) holds W1[kh][kw][j4][i16] for all 64 (kh,kw)
-  float w1r[64];
+  // stage: u8 planes -> bf16 planes (integers 0..255 are exact in bf16)
+  for (int i = threadIdx.x; i < HIST * (PLANE / 16); i += 512) {
+    const int c = i / (PLANE / 16), j = i - c * (PLANE / 16);
+    const uint4 v = ((const uint4*)state_plane(sa, b, c, tau0))[j];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[8];
 #pragma unroll
-  for (int s = 0; s < 64; ++s) w1r[s] = W1[(s * HIST + j4) * C1_N + i16];
+    for (int q = 0; q < 4; ++q) {
+      const float f0 = (float)(w[q] & 255u), f1 = (float)((w[q] >> 8) & 255u);
+      const float f2 = (float)((w[q] >> 16) & 255u), f3 = (float)(w[q] >> 24);
+      o[2 * q] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
+      o[2 * q + 1] = __builtin_amdgcn_perm(__float_as_uint(f3), __float_as_uint(f2), 0x07060302u);
+    }
+    uint4* dst = (uint4*)(xb + c * PLANE + 16 * j);
+    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+  }
+
+  // conv1 weight fragments (3 bf16 terms per K step)
+  bf16x8 wf[C1_K][3];
+#pragma unroll
+  for (int kh = 0; kh < C1_K; ++kh)
+#pragma unroll
+    for (int t = 0; t < 3; ++t) wf[kh][t] = __builtin_bit_cast(bf16x8, ((const uint4*)w1s)[(kh * 3 + t) * 64 + lane]);
   const float bias1 = b1[i16];
   __syncthreads();
 
-  // ---- conv1: 25 M-tiles of 16 positions, K = 64 steps of (kh,kw) x 4 cin ----
-  for (int m = wid; m < C1_P / 16; m += 4) {
+  // ---- conv1 ----
+  for (int m = wid; m < C1_P / 16; m += 8) {
     const int p = 16 * m + i16;
     const int oy = p / C1_O, ox = p - oy * C1_O;
-    const uint8_t* row = x8 + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;
+    const uint16_t* row = xb + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;    // cin = j4
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kh = 0; kh < C1_K; ++kh) {
-      uint32_t lo = *(const uint32_t*)(row + kh * IMG);
-      uint32_t hi = *(const uint32_t*)(row + kh * IMG + 4);
-#pragma unroll
-      for (int kw = 0; kw < 4; ++kw)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32((float)((lo >> (8 * kw)) & 255u), w1r[kh * 8 + kw], acc, 0, 0, 0);
-#pragma unroll
-      for (int kw = 0; kw < 4; ++kw)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32((float)((hi >> (8 * kw)) & 255u), w1r[kh * 8 + 4 + kw], acc, 0, 0, 0);
+      const uint2* q = (const uint2*)(row + kh * IMG);                        // 8-byte aligned
+      const uint2 lo = q[0], hi = q[1];
+      const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][2], acc, 0, 0, 0);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -72,7 +129,7 @@ __global__ void __launch_bounds__(256) k_conv12_fwd(StateAddr sa, int64_t B,
   }
 
   // conv2 weights for this wave's N tile: W2[kh][kw][4*j4 + c4][16*nt + i16]
-  const int nt = wid >> 1, mbase = (wid & 1) * 3;
+  const int nt = wid & 1, grp = wid >> 1;          // M-tiles grp and grp + 4 (when < 6)
   float w2r[64];
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk)
@@ -82,35 +139,39 @@ __global__ void __launch_bounds__(256) k_conv12_fwd(StateAddr sa, int64_t B,
   __syncthreads();
 
   // ---- conv2: 6 M-tiles (81 rows padded to 96) x 2 N-tiles, K = 16 (kh,kw) x 16 cin ----
-  int pos0[3];
+  const int nm = grp + 4 < 6 ? 2 : 1;
+  int pos0[2];
 #pragma unroll
-  for (int mi = 0; mi < 3; ++mi) {
-    int q = 16 * (mbase + mi) + i16;
+  for (int mi = 0; mi < 2; ++mi) {
+    int q = 16 * (grp + 4 * mi) + i16;
     q = q < C2_Q ? q : C2_Q - 1;
     int oy = q / C2_O, ox = q - oy * C2_O;
     pos0[mi] = (C2_S * oy) * C1_O + C2_S * ox;
   }
-  f32x4 acc2[3];
+  f32x4 acc2[2];
 #pragma unroll
-  for (int mi = 0; mi < 3; ++mi) acc2[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int mi = 0; mi < 2; ++mi) acc2[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int kh = 0; kh < C2_K; ++kh)
 #pragma unroll
     for (int kw = 0; kw < C2_K; ++kw)
 #pragma unroll
-      for (int mi = 0; mi < 3; ++mi) {
+      for (int mi = 0; mi < 2; ++mi) {
+        if (mi >= nm) break;
         f32x4 a = *(const f32x4*)(l1s + (pos0[mi] + kh * C1_O + kw) * L1S_LD + 4 * j4);
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4)
           acc2[mi] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c4], w2r[(kh * 4 + kw) * 4 + c4], acc2[mi], 0, 0, 0);
       }
 #pragma unroll
-  for (int mi = 0; mi < 3; ++mi)
+  for (int mi = 0; mi < 2; ++mi) {
+    if (mi >= nm) break;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int q = 16 * (mbase + mi) + 4 * j4 + r;
+      const int q = 16 * (grp + 4 * mi) + 4 * j4 + r;
       if (q < C2_Q) act_l2[b * FLAT + q * C2_N + 16 * nt + i16] = fmaxf(acc2[mi][r] + bias2, 0.f);
     }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -226,21 +287,14 @@ __global__ void __launch_bounds__(256) k_select(const float* __restrict__ z, int
   if (lane == 0) sel.actions[b] = a;
 }
 
-int64_t a3c_fwd_slab_floats(int64_t B, int* split_out) {
-  int split = a3c_gemm_plan_split((int)B, FC, FLAT, 512);
-  split = a3c_gemm_effective_split(FLAT, split);
-  if (split_out) *split_out = split;
-  return split > 1 ? (int64_t)split * B * FC : 0;
-}
-
 int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s);
 
-int a3c_forward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
-                       float* act_l1, float* act_l2, float* act_l3, float* z, float* slab,
-                       int fc_split, const HeadSelect& sel, hipStream_t s) {
+int a3c_forward_launch(const NetLayout& L, const float* params, const uint16_t* w1s, const StateAddr& sa,
+                       int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
+                       hipStream_t s) {
   if (B <= 0) return 0;
   const float* P = params;
-  int rc0 = a3c_conv12_launch(L, P, sa, B, act_l1, act_l2, s);
+  int rc0 = a3c_conv12_launch(L, P, w1s, sa, B, act_l1, act_l2, s);
   if (rc0) return rc0;
   int rc = a3c_fc_fwd_launch(act_l2, P + L.off[T_FCW], P + L.off[T_FCB], act_l3, B, s);
   if (rc) return rc;
@@ -252,14 +306,15 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const StateAddr&
   return 0;
 }
 
-int a3c_conv12_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, float* act_l1,
-                      float* act_l2, hipStream_t s) {
+int a3c_conv12_launch(const NetLayout& L, const float* P, const uint16_t* w1s, const StateAddr& sa, int64_t B,
+                      float* act_l1, float* act_l2, hipStream_t s) {
+  if (!w1s) return a3c_set_error(A3C_ERR_INVALID, "a3c_conv12_launch", "split conv1 weights missing");
   if (act_l1)
-    hipLaunchKernelGGL((k_conv12_fwd<true>), dim3((unsigned)B), dim3(256), CONV12_SMEM, s, sa, B,
-                       P + L.off[T_L1W], P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2);
+    hipLaunchKernelGGL((k_conv12_fwd<true>), dim3((unsigned)B), dim3(512), CONV12_SMEM, s, sa, B, w1s,
+                       P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2);
   else
-    hipLaunchKernelGGL((k_conv12_fwd<false>), dim3((unsigned)B), dim3(256), CONV12_SMEM, s, sa, B,
-                       P + L.off[T_L1W], P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2);
+    hipLaunchKernelGGL((k_conv12_fwd<false>), dim3((unsigned)B), dim3(512), CONV12_SMEM, s, sa, B, w1s,
+                       P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
