@@ -71,7 +71,7 @@ struct a3c_engine {
   bool captured[5];
   // overlap pipeline
   hipStream_t rs;          // rollout stream
-  hipEvent_t ev_start, ev_snap[2], ev_roll[2];
+  hipEvent_t ev_start, ev_roll[2];
   int64_t iter;            // rollouts issued since reset
   bool grad_ready;         // the last rollout_grad call computed a gradient
   bool reset_done;
@@ -133,7 +133,6 @@ extern "C" int a3c_engine_destroy(a3c_engine* e) {
   if (e->rs) (void)hipStreamDestroy(e->rs);
   if (e->ev_start) (void)hipEventDestroy(e->ev_start);
   for (int k = 0; k < 2; ++k) {
-    if (e->ev_snap[k]) (void)hipEventDestroy(e->ev_snap[k]);
     if (e->ev_roll[k]) (void)hipEventDestroy(e->ev_roll[k]);
   }
   for (void* p : e->allocs) (void)hipFree(p);
@@ -225,8 +224,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     bool ok = hipStreamCreateWithFlags(&e->rs, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&e->ev_start, hipEventDisableTiming) == hipSuccess;
     for (int k = 0; k < 2 && ok; ++k)
-      ok = hipEventCreateWithFlags(&e->ev_snap[k], hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&e->ev_roll[k], hipEventDisableTiming) == hipSuccess;
+      ok = hipEventCreateWithFlags(&e->ev_roll[k], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
       a3c_engine_destroy(e);
       return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "stream/event creation failed");
@@ -460,6 +458,9 @@ extern "C" int a3c_engine_reset(a3c_engine* e, const float* host_params, void* s
   if (rc) return rc;
   rc = a3c_env_init_launch(e->envp, e->env, e->E, e->pool, e->ring, e->R, e->counters, s);
   if (rc) return rc;
+  if (e->overlap)
+    for (int k = 0; k < 2; ++k)
+      A3C_CHECK(hipMemcpyAsync(e->slot[k].P, e->params, L.total * 4, hipMemcpyDeviceToDevice, s));
   e->iter = 0;
   e->grad_ready = false;
   e->reset_done = true;
@@ -476,23 +477,20 @@ extern "C" int a3c_engine_rollout_grad(a3c_engine* e, void* stream) {
     return rc;
   }
   // overlap: rollout k (slot p) on the engine's rollout stream, after everything the caller
-  // enqueued so far (in steady state: the apply of rollout k-2, whose parameters it snapshots);
-  // the backward of rollout k-1 (slot p^1) on the caller's stream, after that rollout and after
-  // rollout k has taken its parameter snapshot (the caller's apply rewrites the parameters).
+  // enqueued so far -- in steady state the apply of rollout k-2, which also left the parameter
+  // snapshot of rollout k in slot p (a3c_engine_apply); the backward of rollout k-1 (slot p^1) on
+  // the caller's stream once that rollout is complete.
   const int p = (int)(e->iter & 1);
   const Slot& sl = e->slot[p];
   A3C_CHECK(hipEventRecord(e->ev_start, s));
   A3C_CHECK(hipStreamWaitEvent(e->rs, e->ev_start, 0));
-  A3C_CHECK(hipMemcpyAsync(sl.P, e->params, e->L.total * 4, hipMemcpyDeviceToDevice, e->rs));
   A3C_CHECK(hipMemcpyAsync(sl.tau, e->counters, 8, hipMemcpyDeviceToDevice, e->rs));
-  A3C_CHECK(hipEventRecord(e->ev_snap[p], e->rs));
   int rc = run_graph(e, 1 + p, 1, p, e->rs);
   if (rc) return rc;
   A3C_CHECK(hipEventRecord(e->ev_roll[p], e->rs));
   e->grad_ready = false;
   if (e->iter >= 1) {
     A3C_CHECK(hipStreamWaitEvent(s, e->ev_roll[p ^ 1], 0));
-    A3C_CHECK(hipStreamWaitEvent(s, e->ev_snap[p], 0));
     rc = run_graph(e, 3 + (p ^ 1), 2, p ^ 1, s);
     if (rc) return rc;
     e->grad_ready = true;
@@ -511,8 +509,13 @@ extern "C" int a3c_engine_apply(a3c_engine* e, void* stream) {
   if (!e->grad_ready) return 0;          // overlap pipeline still filling: nothing to apply
   OptParams op = opt_params(e);
   op.mode = e->cfg.world_size > 1 ? OPT_APPLY : (OPT_CLIP | OPT_APPLY);
-  return a3c_apply_launch(e->params, e->ms, e->mom, e->grads, e->tt, op, e->opt_part,
-                          e->cfg.world_size > 1 ? nullptr : e->sumsq, s);
+  int rc = a3c_apply_launch(e->params, e->ms, e->mom, e->grads, e->tt, op, e->opt_part,
+                            e->cfg.world_size > 1 ? nullptr : e->sumsq, s);
+  if (rc || !e->overlap) return rc;
+  // overlap: parameter snapshot for the next rollout (iter), whose slot's previous rollout
+  // (iter - 2) has just been back-propagated on this stream
+  A3C_CHECK(hipMemcpyAsync(e->slot[e->iter & 1].P, e->params, e->L.total * 4, hipMemcpyDeviceToDevice, s));
+  return 0;
 }
 
 extern "C" int a3c_engine_slot_buffers(a3c_engine* e, int slot, a3c_engine_buffers* b) {
