@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(256) k_apply(float* __restrict__ w, float* __r
       *(f32x4*)(grads + i) = g;
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && op.counters) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && op.counters && apply) {   // clip-only passes leave them
     if (op.dtau) op.counters[0] += op.dtau;   // overlap mode: the rollout owns tau
     op.counters[1] += op.step_add;
   }
