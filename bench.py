@@ -56,36 +56,23 @@ def parse():
 
 
 def cpu_baseline(seconds, game, algo):
-    """oracle/engine_ref.py (numpy restatement of the same iteration) on one host core."""
-    import numpy as np
-    try:
-        from threadpoolctl import threadpool_limits
-        lim = threadpool_limits(1)
-    except Exception:   # pragma: no cover
-        lim = None
-    from oracle.engine_ref import EngineRef
-    from src.initializers import init_params
-    from src.kernels import param_names_shapes
+    """The reference's ps/worker algorithm restated on the CPU (oracle/ps_worker.py: shared-memory
+    PS, W worker processes with Hogwild RMSProp, one numpy thread each) on the same synthetic
+    env: 1 ps / 1 worker (BASELINE config 1) and W = min(nproc - 1, 15) workers.  Runs before
+    the GPU is initialised (the workers are spawned processes)."""
+    from oracle import ps_worker
     A, lives = GAMES[game]
-    E, n = 8, 5 if algo == 'a3c' else 32
-    p = init_params(param_names_shapes(A, algo), seed=123)
-    ref = EngineRef(p, E, n, A, algo, lives, num_frames=16384, seed=123, dtype=np.float32)
-    ref.cache_screens = False
-    ref.reset()
-    t0 = time.perf_counter()
-    iters = 0
-    while True:
-        out = ref.iterate()
-        ref.apply(out['clipped'])
-        iters += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    if lim is not None:
-        lim.unregister() if hasattr(lim, 'unregister') else None
-    return dict(value=round(iters * E * n / el, 2), unit='env-steps/s', cores=1, kind='port',
-                sample=f'oracle/engine_ref.py {algo} iteration (numpy fp32), {E} envs x n={n}, '
-                       f'{iters} iterations in {el:.1f} s, 1 thread, no screen cache')
+    n = 5 if algo == 'a3c' else 32
+    W = max(1, min((os.cpu_count() or 2) - 1, 15))
+    one = ps_worker.run(seconds=seconds / 2, workers=1, envs_per_worker=8, n_step=n, action_size=A, algo=algo,
+                        start_lives=lives)
+    many = ps_worker.run(seconds=seconds / 2, workers=W, envs_per_worker=8, n_step=n, action_size=A, algo=algo,
+                         start_lives=lives) if W > 1 else one
+    return dict(value=round(many['value'], 2), unit='env-steps/s', cores=W, kind='port',
+                one_worker=round(one['value'], 2),
+                sample=f'oracle/ps_worker.py ({algo} ps/worker, shared-memory PS, unlocked RMSProp, numpy fp32, '
+                       f'8 envs x n={n} per worker): {W} workers x {many["seconds"]:.1f} s = '
+                       f'{many["iterations"]} iterations; 1 ps/1 worker: {one["value"]:.1f} env-steps/s')
 
 
 def main():
@@ -100,6 +87,9 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit('--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)')
+    cpu = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds, args.game, args.algo)    # before any HIP initialisation
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
@@ -188,9 +178,6 @@ def main():
     if world > 1:
         dist.barrier()
     if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.cpu_seconds, args.game, args.algo)
         steps_total = world * E * n * args.steps
         line = {
             'metric': METRIC, 'value': round(steps_total / el, 1), 'unit': 'env-steps/s', 'n_gpus': world,
