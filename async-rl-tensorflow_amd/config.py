@@ -93,7 +93,7 @@ def get_config(FLAGS):
       else:
         config.cnn_format = 'NCHW'
 
-    if hasattr(config, k):
+    if hasattr(config, k) and v is not None:     # unset optional flags keep the config default
       setattr(config, k, v)
 
   return config

@@ -535,6 +535,21 @@ extern "C" int a3c_engine_slot_buffers(a3c_engine* e, int slot, a3c_engine_buffe
   b->env_step = e->env.ep_step; b->env_len = e->env.ep_len;
   b->zs = e->L.zs; b->n_tensors = e->L.nt;
   for (int i = 0; i < e->L.nt; ++i) { b->offsets[i] = e->L.off[i]; b->sizes[i] = e->L.size[i]; }
+  b->sched = e->sched;
+  return 0;
+}
+
+__global__ void k_advance(int64_t* counters, int64_t dtau, int64_t dstep) {
+  counters[0] += dtau;
+  counters[1] += dstep;
+}
+
+extern "C" int a3c_engine_advance(a3c_engine* e, void* stream) {
+  if (!e || e->overlap) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_advance", "sync engines only");
+  if (!e->grad_ready) return 0;
+  hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, (hipStream_t)stream, e->counters, (int64_t)e->n,
+                     e->nE * e->cfg.world_size);
+  A3C_CHECK(hipGetLastError());
   return 0;
 }
 

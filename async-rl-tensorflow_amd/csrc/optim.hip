@@ -9,6 +9,7 @@
 //          block 0 advances the engine counters at the end (nothing in this launch reads them).
 // Element math is written with contraction off so it matches the numpy oracle bit for bit on
 // equal gradients.
+#include <cstring>
 #include "optim.h"
 
 int a3c_make_tab(int n, const int64_t* off, const int64_t* size, int64_t total, TensorTab* tt) {
@@ -220,5 +221,66 @@ extern "C" int a3c_copy_params(float* dst, const float* src, int64_t n, void* st
   if (!dst || !src || n < 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_copy_params", "bad argument");
   if (n == 0) return 0;
   A3C_CHECK(hipMemcpyAsync(dst, src, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+
+// ---- Hogwild shard apply ------------------------------------------------------------------
+__global__ void k_rmsprop_range(float* __restrict__ w, float* __restrict__ ms, float* __restrict__ mom,
+                                const float* __restrict__ g, int64_t n, const float* __restrict__ lr_dev, float lr,
+                                float rho, float momentum, float eps) {
+  const float l = lr_dev ? lr_dev[0] : lr;
+  const float one_m_rho = 1.0f - rho;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i];
+    const float m2 = ms[i] + (gi * gi - ms[i]) * one_m_rho;
+    const float mo = mom[i] * momentum + (gi * l) / sqrtf(m2 + eps);
+    ms[i] = m2;                // unlocked read-modify-write: concurrent workers may interleave
+    mom[i] = mo;
+    w[i] = w[i] - mo;
+  }
+}
+
+extern "C" int a3c_rmsprop_range(float* w, float* ms, float* mom, const float* grads, int64_t n, const float* lr_dev,
+                                 float lr, float rho, float momentum, float eps, void* stream) {
+  if (!w || !ms || !mom || !grads || n < 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_rmsprop_range", "bad argument");
+  if (n == 0) return 0;
+  const int64_t blocks = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  hipLaunchKernelGGL(k_rmsprop_range, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, w, ms, mom, grads, n,
+                     lr_dev, lr, rho, momentum, eps);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int a3c_dev_alloc(int64_t bytes, void** out) {
+  if (!out || bytes <= 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_dev_alloc", "bad argument");
+  A3C_CHECK(hipMalloc(out, (size_t)bytes));
+  return 0;
+}
+
+extern "C" int a3c_dev_free(void* p) {
+  if (p) A3C_CHECK(hipFree(p));
+  return 0;
+}
+
+extern "C" int a3c_ipc_handle(void* base, void* handle64) {
+  if (!base || !handle64) return a3c_set_error(A3C_ERR_INVALID, "a3c_ipc_handle", "bad argument");
+  static_assert(sizeof(hipIpcMemHandle_t) <= 64, "ipc handle size");
+  hipIpcMemHandle_t h;
+  A3C_CHECK(hipIpcGetMemHandle(&h, base));
+  memset(handle64, 0, 64);
+  memcpy(handle64, &h, sizeof(h));
+  return 0;
+}
+
+extern "C" int a3c_ipc_open(const void* handle64, void** out) {
+  if (!handle64 || !out) return a3c_set_error(A3C_ERR_INVALID, "a3c_ipc_open", "bad argument");
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle64, sizeof(h));
+  A3C_CHECK(hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess));
+  return 0;
+}
+
+extern "C" int a3c_ipc_close(void* p) {
+  if (p) A3C_CHECK(hipIpcCloseMemHandle(p));
   return 0;
 }

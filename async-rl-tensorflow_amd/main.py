@@ -60,6 +60,8 @@ def parse_flags(argv=None):
   p.add_argument('--iterations', type=int, default=1000)
   p.add_argument('--max_step', type=int, default=None)
   p.add_argument('--log_every', type=int, default=100)
+  p.add_argument('--update', choices=['overlap', 'sync', 'hogwild'], default='overlap',
+                 help='engine mode: stale-1 overlapped A3C, synchronous all-reduce, or Hogwild sharded PS')
   p.add_argument('--logdir', default='./logs')
   return p.parse_args(argv)
 
@@ -78,13 +80,21 @@ def run_engine(config, flags):
               ep_end=config.ep_end, ep_end_t=config.ep_end_t, learn_start=config.learn_start,
               target_q_update_step=config.target_q_update_step, random_start=config.random_start,
               action_repeat=config.action_repeat)
+  overlap = flags.update == 'overlap' and flags.algo == 'a3c'
   eng = Engine(num_envs=E, n_step=flags.n_step, action_size=A, algo=flags.algo, start_lives=lives,
-               num_frames=flags.num_frames, seed=flags.random_seed, env_id_base=rank * E, world_size=world, **opts)
+               num_frames=flags.num_frames, seed=flags.random_seed, env_id_base=rank * E, world_size=world,
+               overlap=overlap, **opts)
   eng.reset()
   D.broadcast_params(eng.params, src=0)
   if flags.algo == 'q':
     eng.target_params.copy_(eng.params)
+  if overlap:
+    eng.reset()    # keeps the broadcast parameters, re-takes the pipeline snapshots
   xch = D.GradExchange() if world > 1 else None
+  ps = None
+  if flags.update == 'hogwild':
+    from src.hogwild import HogwildPS
+    ps = HogwildPS(eng.params, decay=config.decay, momentum=config.momentum, epsilon=config.epsilon)
   torch.cuda.synchronize()
   t0 = time.time()
   log = None
@@ -92,7 +102,10 @@ def run_engine(config, flags):
     os.makedirs(flags.logdir, exist_ok=True)
     log = open(os.path.join(flags.logdir, 'engine.jsonl'), 'a')
   for it in range(flags.iterations):
-    eng.iterate(exchange=xch)
+    if ps is not None:
+      eng.iterate_hogwild(ps)
+    else:
+      eng.iterate(exchange=xch)
     if rank == 0 and (it + 1) % flags.log_every == 0:
       loss = eng.loss.tolist()
       torch.cuda.synchronize()
@@ -104,6 +117,8 @@ def run_engine(config, flags):
       print(json.dumps(rec), flush=True)
       log.write(json.dumps(rec) + '\n')
   torch.cuda.synchronize()
+  if ps is not None:
+    ps.close()
   if log:
     log.close()
   return eng

@@ -48,7 +48,7 @@ class EngineBuffers(ctypes.Structure):
                 ('frame_pool', c_void_p), ('env_frame', c_void_p), ('env_lives', c_void_p),
                 ('env_episode', c_void_p), ('env_step', c_void_p), ('env_len', c_void_p),
                 ('zs', c_int), ('n_tensors', c_int), ('offsets', c_i64 * MAX_TENSORS),
-                ('sizes', c_i64 * MAX_TENSORS)]
+                ('sizes', c_i64 * MAX_TENSORS), ('sched', c_void_p)]
 
 
 # name -> (restype, argtypes)
@@ -101,6 +101,14 @@ SIGNATURES = {
     'a3c_engine_get_buffers': (c_int, [c_void_p, ctypes.POINTER(EngineBuffers)]),
     'a3c_engine_slot_buffers': (c_int, [c_void_p, c_int, ctypes.POINTER(EngineBuffers)]),
     'a3c_engine_grad_ready': (c_int, [c_void_p]),
+    'a3c_engine_advance': (c_int, [c_void_p, c_void_p]),
+    'a3c_dev_alloc': (c_int, [c_i64, ctypes.POINTER(c_void_p)]),
+    'a3c_dev_free': (c_int, [c_void_p]),
+    'a3c_ipc_handle': (c_int, [c_void_p, c_void_p]),
+    'a3c_ipc_open': (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
+    'a3c_ipc_close': (c_int, [c_void_p]),
+    'a3c_rmsprop_range': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_void_p, c_float, c_float,
+                                  c_float, c_float, c_void_p]),
     'a3c_engine_time_kernel': (c_int, [c_void_p, c_int, c_int, c_void_p, ctypes.POINTER(c_float)]),
 }
 

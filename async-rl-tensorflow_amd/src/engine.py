@@ -85,6 +85,7 @@ class Engine:
         self.ring_slots = int(b.ring_slots)
         self.counters = _view(b.tau, (2,), torch.int64)
         self.loss = _view(b.loss, (4,), torch.float32)
+        self.sched_ptr = int(b.sched)             # device [0] = lr of the last gradient
         self.sumsq = _view(b.sumsq, (b.n_tensors,), torch.float32)
         self._slots = [self._slot_views(k) for k in range(2 if self.overlap else 1)]
         for k, v in self._slots[0].items():
@@ -163,6 +164,28 @@ class Engine:
         if exchange is not None:
             exchange(self.grads)
         self.apply()
+
+    def advance(self):
+        check(lib().a3c_engine_advance(self._h, _lib.stream_handle()), 'a3c_engine_advance')
+
+    def iterate_hogwild(self, ps):
+        """Rollout + gradient, unlocked push of the (per-worker clipped) gradient into the
+        sharded Hogwild parameter server, pull of the shared parameters (src/hogwild.py)."""
+        if self.overlap:
+            raise ValueError('hogwild runs on a synchronous engine (overlap=False)')
+        self.rollout_grad()
+        if self.cfg.world_size == 1:
+            # one worker: the engine fuses its clip into apply, which hogwild bypasses
+            if not hasattr(self, '_clip_ws'):
+                b = _lib.c_i64()
+                check(lib().a3c_optim_workspace_bytes(self.params.numel(), ctypes.byref(b)), 'ws')
+                self._clip_ws = torch.empty(int(b.value), dtype=torch.uint8, device='cuda')
+            check(lib().a3c_clip_grads(_lib.ptr(self.grads), len(self.offsets), _lib.i64_array(self.offsets),
+                                       _lib.i64_array(self.sizes), float(self.cfg.clip_norm), None,
+                                       _lib.ptr(self._clip_ws), _lib.stream_handle()), 'a3c_clip_grads')
+        ps.push(self.grads, lr_dev=self.sched_ptr)
+        self.advance()
+        ps.pull(self.params)
 
     def time_kernel(self, kernel, iters=20):
         """Average device ms of one engine kernel (HIP events on the current stream)."""

@@ -47,8 +47,10 @@ def parse():
     ap.add_argument('--algo', default='a3c', choices=['a3c', 'q'])
     ap.add_argument('--frames', type=int, default=16384, help='HBM frame pool (16384 = 1.65 GB > L3)')
     ap.add_argument('--no-graph', action='store_true')
-    ap.add_argument('--overlap', type=int, default=1, choices=[0, 1],
-                    help='1: rollout k overlaps backward+apply of rollout k-1 (stale-1 async A3C)')
+    ap.add_argument('--update', default='overlap', choices=['overlap', 'sync', 'hogwild'],
+                    help='overlap: rollout k overlaps backward+apply of rollout k-1 (stale-1 async A3C); '
+                         'sync: rollout -> backward -> all-reduce -> apply; hogwild: unlocked pushes into a '
+                         'sharded IPC parameter server, no collective (BASELINE config 4)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
@@ -103,11 +105,22 @@ def main():
     E, n = args.envs, args.n_step
     eng = Engine(num_envs=E, n_step=n, action_size=A, algo=args.algo, start_lives=lives, num_frames=args.frames,
                  seed=123, env_id_base=rank * E, world_size=world, use_graph=not args.no_graph,
-                 overlap=bool(args.overlap))
+                 overlap=args.update == 'overlap')
     ns = param_names_shapes(A, args.algo)
     params = flatten_host(ns, eng.offsets, eng.params.numel(), init_params(ns, seed=123))
     eng.reset(params)     # every rank starts from the same parameters
     torch.cuda.synchronize()
+
+    ps = None
+    if args.update == 'hogwild':
+        from src.hogwild import HogwildPS
+        ps = HogwildPS(eng.params)
+
+    def step():
+        if ps is not None:
+            eng.iterate_hogwild(ps)
+        else:
+            eng.iterate(exchange)
 
     exchange = None
     if world > 1:
@@ -119,12 +132,12 @@ def main():
             dist.barrier()
 
     for _ in range(args.warmup):
-        eng.iterate(exchange)
+        step()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.iterate(exchange)
+        step()
     torch.cuda.synchronize()
     barrier()
     el = time.perf_counter() - t0
@@ -189,15 +202,22 @@ def main():
                                    f'{"A3C" if args.algo == "a3c" else "one-step Q"} conv net (nips trunk)',
                        'game': args.game, 'envs_per_gpu': E, 'n_step': n, 'action_size': A, 'algo': args.algo,
                        'env_steps_per_step': world * E * n,
-                       'parallelism': f'dp{world} sync all-reduce (RCCL) of per-worker-clipped grads'
+                       'parallelism': (f'dp{world} hogwild: unlocked RMSProp pushes into {world} IPC-mapped HBM '
+                                       f'shards over xGMI, pull at rollout start, no collective'
+                                       if args.update == 'hogwild' else
+                                       f'dp{world} all-reduce (RCCL) of per-worker-clipped grads')
                        if world > 1 else 'dp1', 'hipgraph': not args.no_graph,
-                       'update': 'overlap: rollout k uses params after update k-2 (A3C stale-1 async), '
-                                 'backward+apply of k-1 concurrent' if args.overlap else
-                                 'synchronous: rollout -> backward -> apply'},
+                       'update': {'overlap': 'overlap: rollout k uses params after update k-2 (A3C stale-1 async), '
+                                             'backward+apply of k-1 concurrent with rollout k',
+                                  'sync': 'synchronous: rollout -> backward -> apply',
+                                  'hogwild': 'hogwild: sharded lock-free parameter server (reference PS semantics)'
+                                  }[args.update]},
             'roofline': roofline, 'cpu_baseline': cpu, 'kernels': kernels,
             'final_loss': loss, 'params_finite': finite,
         }
         print(json.dumps(line), flush=True)
+    if ps is not None:
+        ps.close()
     if world > 1:
         dist.destroy_process_group()
 

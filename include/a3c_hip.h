@@ -175,6 +175,26 @@ int a3c_matmul(const float* A, int64_t sam, int64_t sak, const float* B, int64_t
 int a3c_copy_params(float* dst, const float* src, int64_t n, void* stream);
 
 /* ----------------------------------------------------------------------------
+ * Hogwild parameter server across GPUs (main.py:58-66 ps with unlocked RMSProp,
+ * SURVEY §8(e) "async"): every GPU owns a byte-range shard of params / ms / mom in
+ * its HBM, exported over IPC; workers push clipped gradients straight into every
+ * shard with an unlocked elementwise RMSProp over xGMI and pull the parameters back
+ * at rollout start (theta' <- theta, network.py:96-107).
+ *  a3c_dev_alloc/free: plain hipMalloc'd device memory (IPC-exportable base pointer).
+ *  a3c_ipc_handle:     64-byte hipIpcMemHandle of such a base pointer.
+ *  a3c_ipc_open/close: map a peer's handle (lazy peer access) into this process.
+ *  a3c_rmsprop_range:  TF ApplyRMSProp on n elements (w, ms, mom may live on a peer
+ *                      GPU); lr read from lr_dev[0] when lr_dev != NULL.
+ * -------------------------------------------------------------------------- */
+int a3c_dev_alloc(int64_t bytes, void** out);
+int a3c_dev_free(void* p);
+int a3c_ipc_handle(void* base, void* handle64);
+int a3c_ipc_open(const void* handle64, void** out);
+int a3c_ipc_close(void* p);
+int a3c_rmsprop_range(float* w, float* ms, float* mom, const float* grads, int64_t n, const float* lr_dev,
+                      float lr, float rho, float momentum, float eps, void* stream);
+
+/* ----------------------------------------------------------------------------
  * Batched synthetic Atari env (gym/ALE is absent): the Environment / GymEnvironment interface
  * of environment.py:14-106 for E envs on device (dynamics: oracle/synthetic_env.py).
  *  new_game(random=0): environment.py:74-79; random=1: new_random_game :81-86 (mask nullable)
@@ -246,6 +266,9 @@ int a3c_engine_apply(a3c_engine* eng, void* stream);
 /* 1 if the last a3c_engine_rollout_grad produced a gradient (always, unless overlap and it
  * was the first call after reset) -- exchange / apply only then. */
 int a3c_engine_grad_ready(a3c_engine* eng);
+/* advance tau / global step as a3c_engine_apply does, without touching the parameters
+ * (Hogwild: the gradient went to the shared shards instead) */
+int a3c_engine_advance(a3c_engine* eng, void* stream);
 
 /* device pointers owned by the engine (valid until destroy) */
 typedef struct a3c_engine_buffers {
@@ -267,6 +290,7 @@ typedef struct a3c_engine_buffers {
   int32_t* env_frame; int32_t* env_lives; uint32_t* env_episode; uint32_t* env_step;
   uint32_t* env_len;
   int zs; int n_tensors; int64_t offsets[A3C_MAX_TENSORS]; int64_t sizes[A3C_MAX_TENSORS];
+  float* sched;            /* device: [0] learning rate of the last gradient (agent.py:393-395) */
 } a3c_engine_buffers;
 int a3c_engine_get_buffers(a3c_engine* eng, a3c_engine_buffers* out);
 /* same, with the rollout buffers (actions .. act_l3) of slot 0 or 1 (overlap: rollout k

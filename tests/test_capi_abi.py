@@ -76,7 +76,7 @@ int main(void) {
   F(a3c_engine_config, seed) F(a3c_engine_config, gamma) F(a3c_engine_config, max_step)
   F(a3c_engine_config, clip_norm) F(a3c_engine_config, ep_end_t) F(a3c_engine_config, discount) F(a3c_engine_config, overlap)
   F(a3c_engine_buffers, n_params) F(a3c_engine_buffers, ring_slots) F(a3c_engine_buffers, zs)
-  F(a3c_engine_buffers, offsets) F(a3c_engine_buffers, sizes)
+  F(a3c_engine_buffers, offsets) F(a3c_engine_buffers, sizes) F(a3c_engine_buffers, sched)
   return 0;
 }
 '''

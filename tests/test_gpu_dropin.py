@@ -340,3 +340,15 @@ def test_agent_double_q_and_dueling():
     duel.step, duel.total_loss, duel.total_q, duel.update_count = 10, 0., 0., 0
     duel.batch_update(True)
     assert duel.update_count == 1 and np.isfinite(duel.total_loss)
+
+
+@pytest.mark.parametrize('update', ['overlap', 'sync', 'hogwild'])
+def test_main_engine_mode_runs(tmp_path, update):
+    """main.py --mode engine (the batched drop-in for main.py:58-94) in every update mode."""
+    import main
+    eng = main.main(['--mode', 'engine', '--env_name', 'Breakout-v0', '--num_envs', '32', '--num_frames', '256',
+                     '--iterations', '6', '--log_every', '3', '--logdir', str(tmp_path), '--update', update])
+    torch.cuda.synchronize()
+    assert torch.isfinite(eng.params).all()
+    lines = open(tmp_path / 'engine.jsonl').read().splitlines()
+    assert len(lines) == 2

@@ -88,3 +88,81 @@ def test_two_ranks_stay_identical_and_match_manual_exchange(overlap):
     torch.cuda.synchronize()
     assert torch.equal(engs[0].params, engs[1].params)
     np.testing.assert_array_equal(engs[0].params.cpu().numpy(), res[0]['params'])
+
+
+# ------------------------------------------------------------------ Hogwild (SURVEY §8(e) async)
+def _hog_worker(rank, world, port, out, lockstep):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, 'async-rl-tensorflow_amd')]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK='0')
+    import torch.distributed as dist
+    from src.hogwild import HogwildPS
+    dist.init_process_group('gloo')
+    eng = _make(rank, world, False)
+    ps = HogwildPS(eng.params)
+    grads = []
+    for it in range(ITERS):
+        if lockstep:                      # deterministic order for the check: rank 0 then rank 1
+            for turn in range(world):
+                dist.barrier()
+                if turn == rank:
+                    eng.rollout_grad()
+                    grads.append(eng.grads.clone())
+                    ps.push(eng.grads, lr_dev=eng.sched_ptr)
+                    eng.advance()
+                    torch.cuda.synchronize()
+            dist.barrier()
+            ps.pull(eng.params)
+            torch.cuda.synchronize()
+        else:
+            eng.iterate_hogwild(ps)
+    torch.cuda.synchronize()
+    dist.barrier()
+    out[rank] = dict(shared=ps.gather().cpu().numpy(), params=eng.params.cpu().numpy(),
+                     finite=bool(torch.isfinite(eng.params).all().item()))
+    ps.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('lockstep', [True, False])
+def test_hogwild_sharded_ps(lockstep):
+    """Two ranks on one GPU push into each other's IPC-mapped shards.  Lock-step order must equal
+    a single process applying rank 0's then rank 1's clipped gradient each iteration; free-running
+    (the real unlocked mode) must stay finite with both ranks seeing the same shared params."""
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context('spawn')
+    with ctx.Manager() as m:
+        out = m.dict()
+        port = _free_port()
+        procs = [ctx.Process(target=_hog_worker, args=(r, world, port, out, lockstep)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(500)
+            assert p.exitcode == 0
+        res = dict(out)
+    np.testing.assert_array_equal(res[0]['shared'], res[1]['shared'])
+    assert res[0]['finite'] and res[1]['finite']
+    if not lockstep:
+        return
+    # replay: two engines, one shared RMSProp state applied in the same order
+    from oracle import ref_cpu as Rc
+    engs = [_make(r, world, False) for r in range(world)]
+    w = engs[0].params.clone()
+    ms, mom = torch.ones_like(w), torch.zeros_like(w)
+    from src._lib import lib, ptr, stream_handle
+    for it in range(ITERS):
+        for e in engs:
+            e.params.copy_(w)
+        for e in engs:
+            e.rollout_grad()
+            e.advance()
+            lib().a3c_rmsprop_range(ptr(w), ptr(ms), ptr(mom), ptr(e.grads), w.numel(),
+                                    __import__('ctypes').c_void_p(e.sched_ptr), 0.0, 0.99, 0.0, 0.1, stream_handle())
+            # the next engine of the same iteration still uses the start-of-iteration params
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(w.cpu().numpy(), res[0]['shared'])
