@@ -54,6 +54,7 @@ struct a3c_engine {
   EnvBufs env;
   EnvParams envp;
   int overlap, nslot;
+  int fused_screen;        // 1: screen kernel fused into the head (k_head_screen)
   Slot slot[2];
   float* loss;
   float* sumsq;
@@ -157,6 +158,8 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   e->E = cfg->num_envs;
   e->n = cfg->n_step;
   e->overlap = cfg->overlap ? 1 : 0;
+  e->fused_screen = 1;
+  if (const char* v = getenv("A3C_FUSED_SCREEN")) e->fused_screen = atoi(v) != 0;
   e->nslot = e->overlap ? 2 : 1;
   // ring: the states of one rollout (frames tau-3 .. tau+n); overlap keeps two rollouts' frames
   e->R = (e->overlap ? 2 * e->n : e->n) + HIST + (cfg->net.algo == A3C_ALGO_Q ? 1 : 0);
@@ -330,11 +333,18 @@ static int enqueue_rollout(a3c_engine* e, const Slot& sl, hipStream_t s) {
     sel.rewards = sl.rewards + o;
     sel.terms = sl.terms + o;
     sel.frames_out = sl.frames + o;
+    if (e->fused_screen) {      // Environment.screen of the new frame inside the head kernel
+      sel.pool = e->pool;
+      sel.ring = e->ring;
+      sel.R = e->R;
+    }
     rc = a3c_forward_launch(L, sl.P, sl.w1s, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
                             sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s);
     if (rc) return rc;
-    rc = a3c_env_screen_launch(E, sl.frames + o, e->pool, e->ring, e->R, e->counters, t, s);
-    if (rc) return rc;
+    if (!e->fused_screen) {
+      rc = a3c_env_screen_launch(E, sl.frames + o, e->pool, e->ring, e->R, e->counters, t, s);
+      if (rc) return rc;
+    }
   }
   if (!q) {
     // bootstrap V(s_{t+n}) with the same parameters (assets/a3c.png)
@@ -578,6 +588,20 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
         return a3c_fc_fwd_launch(sl.act_l2, e->params + L.off[T_FCW], e->params + L.off[T_FCB], sl.act_l3, E, s);
       case A3C_KER_ENV_STEP:
         return a3c_env_screen_launch(E, sl.frames, e->pool, e->ring, e->R, e->counters, 0, s);
+      case A3C_KER_HEAD_SCREEN: {
+        // head + action draw + Environment.screen of the last step's frames (env not stepped)
+        HeadSelect sel = {};
+        sel.mode = L.algo == A3C_ALGO_Q ? 1 : 0;
+        sel.k0 = e->k0; sel.k1 = e->k1;
+        sel.tau_ptr = e->counters; sel.tau_add = 0;
+        sel.env_id_base = e->cfg.env_id_base; sel.E = E; sel.par_E = E;
+        sel.eps = e->eps;
+        sel.actions = sl.actions;
+        sel.env_on = 0;
+        sel.frames_out = sl.frames;
+        sel.pool = e->pool; sel.ring = e->ring; sel.R = e->R;
+        return a3c_head_screen_launch(L, e->params, sl.act_l3, E, sl.z, sel, s);
+      }
       case A3C_KER_CONV_BWD: {
         const BwdPlan p = a3c_bwd_plan(L, e->nE);
         a3c_conv_bwd_set_compact(e->overlap != 0);

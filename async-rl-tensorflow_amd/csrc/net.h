@@ -95,6 +95,11 @@ struct HeadSelect {
   float* rewards;           // [E] observe-clipped reward (agent.py:154)
   uint8_t* terms;           // [E]
   int32_t* frames_out;      // [E] post-act frame index (the screen the history gets)
+  // fused Environment.screen of the post-act frame into the frame ring (engine rollout):
+  // ring slot (tau + 1) % R of env e <- screen(pool[frame]); null ring -> separate kernel
+  const uint8_t* pool;
+  uint8_t* ring;
+  int R;
 };
 
 // forward of B states; returns 0 or error

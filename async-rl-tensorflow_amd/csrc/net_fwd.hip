@@ -15,6 +15,7 @@
 #include "gemm.h"
 #include "net_bwd.h"
 #include "env_dev.h"
+#include "screen_atari.h"
 
 #define XB_BYTES (HIST * PLANE * 2)                  // 56448: state planes as bf16
 #define L1S_BYTES (C1_P * L1S_LD * 4)                // 32000
@@ -211,13 +212,10 @@ __device__ inline int32_t select_from_lanes(float myz, int lane, int A, const He
 }
 
 // head: one wave per state.  z[b][j] = h3[b] . W[:,j] + bias[j]
-__global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, int64_t B,
-                                                  const float* __restrict__ Wp, const float* __restrict__ bp,
-                                                  const float* __restrict__ Wv, const float* __restrict__ bv,
-                                                  int A, int zs, float* __restrict__ z, HeadSelect sel) {
-  const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
+// logits / value (or q) of row b by one wave: lane j returns z[b][j] (0 past the outputs)
+__device__ inline float head_row(const float* __restrict__ h3, int64_t b, const float* __restrict__ Wp,
+                                 const float* __restrict__ bp, const float* __restrict__ Wv,
+                                 const float* __restrict__ bv, int A, int lane) {
   float myz = 0.f;
   const int nout = A + (Wv ? 1 : 0);
   if (nout <= 8) {
@@ -236,45 +234,88 @@ __global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, 
     p += __shfl_xor(p, 8, 64);
     p += __shfl_xor(p, 16, 64);
     p += __shfl_xor(p, 32, 64);
-    // lane j (< 8) now holds output j in lane j (c == 0 lanes)
     const float zj = __shfl(p, lane & 7, 64);
     if (lane < A) myz = zj + bp[lane];
     else if (Wv && lane == A) myz = zj + bv[0];
-    if (lane < zs) z[b * zs + lane] = myz;
   } else {
-  f32x4 h = *(const f32x4*)(h3 + b * FC + 4 * lane);
-  for (int j = 0; j < A; ++j) {
-    const float* w = Wp + (int64_t)(4 * lane) * A + j;
-    float p = h[0] * w[0] + h[1] * w[A] + h[2] * w[2 * A] + h[3] * w[3 * A];
-    p = wave_sum(p);
-    if (lane == j) myz = p + bp[j];
-  }
-  if (Wv) {
-    f32x4 w = *(const f32x4*)(Wv + 4 * lane);
-    float p = wave_sum(h[0] * w[0] + h[1] * w[1] + h[2] * w[2] + h[3] * w[3]);
-    if (lane == A) myz = p + bv[0];
-  }
-  if (lane < zs) z[b * zs + lane] = myz;   // padding columns are 0
-  }
-  if (sel.mode >= 0) {
-    int32_t a = select_from_lanes(myz, lane, A, sel, b);
-    if (lane == 0) {
-      sel.actions[b] = a;
-      if (sel.env_on) {
-        const int64_t tau = *sel.tau_ptr + sel.tau_add;
-        const int e = (int)b;
-        const int64_t cur = (tau & 1) * (int64_t)sel.par_E + e, nxt = ((tau + 1) & 1) * (int64_t)sel.par_E + e;
-        const uint32_t id = (uint32_t)(sel.env_id_base + e);
-        EnvState s = env_load(sel.envb, cur);
-        env_act(s, sel.envp, id, (uint32_t)a, true);
-        sel.rewards[e] = fmaxf(-1.0f, fminf(1.0f, s.reward));   // observe clip, agent.py:154
-        sel.terms[e] = (uint8_t)s.terminal;
-        sel.frames_out[e] = s.frame;
-        if (s.terminal) env_new_random_game(s, sel.envp, id);    // agent.py:66-67
-        env_store(sel.envb, nxt, s);
-      }
+    f32x4 h = *(const f32x4*)(h3 + b * FC + 4 * lane);
+    for (int j = 0; j < A; ++j) {
+      const float* w = Wp + (int64_t)(4 * lane) * A + j;
+      float p = h[0] * w[0] + h[1] * w[A] + h[2] * w[2 * A] + h[3] * w[3 * A];
+      p = wave_sum(p);
+      if (lane == j) myz = p + bp[j];
+    }
+    if (Wv) {
+      f32x4 w = *(const f32x4*)(Wv + 4 * lane);
+      float p = wave_sum(h[0] * w[0] + h[1] * w[1] + h[2] * w[2] + h[3] * w[3]);
+      if (lane == A) myz = p + bv[0];
     }
   }
+  return myz;
+}
+
+// action draw for row b (all lanes) and, in lane 0, the fused env act (agent.py:59-62).
+// Returns the post-act frame index in lane 0 when the env is stepped, else -1.
+__device__ inline int32_t head_act(float myz, int lane, int A, const HeadSelect& sel, int64_t b) {
+  int32_t frame = -1;
+  const int32_t a = select_from_lanes(myz, lane, A, sel, b);
+  if (lane == 0) {
+    sel.actions[b] = a;
+    if (sel.env_on) {
+      const int64_t tau = *sel.tau_ptr + sel.tau_add;
+      const int e = (int)b;
+      const int64_t cur = (tau & 1) * (int64_t)sel.par_E + e, nxt = ((tau + 1) & 1) * (int64_t)sel.par_E + e;
+      const uint32_t id = (uint32_t)(sel.env_id_base + e);
+      EnvState s = env_load(sel.envb, cur);
+      env_act(s, sel.envp, id, (uint32_t)a, true);
+      sel.rewards[e] = fmaxf(-1.0f, fminf(1.0f, s.reward));   // observe clip, agent.py:154
+      sel.terms[e] = (uint8_t)s.terminal;
+      sel.frames_out[e] = s.frame;
+      frame = s.frame;
+      if (s.terminal) env_new_random_game(s, sel.envp, id);    // agent.py:66-67
+      env_store(sel.envb, nxt, s);
+    }
+  }
+  return frame;
+}
+
+// head: one wave per state.  z[b][j] = h3[b] . W[:,j] + bias[j]
+__global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, int64_t B,
+                                                  const float* __restrict__ Wp, const float* __restrict__ bp,
+                                                  const float* __restrict__ Wv, const float* __restrict__ bv,
+                                                  int A, int zs, float* __restrict__ z, HeadSelect sel) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float myz = head_row(h3, b, Wp, bp, Wv, bv, A, lane);
+  if (lane < zs) z[b * zs + lane] = myz;   // padding columns are 0
+  if (sel.mode >= 0) (void)head_act(myz, lane, A, sel, b);
+}
+
+// engine rollout step tail, one workgroup per env: head + action draw + env act (wave 0), then
+// the whole workgroup computes Environment.screen (environment.py:49-53, bit-exact) of the
+// post-act frame straight from the HBM pool into the env's frame-ring slot
+#define HS_THREADS 512
+__global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restrict__ h3,
+                                                            const float* __restrict__ Wp,
+                                                            const float* __restrict__ bp,
+                                                            const float* __restrict__ Wv,
+                                                            const float* __restrict__ bv, int A, int zs,
+                                                            float* __restrict__ z, HeadSelect sel) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ int32_t s_frame;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = blockIdx.x;
+  if (threadIdx.x < 64) {
+    const float myz = head_row(h3, b, Wp, bp, Wv, bv, A, lane);
+    if (lane < zs) z[b * zs + lane] = myz;
+    const int32_t f = head_act(myz, lane, A, sel, b);
+    if (lane == 0) s_frame = f >= 0 ? f : sel.frames_out[b];   // env_on = 0 (kernel timing): last frame
+  }
+  __syncthreads();
+  const int64_t tau = *sel.tau_ptr + sel.tau_add;
+  atari::screen_frame<HS_THREADS>(sel.pool + (int64_t)s_frame * (atari::IH * atari::IW * 3),
+                                  sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE, smem);
 }
 
 __global__ void __launch_bounds__(256) k_select(const float* __restrict__ z, int64_t B, int zs, int A,
@@ -300,7 +341,22 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint16_t* 
   if (rc) return rc;
   const float* Wv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VW] : nullptr;
   const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
-  hipLaunchKernelGGL(k_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, act_l3, B,
+  if (sel.mode >= 0 && sel.env_on && sel.ring)
+    hipLaunchKernelGGL(k_head_screen, dim3((unsigned)B), dim3(HS_THREADS), SCREEN_FRAME_SMEM, s, act_l3,
+                       P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel);
+  else
+    hipLaunchKernelGGL(k_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, act_l3, B,
+                       P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+// the fused head + env act + screen of one rollout step (profiling hook; see engine.hip)
+int a3c_head_screen_launch(const NetLayout& L, const float* P, const float* act_l3, int64_t B, float* z,
+                           const HeadSelect& sel, hipStream_t s) {
+  const float* Wv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VW] : nullptr;
+  const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
+  hipLaunchKernelGGL(k_head_screen, dim3((unsigned)B), dim3(HS_THREADS), SCREEN_FRAME_SMEM, s, act_l3,
                      P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel);
   A3C_CHECK(hipGetLastError());
   return 0;
@@ -329,6 +385,7 @@ int a3c_select_launch(const float* z, int64_t B, int zs, int A, const HeadSelect
 void a3c_conv12_set_smem() {
   (void)hipFuncSetAttribute((const void*)k_conv12_fwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize, CONV12_SMEM);
   (void)hipFuncSetAttribute((const void*)k_conv12_fwd<false>, hipFuncAttributeMaxDynamicSharedMemorySize, CONV12_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_head_screen, hipFuncAttributeMaxDynamicSharedMemorySize, SCREEN_FRAME_SMEM);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -85,6 +85,79 @@ __device__ inline uint32_t lum_exact(uint32_t r, uint32_t g, uint32_t b) {
   return q;
 }
 
+// 16 pixels (48 bytes of RGB) -> 16 luminance bytes
+__device__ inline uint4 lum16(const uint4 a, const uint4 b, const uint4 c) {
+  const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+  uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int p = 0; p < 16; ++p) {
+    const int i0 = 3 * p, i1 = 3 * p + 1, i2 = 3 * p + 2;
+    const uint32_t rr = (w[i0 >> 2] >> (8 * (i0 & 3))) & 255u;
+    const uint32_t gg = (w[i1 >> 2] >> (8 * (i1 & 3))) & 255u;
+    const uint32_t bb = (w[i2 >> 2] >> (8 * (i2 & 3))) & 255u;
+    o[p >> 2] |= lum_exact(rr, gg, bb) << (8 * (p & 3));
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// Whole-frame Environment.screen by one workgroup of NT threads (gray 210x160 and the
+// horizontal-pass 210x84 in LDS, SCREEN_FRAME_SMEM bytes); the RGB frame streams from HBM
+// straight into registers (all of a thread's loads issued before any use).
+#define SCREEN_FRAME_SMEM (210 * 160 + 210 * 84)
+template <int NT>
+__device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __restrict__ out, uint8_t* smem) {
+  uint8_t* gray = smem;
+  uint8_t* tmp = smem + IH * IW;
+  const int tid = threadIdx.x;
+  constexpr int NUNIT = IH * IW / 16;                  // 2100 units of 16 pixels
+  constexpr int PER = (NUNIT + NT - 1) / NT;
+  uint4 r[PER][3];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint4* s = (const uint4*)(rgb + 48 * min(tid + NT * j, NUNIT - 1));
+    r[j][0] = s[0];
+    r[j][1] = s[1];
+    r[j][2] = s[2];
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int u = tid + NT * j;
+    if (u < NUNIT) *(uint4*)(gray + 16 * u) = lum16(r[j][0], r[j][1], r[j][2]);
+  }
+  __syncthreads();
+  constexpr int RP = NT / OW;                          // row phases
+  const int xx = tid % OW, rp = tid / OW;
+  if (rp < RP) {
+    const int x0 = cH.xmin[xx];
+    int kk[KH], off[KH];
+#pragma unroll
+    for (int x = 0; x < KH; ++x) {
+      kk[x] = cH.k[xx][x];
+      off[x] = min(x0 + x, IW - 1);
+    }
+    for (int rr = rp; rr < IH; rr += RP) {
+      const uint8_t* s = gray + rr * IW;
+      int acc = 1 << (A3C_PRECISION_BITS - 1);
+#pragma unroll
+      for (int x = 0; x < KH; ++x) acc += (int)s[off[x]] * kk[x];
+      tmp[rr * OW + xx] = a3c_clip8(acc);
+    }
+  }
+  __syncthreads();
+  if (rp < RP) {
+    for (int yy = rp; yy < OH; yy += RP) {
+      const int b0 = cV.xmin[yy];
+      int acc = 1 << (A3C_PRECISION_BITS - 1);
+#pragma unroll
+      for (int y = 0; y < KV; ++y) {
+        const int ry = min(b0 + y, IH - 1);
+        acc += (int)tmp[ry * OW + xx] * cV.k[yy][y];
+      }
+      out[yy * OW + xx] = a3c_clip8(acc);
+    }
+  }
+}
+
 template <int ROWS>
 struct Smem {
   static constexpr int SR = max_src_rows<ROWS>();
@@ -124,18 +197,7 @@ __device__ inline void screen_band(const uint8_t* __restrict__ rgb, uint8_t* __r
   const int nunit = (y1 - y0) * (IW / 16);
   for (int u = tid; u < nunit; u += 256) {
     const uint4* r4 = (const uint4*)(raw + 48 * u);
-    const uint4 a = r4[0], b = r4[1], c = r4[2];
-    const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
-    uint32_t o[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int p = 0; p < 16; ++p) {
-      const int i0 = 3 * p, i1 = 3 * p + 1, i2 = 3 * p + 2;
-      const uint32_t rr = (w[i0 >> 2] >> (8 * (i0 & 3))) & 255u;
-      const uint32_t gg = (w[i1 >> 2] >> (8 * (i1 & 3))) & 255u;
-      const uint32_t bb = (w[i2 >> 2] >> (8 * (i2 & 3))) & 255u;
-      o[p >> 2] |= lum_exact(rr, gg, bb) << (8 * (p & 3));
-    }
-    *(uint4*)(gray + 16 * u) = make_uint4(o[0], o[1], o[2], o[3]);
+    *(uint4*)(gray + 16 * u) = lum16(r4[0], r4[1], r4[2]);
   }
   __syncthreads();
 

@@ -112,7 +112,7 @@ SIGNATURES = {
     'a3c_engine_time_kernel': (c_int, [c_void_p, c_int, c_int, c_void_p, ctypes.POINTER(c_float)]),
 }
 
-KER_CONV12_FWD, KER_FC_FWD, KER_ENV_STEP, KER_CONV_BWD = 0, 1, 2, 3
+KER_CONV12_FWD, KER_FC_FWD, KER_ENV_STEP, KER_CONV_BWD, KER_HEAD_SCREEN = 0, 1, 2, 3, 4
 
 _lib = None
 

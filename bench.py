@@ -154,14 +154,14 @@ def main():
             'k_conv12_fwd': eng.time_kernel(_lib.KER_CONV12_FWD, 20),
             'k_conv_bwd': eng.time_kernel(_lib.KER_CONV_BWD, 10),
             'k_fc_fwd': eng.time_kernel(_lib.KER_FC_FWD, 20),
-            'k_env_screen': eng.time_kernel(_lib.KER_ENV_STEP, 20),
+            'k_head_screen': eng.time_kernel(_lib.KER_HEAD_SCREEN, 20),
         }
-        count = {'k_conv12_fwd': n + 1, 'k_conv_bwd': 1, 'k_fc_fwd': n + 1, 'k_env_screen': n}
+        count = {'k_conv12_fwd': n + 1, 'k_conv_bwd': 1, 'k_fc_fwd': n + 1, 'k_head_screen': n}
         work = {
             'k_conv12_fwd': ('mfma', CONV12_FWD_FLOP * E),
             'k_conv_bwd': ('mfma', CONV_BWD_FLOP * n * E),
             'k_fc_fwd': ('mfma', FC_FWD_FLOP * E),
-            'k_env_screen': ('hbm', ENV_STEP_BYTES * E),
+            'k_head_screen': ('hbm', ENV_STEP_BYTES * E),
         }
         iter_ms = el / args.steps * 1e3
         for k in ms:
