@@ -57,7 +57,7 @@ extern "C" int a3c_workspace_bytes(const a3c_net_desc* net, int64_t B, int64_t* 
     return a3c_set_error(A3C_ERR_INVALID, "a3c_workspace_bytes", "bad argument");
   // forward: the bf16-split conv1 weights; backward: its plan (they never run at once)
   BwdPlan p = a3c_bwd_plan(L, B > 0 ? B : 1);
-  int64_t m = p.total > W1S_ELEMS / 2 ? p.total : W1S_ELEMS / 2;
+  int64_t m = p.total > PREP_BYTES / 4 ? p.total : PREP_BYTES / 4;
   *bytes = m * (int64_t)sizeof(float) + 256;
   return 0;
 }
@@ -90,10 +90,10 @@ extern "C" int a3c_forward(const a3c_net_desc* net, const float* params, const u
   HeadSelect sel = {};
   sel.mode = -1;
   sel.E = 1;
-  uint16_t* w1s = (uint16_t*)align_ws(workspace);
-  int rc = a3c_split_w1_launch(params + L.off[T_L1W], w1s, (hipStream_t)stream);
+  uint8_t* prep = (uint8_t*)align_ws(workspace);
+  int rc = a3c_prep_fwd_launch(L, params, prep, (hipStream_t)stream);
   if (rc) return rc;
-  return a3c_forward_launch(L, params, w1s, contiguous_states(states, B), B, act_l1, act_l2, act_l3, z, sel,
+  return a3c_forward_launch(L, params, prep, contiguous_states(states, B), B, act_l1, act_l2, act_l3, z, sel,
                             (hipStream_t)stream);
 }
 

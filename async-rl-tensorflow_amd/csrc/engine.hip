@@ -20,7 +20,8 @@
 #include "gemm.h"
 
 void a3c_init_once();
-int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s);
+int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s,
+                      const float* Wrows = nullptr);
 
 // Per-rollout buffers.  Sync mode has one slot whose params are the live parameters and whose
 // tau is the live frame counter.  Overlap mode (cfg.overlap = 1) has two: rollout k fills slot
@@ -38,7 +39,7 @@ struct Slot {
   float* R_buf;            // [n][E] returns / TD targets
   float *act_l1, *act_l2, *act_l3;
   float *scr_l2, *scr_l3;  // bootstrap / target forward scratch
-  uint16_t* w1s;           // conv1 weights of P split into bf16 terms (net_fwd.hip)
+  uint8_t* prep;           // forward weights of P prepared for the kernels (k_prep_fwd)
 };
 
 struct a3c_engine {
@@ -59,7 +60,7 @@ struct a3c_engine {
   float* loss;
   float* sumsq;
   float* zt;               // q: target-net q values [nE][zs]
-  uint16_t* w1s_t;         // q: split conv1 weights of the target network
+  uint8_t* prep_t;         // q: prepared forward weights of the target network
   float* eps;              // q: per env epsilon
   float* ep_end;           // q: per env final epsilon
   float* ws;               // backward workspace
@@ -208,9 +209,9 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     ALLOC(sl.act_l3, nE * FC * 4);
     ALLOC(sl.scr_l2, scrB * FLAT * 4);
     ALLOC(sl.scr_l3, scrB * FC * 4);
-    ALLOC(sl.w1s, W1S_ELEMS * 2);
+    ALLOC(sl.prep, PREP_BYTES);
   }
-  ALLOC(e->w1s_t, W1S_ELEMS * 2);
+  ALLOC(e->prep_t, PREP_BYTES);
   ALLOC(e->zt, scrB * zs * 4);
   ALLOC(e->eps, E * 4);
   ALLOC(e->ep_end, E * 4);
@@ -224,7 +225,13 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "tensor table");
   }
   if (e->overlap) {
-    bool ok = hipStreamCreateWithFlags(&e->rs, hipStreamNonBlocking) == hipSuccess &&
+    // the rollout is a serial chain of small kernels: give its stream the higher priority so
+    // its workgroups are dispatched first when the concurrent backward frees CU resources
+    int lo_prio = 0, hi_prio = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
+    int prio = hi_prio;
+    if (const char* v = getenv("A3C_ROLLOUT_PRIO")) prio = atoi(v) ? hi_prio : lo_prio;
+    bool ok = hipStreamCreateWithPriority(&e->rs, hipStreamNonBlocking, prio) == hipSuccess &&
               hipEventCreateWithFlags(&e->ev_start, hipEventDisableTiming) == hipSuccess;
     for (int k = 0; k < 2 && ok; ++k)
       ok = hipEventCreateWithFlags(&e->ev_roll[k], hipEventDisableTiming) == hipSuccess;
@@ -310,7 +317,7 @@ static int enqueue_rollout(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const NetLayout& L = e->L;
   const int E = e->E, n = e->n, zs = L.zs;
   const bool q = L.algo == A3C_ALGO_Q;
-  int rc = a3c_split_w1_launch(sl.P + L.off[T_L1W], sl.w1s, s);   // params are fixed for the rollout
+  int rc = a3c_prep_fwd_launch(L, sl.P, sl.prep, s);   // params are fixed for the rollout
   if (rc) return rc;
   if (q) {
     hipLaunchKernelGGL(k_eps, dim3((E + 255) / 256), dim3(256), 0, s, e->eps, e->ep_end, E, e->counters,
@@ -338,7 +345,7 @@ static int enqueue_rollout(a3c_engine* e, const Slot& sl, hipStream_t s) {
       sel.ring = e->ring;
       sel.R = e->R;
     }
-    rc = a3c_forward_launch(L, sl.P, sl.w1s, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
+    rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
                             sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s);
     if (rc) return rc;
     if (!e->fused_screen) {
@@ -351,7 +358,7 @@ static int enqueue_rollout(a3c_engine* e, const Slot& sl, hipStream_t s) {
     HeadSelect none = {};
     none.mode = -1;
     none.E = E;
-    rc = a3c_forward_launch(L, sl.P, sl.w1s, ring_addr(e, n, e->counters), E, nullptr, sl.scr_l2, sl.scr_l3,
+    rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, n, e->counters), E, nullptr, sl.scr_l2, sl.scr_l3,
                             sl.z + e->nE * zs, none, s);
     if (rc) return rc;
   }
@@ -384,9 +391,9 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
     HeadSelect none = {};
     none.mode = -1;
     none.E = E;
-    rc = a3c_split_w1_launch(e->tparams + L.off[T_L1W], e->w1s_t, s);
+    rc = a3c_prep_fwd_launch(L, e->tparams, e->prep_t, s);
     if (rc) return rc;
-    rc = a3c_forward_launch(L, e->tparams, e->w1s_t, ring_addr(e, 1, sl.tau), e->nE, nullptr, sl.scr_l2,
+    rc = a3c_forward_launch(L, e->tparams, e->prep_t, ring_addr(e, 1, sl.tau), e->nE, nullptr, sl.scr_l2,
                             sl.scr_l3, e->zt, none, s);
     if (rc) return rc;
     rc = a3c_td_target_launch(sl.rewards, sl.terms, e->zt, e->nE, L.A, zs, c.discount, sl.R_buf, s);
@@ -576,16 +583,17 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
   const int E = e->E;
   const Slot& sl = e->slot[0];
   if (e->rs) A3C_CHECK(hipStreamSynchronize(e->rs));
-  if (kernel == A3C_KER_CONV12_FWD) {
-    int rc0 = a3c_split_w1_launch(e->params + L.off[T_L1W], sl.w1s, s);
+  if (kernel == A3C_KER_CONV12_FWD || kernel == A3C_KER_FC_FWD) {
+    int rc0 = a3c_prep_fwd_launch(L, e->params, sl.prep, s);
     if (rc0) return rc0;
   }
   auto launch = [&]() -> int {
     switch (kernel) {
       case A3C_KER_CONV12_FWD:
-        return a3c_conv12_launch(L, e->params, sl.w1s, ring_addr(e, 0, e->counters), E, sl.act_l1, sl.act_l2, s);
+        return a3c_conv12_launch(L, e->params, sl.prep, ring_addr(e, 0, e->counters), E, sl.act_l1, sl.act_l2, s);
       case A3C_KER_FC_FWD:
-        return a3c_fc_fwd_launch(sl.act_l2, e->params + L.off[T_FCW], e->params + L.off[T_FCB], sl.act_l3, E, s);
+        return a3c_fc_fwd_launch(sl.act_l2, (const float*)(sl.prep + PREP_W1S_BYTES), e->params + L.off[T_FCB],
+                                 sl.act_l3, E, s, e->params + L.off[T_FCW]);
       case A3C_KER_ENV_STEP:
         return a3c_env_screen_launch(E, sl.frames, e->pool, e->ring, e->R, e->counters, 0, s);
       case A3C_KER_HEAD_SCREEN: {

@@ -103,12 +103,16 @@ struct HeadSelect {
 };
 
 // forward of B states; returns 0 or error
-// w1s: conv1 weights split into bf16 terms (a3c_split_w1_launch, W1S_ELEMS u16)
-int a3c_forward_launch(const NetLayout& L, const float* params, const uint16_t* w1s, const StateAddr& sa,
+// prep: the forward's prepared weights of `params` (a3c_prep_fwd_launch, PREP_BYTES):
+// conv1 split into bf16 terms (W1S_ELEMS u16) then the fc weights in MFMA fragment order
+#define W1S_ELEMS (C1_K * 3 * 64 * 8)   // 12288 bf16
+#define PREP_W1S_BYTES (W1S_ELEMS * 2)  // 24576
+#define FC_CH (FLAT / 16)               // 162 K-chunks of 16
+#define PREP_BYTES (PREP_W1S_BYTES + FLAT * FC * 4)
+int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* prep, const StateAddr& sa,
                        int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
                        hipStream_t s);
-#define W1S_ELEMS (C1_K * 3 * 64 * 8)   // 12288 bf16
-int a3c_split_w1_launch(const float* W1, uint16_t* w1s, hipStream_t s);
+int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s);
 
 // stage the HIST u8 planes of state b into LDS (HIST x 441 uint4)
 __device__ inline void stage_state(const StateAddr& sa, int64_t b, int64_t tau0, uint8_t* x8) {

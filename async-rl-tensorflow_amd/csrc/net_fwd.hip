@@ -1,3 +1,4 @@
+#include <cstdlib>
 // Forward of the NIPS trunk + heads on gfx950 matrix cores.
 //
 //  k_conv12_fwd : one workgroup per state.  The 4 u8 frame planes (28 KB) are staged in LDS;
@@ -35,25 +36,42 @@ __device__ inline uint32_t bf16_rn_bits(float f) {
   return u >> 16;
 }
 
-__global__ void __launch_bounds__(256) k_split_w1(const float* __restrict__ W1, uint16_t* __restrict__ w1s) {
+// Forward weight preparation, once per parameter version (rollout start): the conv1 bf16
+// terms above and the fc weights in MFMA fragment order, Wp[ct][c][lane][c4] =
+// W[16c + 4(lane>>4) + c4][16ct + (lane&15)], so a lane's B operands for 4 MFMAs are one 16-byte load.
+__global__ void __launch_bounds__(256) k_prep_fwd(const float* __restrict__ W1, const float* __restrict__ Wfc,
+                                                  uint8_t* __restrict__ prep) {
 #pragma clang fp contract(off)
-  const int t = blockIdx.x * 256 + threadIdx.x;            // (kh, lane, j): 8 * 64 * 8
-  if (t >= C1_K * 64 * 8) return;
-  const int kh = t >> 9, lane = (t >> 3) & 63, j = t & 7;
-  const int g = lane >> 4, i = lane & 15;
-  const float w = W1[((kh * C1_K + j) * HIST + g) * C1_N + i];
-  const uint32_t h = bf16_rn_bits(w);
-  const float r1 = w - __uint_as_float(h << 16);
-  const uint32_t m = bf16_rn_bits(r1);
-  const float r2 = r1 - __uint_as_float(m << 16);
-  const uint32_t l = bf16_rn_bits(r2);
-  w1s[((kh * 3 + 0) * 64 + lane) * 8 + j] = (uint16_t)h;
-  w1s[((kh * 3 + 1) * 64 + lane) * 8 + j] = (uint16_t)m;
-  w1s[((kh * 3 + 2) * 64 + lane) * 8 + j] = (uint16_t)l;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t < C1_K * 64 * 8) {                                   // (kh, lane, j): conv1 split
+    uint16_t* w1s = (uint16_t*)prep;
+    const int kh = t >> 9, lane = (t >> 3) & 63, j = t & 7;
+    const int g = lane >> 4, i = lane & 15;
+    const float w = W1[((kh * C1_K + j) * HIST + g) * C1_N + i];
+    const uint32_t h = bf16_rn_bits(w);
+    const float r1 = w - __uint_as_float(h << 16);
+    const uint32_t m = bf16_rn_bits(r1);
+    const float r2 = r1 - __uint_as_float(m << 16);
+    const uint32_t l = bf16_rn_bits(r2);
+    w1s[((kh * 3 + 0) * 64 + lane) * 8 + j] = (uint16_t)h;
+    w1s[((kh * 3 + 1) * 64 + lane) * 8 + j] = (uint16_t)m;
+    w1s[((kh * 3 + 2) * 64 + lane) * 8 + j] = (uint16_t)l;
+    return;
+  }
+  const int q = t - C1_K * 64 * 8;                          // (ct, c, lane): one f32x4 of the fc pack
+  if (q >= (FC / 16) * FC_CH * 64) return;
+  const int lane = q & 63, c = (q >> 6) % FC_CH, ct = (q >> 6) / FC_CH;
+  const int j4 = lane >> 4, n = 16 * ct + (lane & 15);
+  f32x4 v;
+#pragma unroll
+  for (int c4 = 0; c4 < 4; ++c4) v[c4] = Wfc[(int64_t)(16 * c + 4 * j4 + c4) * FC + n];
+  ((f32x4*)(prep + PREP_W1S_BYTES))[q] = v;
 }
 
-int a3c_split_w1_launch(const float* W1, uint16_t* w1s, hipStream_t s) {
-  hipLaunchKernelGGL(k_split_w1, dim3(C1_K * 64 * 8 / 256), dim3(256), 0, s, W1, w1s);
+int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s) {
+  const int total = C1_K * 64 * 8 + (FC / 16) * FC_CH * 64;
+  hipLaunchKernelGGL(k_prep_fwd, dim3((total + 255) / 256), dim3(256), 0, s, P + L.off[T_L1W], P + L.off[T_FCW],
+                     prep);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
@@ -328,16 +346,18 @@ __global__ void __launch_bounds__(256) k_select(const float* __restrict__ z, int
   if (lane == 0) sel.actions[b] = a;
 }
 
-int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s);
+int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s,
+                      const float* Wrows = nullptr);
 
-int a3c_forward_launch(const NetLayout& L, const float* params, const uint16_t* w1s, const StateAddr& sa,
+int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* prep, const StateAddr& sa,
                        int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
                        hipStream_t s) {
   if (B <= 0) return 0;
   const float* P = params;
-  int rc0 = a3c_conv12_launch(L, P, w1s, sa, B, act_l1, act_l2, s);
+  int rc0 = a3c_conv12_launch(L, P, prep, sa, B, act_l1, act_l2, s);
   if (rc0) return rc0;
-  int rc = a3c_fc_fwd_launch(act_l2, P + L.off[T_FCW], P + L.off[T_FCB], act_l3, B, s);
+  int rc = a3c_fc_fwd_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), P + L.off[T_FCB], act_l3, B, s,
+                             P + L.off[T_FCW]);
   if (rc) return rc;
   const float* Wv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VW] : nullptr;
   const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
@@ -362,9 +382,10 @@ int a3c_head_screen_launch(const NetLayout& L, const float* P, const float* act_
   return 0;
 }
 
-int a3c_conv12_launch(const NetLayout& L, const float* P, const uint16_t* w1s, const StateAddr& sa, int64_t B,
+int a3c_conv12_launch(const NetLayout& L, const float* P, const uint8_t* prep, const StateAddr& sa, int64_t B,
                       float* act_l1, float* act_l2, hipStream_t s) {
-  if (!w1s) return a3c_set_error(A3C_ERR_INVALID, "a3c_conv12_launch", "split conv1 weights missing");
+  if (!prep) return a3c_set_error(A3C_ERR_INVALID, "a3c_conv12_launch", "prepared forward weights missing");
+  const uint16_t* w1s = (const uint16_t*)prep;
   if (act_l1)
     hipLaunchKernelGGL((k_conv12_fwd<true>), dim3((unsigned)B), dim3(512), CONV12_SMEM, s, sa, B, w1s,
                        P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2);
@@ -390,12 +411,66 @@ void a3c_conv12_set_smem() {
 
 // ---------------------------------------------------------------------------------------
 // fc layer of the rollout (agent.py:251 / network.py:447): l3 = relu(l2 @ W + b) for a
-// skinny batch (M = E states, N = 256, K = 2592).  One workgroup per 16x16 output tile, the
-// 4 waves split K four ways on v_mfma_f32_16x16x4_f32 and meet in LDS: no split-K slab, no
-// second launch.  Operands stream from L2 straight to registers (A as 16-byte rows, B as
-// 64-byte row segments); K is walked in 16-wide chunks with the next chunk prefetched.
+// skinny batch (M = E states, N = 256, K = 2592).  One workgroup per 16x16 output tile; the
+// 4 waves split the 162 K-chunks of 16 and meet in LDS.  Per chunk a lane loads one 16-byte A
+// fragment (4 consecutive k of its row) and one 16-byte B fragment from the fragment-packed
+// weights (k_prep_fwd), feeding 4 v_mfma_f32_16x16x4_f32; a ring of D chunks keeps 2D loads in
+// flight per wave.  blockIdx.x (column tile) is the fast grid index, so the 8 XCDs each stream
+// 2 column tiles of W (L2-resident) and the l2 rows.
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_fc_fwd(const float* __restrict__ A, const float* __restrict__ W,
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_fc_fwd(const float* __restrict__ A, const float* __restrict__ Wp,
+                                                    const float* __restrict__ bias, float* __restrict__ C, int M) {
+  __shared__ f32x4 red[NW - 1][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i16 = lane & 15, j4 = lane >> 4;
+  const int ct = blockIdx.x;
+  const int m0 = blockIdx.y * 16, n0 = ct * 16;
+  const int m = min(m0 + i16, M - 1);
+  // chunks [c0, c1) of this wave: the 162 chunks split as evenly as possible
+  const int c0 = (wid * FC_CH) / NW, c1 = ((wid + 1) * FC_CH) / NW;
+  constexpr int D = 8;
+  const float* a = A + (int64_t)m * FLAT + 4 * j4;
+  const f32x4* b = (const f32x4*)Wp + (int64_t)ct * FC_CH * 64 + lane;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 ra[D], rb[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    ra[d] = *(const f32x4*)(a + 16 * (c0 + d));
+    rb[d] = b[(int64_t)(c0 + d) * 64];
+  }
+  for (int c = c0; c < c1; c += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (c + d < c1) {
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][c4], rb[d][c4], acc, 0, 0, 0);
+        const int cn = c + d + D;                 // refill this slot with chunk cn
+        if (cn < c1) {
+          ra[d] = *(const f32x4*)(a + 16 * cn);
+          rb[d] = b[(int64_t)cn * 64];
+        }
+      }
+    }
+  }
+  if (wid > 0) red[wid - 1][lane] = acc;
+  __syncthreads();
+  if (wid == 0) {
+#pragma unroll
+    for (int w = 0; w < NW - 1; ++w) acc += red[w][lane];
+    const int n = n0 + i16;
+    const float bb = bias[n];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + 4 * j4 + r;
+      if (row < M) C[(int64_t)row * FC + n] = fmaxf(acc[r] + bb, 0.f);
+    }
+  }
+}
+
+// row-major-weight variant (4 scalar B loads per chunk), kept for A/B measurement
+__global__ void __launch_bounds__(256) k_fc_fwd_rows(const float* __restrict__ A, const float* __restrict__ W,
                                                 const float* __restrict__ bias, float* __restrict__ C, int M) {
   __shared__ f32x4 red[3][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -456,9 +531,19 @@ __global__ void __launch_bounds__(256) k_fc_fwd(const float* __restrict__ A, con
   }
 }
 
-int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s) {
+int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s,
+                      const float* Wrows) {
   if (M <= 0) return 0;
-  hipLaunchKernelGGL(k_fc_fwd, dim3(FC / 16, (unsigned)((M + 15) / 16)), dim3(256), 0, s, A, W, bias, C, (int)M);
+  static const int nw = getenv("A3C_FC_WAVES") ? atoi(getenv("A3C_FC_WAVES")) : 4;
+  if (nw == 0 && Wrows)
+    hipLaunchKernelGGL(k_fc_fwd_rows, dim3(FC / 16, (unsigned)((M + 15) / 16)), dim3(256), 0, s, A, Wrows, bias, C,
+                       (int)M);
+  else if (nw == 4)
+    hipLaunchKernelGGL(k_fc_fwd<4>, dim3(FC / 16, (unsigned)((M + 15) / 16)), dim3(256), 0, s, A, W, bias, C, (int)M);
+  else if (nw == 16)
+    hipLaunchKernelGGL(k_fc_fwd<16>, dim3(FC / 16, (unsigned)((M + 15) / 16)), dim3(1024), 0, s, A, W, bias, C, (int)M);
+  else
+    hipLaunchKernelGGL(k_fc_fwd<8>, dim3(FC / 16, (unsigned)((M + 15) / 16)), dim3(512), 0, s, A, W, bias, C, (int)M);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
