@@ -1,3 +1,4 @@
+#include <cstdlib>
 // Loss + backward of the NIPS trunk on gfx950.
 //
 //  k_returns     n-step return per env in float64 (assets/a3c.png Algorithm S3).
@@ -137,10 +138,11 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ z, i
 #define CB_L1ST (C1_P * C1_N * 4)            // 25600: linear DMA staging of l1
 #define CB_DL2ST (FLAT * 4)                  // 10368: linear DMA staging of dl2
 // LDS: x8[2] | l1 stage | dl2 stage | l1s (dl1 written in place) | dl2s | red
-#define CB_SMEM_DMA (2 * CB_X8 + CB_L1ST + CB_DL2ST + CB_L1 + CB_DL2 + 4 * 64 * 4)   // 137104
+#define CB_RED (8 * 64 * 4)
+#define CB_SMEM_DMA (2 * CB_X8 + CB_L1ST + CB_DL2ST + CB_L1 + CB_DL2 + CB_RED)   // 138128
 // compact variant (no prefetch): x8 | l1s | dl2s | red -- leaves LDS for co-resident rollout
 // kernels when the backward overlaps the next rollout (engine overlap mode)
-#define CB_SMEM_COMPACT (CB_X8 + CB_L1 + CB_DL2 + 4 * 64 * 4)                          // 72912
+#define CB_SMEM_COMPACT (CB_X8 + CB_L1 + CB_DL2 + CB_RED)                              // 73936
 
 // one 16-byte-per-lane global -> LDS DMA wave-instruction: lane l's 16 bytes land at
 // lds_base + 16 l (lds_base wave-uniform), no VGPR destination
@@ -149,9 +151,9 @@ __device__ inline void glds16(const void* g, void* lds_base) {
                                    (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
-// the 4 waves DMA `nbytes` (multiple of 16) from g to LDS dst in 1 KiB wave-instructions
-__device__ inline void glds_copy(const uint8_t* g, uint8_t* dst, int nbytes, int wid, int lane) {
-  for (int c = wid; c * 1024 < nbytes; c += 4) {
+// the nw waves DMA `nbytes` (multiple of 16) from g to LDS dst in 1 KiB wave-instructions
+__device__ inline void glds_copy(const uint8_t* g, uint8_t* dst, int nbytes, int wid, int lane, int nw) {
+  for (int c = wid; c * 1024 < nbytes; c += nw) {
     const int off = c * 1024 + lane * 16;
     if (off < nbytes) glds16(g + off, dst + c * 1024);
   }
@@ -160,8 +162,8 @@ __device__ inline void glds_copy(const uint8_t* g, uint8_t* dst, int nbytes, int
 // workgroup barrier that keeps LDS-DMA loads in flight (retires LDS ops only)
 __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <bool DMA>
-__global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int per_wg,
+template <bool DMA, int NW>
+__global__ void __launch_bounds__(64 * NW) k_conv_bwd(StateAddr sa, int64_t B, int per_wg,
                                                   const float* __restrict__ act_l1,
                                                   const float* __restrict__ dl2,
                                                   const float* __restrict__ W2,
@@ -173,15 +175,19 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
   float* l1s = (float*)(dl2st + (DMA ? CB_DL2ST : 0));
   float* dl2s = (float*)((uint8_t*)l1s + CB_L1);
   float* dl1s = l1s;                                                 // dl1 overwrites l1 in place
-  float* red = (float*)((uint8_t*)dl2s + CB_DL2);                    // [4 waves][64]
+  float* red = (float*)((uint8_t*)dl2s + CB_DL2);                    // [NW waves][64]
+  constexpr int NT = 64 * NW;
+  constexpr int T = 16 / NW;          // (kh,kw) tiles of dW2 and K1 tiles of dW1 per wave
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int i16 = lane & 15, j4 = lane >> 4;
   const int64_t tau0 = sa.tau_ptr ? *sa.tau_ptr : 0;
   const int64_t b0 = (int64_t)blockIdx.x * per_wg;
   const int64_t b1 = min(B, b0 + per_wg);
 
-  // parity class of this wave for dl1: (py, px)
-  const int py = wid >> 1, px = wid & 1;
+  // parity class of this wave for dl1: (py, px); with 8 waves two waves share a class and
+  // split its 7 M-tiles (0-3 / 4-6)
+  const int py = (wid & 3) >> 1, px = wid & 1;
+  const int mt_lo = NW == 8 ? (wid >> 2) * 4 : 0, mt_hi = NW == 8 ? (wid >> 2 ? 7 : 4) : 7;
   // W2 taps for the class: w2c[(dy*2+dx)*8 + nb*4 + c4] = W2[py+2dy][px+2dx][ci=i16][16nb+4j4+c4]
   float w2c[32];
 #pragma unroll
@@ -196,10 +202,10 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
         for (int c4 = 0; c4 < 4; ++c4) w2c[(dy * 2 + dx) * 8 + nb * 4 + c4] = w[c4];
       }
 
-  f32x4 accW2[4][2];
-  f32x4 accW1[4];
+  f32x4 accW2[T][2];
+  f32x4 accW1[T];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < T; ++t) {
     accW2[t][0] = accW2[t][1] = accW1[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
   float db1acc = 0.f, db2acc = 0.f;
@@ -209,9 +215,9 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
   // the padded (bank-spread) layouts at the top of the next sample.
   auto issue = [&](int64_t bb, uint8_t* x8dst) {
 #pragma unroll
-    for (int c = 0; c < HIST; ++c) glds_copy(state_plane(sa, bb, c, tau0), x8dst + c * PLANE, PLANE, wid, lane);
-    glds_copy((const uint8_t*)(act_l1 + bb * C1_P * C1_N), l1st, CB_L1ST, wid, lane);
-    glds_copy((const uint8_t*)(dl2 + bb * FLAT), dl2st, CB_DL2ST, wid, lane);
+    for (int c = 0; c < HIST; ++c) glds_copy(state_plane(sa, bb, c, tau0), x8dst + c * PLANE, PLANE, wid, lane, NW);
+    glds_copy((const uint8_t*)(act_l1 + bb * C1_P * C1_N), l1st, CB_L1ST, wid, lane, NW);
+    glds_copy((const uint8_t*)(dl2 + bb * FLAT), dl2st, CB_DL2ST, wid, lane, NW);
   };
   if (DMA && b0 < b1) issue(b0, x8buf);
 
@@ -220,11 +226,11 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
     if constexpr (DMA) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA for sample b landed
       __syncthreads();                                    // ... and every wave's; sample b-1 done
-      for (int i = tid; i < C1_P * 4; i += 256) {         // l1 [400][16] -> stride 20
+      for (int i = tid; i < C1_P * 4; i += NT) {          // l1 [400][16] -> stride 20
         const int p = i >> 2, q4 = i & 3;
         *(f32x4*)(l1s + p * CB_L1_LD + 4 * q4) = ((const f32x4*)l1st)[i];
       }
-      for (int i = tid; i < C2_Q * 8; i += 256) {         // dl2 [81][32] -> stride 36
+      for (int i = tid; i < C2_Q * 8; i += NT) {          // dl2 [81][32] -> stride 36
         const int q = i >> 3, q4 = i & 7;
         *(f32x4*)(dl2s + q * CB_DL2_LD + 4 * q4) = ((const f32x4*)dl2st)[i];
       }
@@ -233,11 +239,11 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
     } else {
       __syncthreads();                                    // previous sample done with LDS
       stage_state(sa, b, tau0, x8);
-      for (int i = tid; i < C1_P * 4; i += 256) {
+      for (int i = tid; i < C1_P * 4; i += NT) {
         const int p = i >> 2, q4 = i & 3;
         *(f32x4*)(l1s + p * CB_L1_LD + 4 * q4) = *(const f32x4*)(act_l1 + (b * C1_P + p) * C1_N + 4 * q4);
       }
-      for (int i = tid; i < C2_Q * 8; i += 256) {
+      for (int i = tid; i < C2_Q * 8; i += NT) {
         const int q = i >> 3, q4 = i & 7;
         *(f32x4*)(dl2s + q * CB_DL2_LD + 4 * q4) = *(const f32x4*)(dl2 + b * FLAT + q * C2_N + 4 * q4);
       }
@@ -253,8 +259,8 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
       const float bq0 = qv ? dl2s[qc * CB_DL2_LD + i16] : 0.f;
       const float bq1 = qv ? dl2s[qc * CB_DL2_LD + 16 + i16] : 0.f;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int mt = 4 * wid + t;
+      for (int t = 0; t < T; ++t) {
+        const int mt = T * wid + t;
         const int kh = mt >> 2, kw = mt & 3;
         const float av = qv ? l1s[((C2_S * oy + kh) * C1_O + C2_S * ox + kw) * CB_L1_LD + i16] : 0.f;
         accW2[t][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bq0, accW2[t][0], 0, 0, 0);
@@ -265,7 +271,7 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
     lds_barrier();   // every wave done reading l1 in (a): (b) overwrites it with dl1
 
     // ---- (b) dl1 for parity class (py,px): 100 positions in 7 M-tiles of 16 ----
-    for (int mt = 0; mt < 7; ++mt) {
+    for (int mt = mt_lo; mt < mt_hi; ++mt) {
       const int pc = 16 * mt + i16;
       const int pcc = pc < 100 ? pc : 99;
       const int ay = pcc / 10, cx = pcc - ay * 10;
@@ -307,10 +313,10 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
     lds_barrier();   // dl1 complete (the DMA for sample b+1 stays in flight)
 
     // ---- (c) dW1[(kh,kw,cin)][n] += sum_p x[cin][4oy+kh][4ox+kw] * dl1[p][n]  (x unscaled) ----
-    int koff[4];
+    int koff[T];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int k = 16 * (4 * wid + t) + i16;
+    for (int t = 0; t < T; ++t) {
+      const int k = 16 * (T * wid + t) + i16;
       const int s8 = k >> 2, cin = k & 3;
       const int kh = s8 >> 3, kw = s8 & 7;
       koff[t] = cin * PLANE + kh * IMG + kw;
@@ -321,7 +327,7 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
       const int base = (C1_S * oy) * IMG + C1_S * ox;
       const float bv = dl1s[p * CB_L1_LD + i16];
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < T; ++t)
         accW1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)x8[base + koff[t]], bv, accW1[t], 0, 0, 0);
     }
   }
@@ -329,8 +335,8 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
   // ---- write this workgroup's partial slab ----
   float* out = slab + (int64_t)blockIdx.x * CB_SLAB;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int mt = 4 * wid + t;
+  for (int t = 0; t < T; ++t) {
+    const int mt = T * wid + t;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int krow = 16 * mt + 4 * j4 + r;     // dW1 row (kh,kw,cin) / dW2 row (kh,kw,ci)
@@ -339,13 +345,18 @@ __global__ void __launch_bounds__(256) k_conv_bwd(StateAddr sa, int64_t B, int p
       out[CB_OFF_W2 + krow * C2_N + 16 + i16] = accW2[t][1][r];
     }
   }
-  // db1: lanes with equal i16 (4 j4 groups) then the 4 waves
+  // db1: lanes with equal i16 (4 j4 groups) then the waves, in a fixed order
   db1acc += __shfl_xor(db1acc, 16, 64);
   db1acc += __shfl_xor(db1acc, 32, 64);
   __syncthreads();
   if (lane < 16) red[wid * 64 + lane] = db1acc;
   __syncthreads();
-  if (tid < 16) out[CB_OFF_B1 + tid] = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
+  if (tid < 16) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w * 64 + tid];
+    out[CB_OFF_B1 + tid] = v;
+  }
   if (tid < C2_N) out[CB_OFF_B2 + tid] = db2acc;
 }
 
@@ -523,11 +534,21 @@ void a3c_conv_bwd_set_compact(bool v) { t_conv_bwd_compact = v; }
 int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,
                         const float* dl2, float* ws, hipStream_t s) {
   const BwdPlan p = a3c_bwd_plan(L, B);
-  if (a3c_conv_bwd_compact())
-    hipLaunchKernelGGL(k_conv_bwd<false>, dim3((unsigned)p.nwg), dim3(256), CB_SMEM_COMPACT, s, sa, B, p.per_wg, act_l1,
-                       dl2, P + L.off[T_L2W], ws + p.cslab);
+  // sync: the DMA-prefetching kernel at 8 waves (2 per SIMD) owns the GPU; overlap: the compact
+  // 4-wave kernel leaves registers and LDS for the concurrent rollout (measured, tools/ab.sh)
+  static const int env_nw = getenv("A3C_CB_WAVES") ? atoi(getenv("A3C_CB_WAVES")) : 0;
+  const int nw = env_nw ? env_nw : (a3c_conv_bwd_compact() ? 4 : 8);
+  if (a3c_conv_bwd_compact() && nw == 4)
+    hipLaunchKernelGGL((k_conv_bwd<false, 4>), dim3((unsigned)p.nwg), dim3(256), CB_SMEM_COMPACT, s, sa, B, p.per_wg,
+                       act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
+  else if (a3c_conv_bwd_compact())
+    hipLaunchKernelGGL((k_conv_bwd<false, 8>), dim3((unsigned)p.nwg), dim3(512), CB_SMEM_COMPACT, s, sa, B, p.per_wg,
+                       act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
+  else if (nw == 4)
+    hipLaunchKernelGGL((k_conv_bwd<true, 4>), dim3((unsigned)p.nwg), dim3(256), CB_SMEM_DMA, s, sa, B, p.per_wg,
+                       act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
   else
-  hipLaunchKernelGGL(k_conv_bwd<true>, dim3((unsigned)p.nwg), dim3(256), CB_SMEM_DMA, s, sa, B, p.per_wg, act_l1,
+  hipLaunchKernelGGL((k_conv_bwd<true, 8>), dim3((unsigned)p.nwg), dim3(512), CB_SMEM_DMA, s, sa, B, p.per_wg, act_l1,
                      dl2, P + L.off[T_L2W], ws + p.cslab);
   A3C_CHECK(hipGetLastError());
   return 0;
@@ -552,7 +573,10 @@ int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float
 }
 
 void a3c_conv_bwd_set_smem() {
-  (void)hipFuncSetAttribute((const void*)k_conv_bwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_SMEM_DMA);
-  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_SMEM_DMA);
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<true, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_SMEM_DMA);
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            CB_SMEM_COMPACT);
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             CB_SMEM_COMPACT);
 }
