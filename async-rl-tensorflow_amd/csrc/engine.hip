@@ -312,7 +312,15 @@ static OptParams opt_params(const a3c_engine* e) {
 
 // n env steps of every env (forward + action draw + env act fused into the head, then the
 // Environment.screen of the new frames into the ring) and the bootstrap forward.
+static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s);
 static int enqueue_rollout(a3c_engine* e, const Slot& sl, hipStream_t s) {
+  a3c_set_shared_gpu(e->overlap != 0);
+  int rc = enqueue_rollout_impl(e, sl, s);
+  a3c_set_shared_gpu(false);
+  return rc;
+}
+
+static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
   const NetLayout& L = e->L;
   const int E = e->E, n = e->n, zs = L.zs;
@@ -373,10 +381,10 @@ static int enqueue_rollout(a3c_engine* e, const Slot& sl, hipStream_t s) {
 // per-worker clip when gradients are exchanged across GPUs).
 static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s);
 static int enqueue_grad(a3c_engine* e, const Slot& sl, hipStream_t s) {
-  // overlap: the backward shares CUs with the next rollout -> the small-LDS conv backward
-  a3c_conv_bwd_set_compact(e->overlap != 0);
+  // overlap: the backward shares CUs with the next rollout -> small-footprint kernel variants
+  a3c_set_shared_gpu(e->overlap != 0);
   int rc = enqueue_grad_impl(e, sl, s);
-  a3c_conv_bwd_set_compact(false);
+  a3c_set_shared_gpu(false);
   return rc;
 }
 
@@ -583,6 +591,8 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
   const int E = e->E;
   const Slot& sl = e->slot[0];
   if (e->rs) A3C_CHECK(hipStreamSynchronize(e->rs));
+  a3c_set_shared_gpu(e->overlap != 0);      // time the variants the engine runs
+  struct ResetShared { ~ResetShared() { a3c_set_shared_gpu(false); } } reset_shared;
   if (kernel == A3C_KER_CONV12_FWD || kernel == A3C_KER_FC_FWD) {
     int rc0 = a3c_prep_fwd_launch(L, e->params, sl.prep, s);
     if (rc0) return rc0;
@@ -612,8 +622,6 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
       }
       case A3C_KER_CONV_BWD: {
         const BwdPlan p = a3c_bwd_plan(L, e->nE);
-        a3c_conv_bwd_set_compact(e->overlap != 0);
-        struct Reset { ~Reset() { a3c_conv_bwd_set_compact(false); } } reset_compact;
         return a3c_conv_bwd_launch(L, e->params, ring_addr(e, 0, e->counters), e->nE, sl.act_l1, e->ws + p.dl2, e->ws, s);
       }
       default:

@@ -113,6 +113,9 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
                        int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
                        hipStream_t s);
 int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s);
+// true while enqueuing work that runs concurrently with another stream (engine overlap mode)
+bool a3c_shared_gpu();
+void a3c_set_shared_gpu(bool v);
 
 // stage the HIST u8 planes of state b into LDS (HIST x 441 uint4)
 __device__ inline void stage_state(const StateAddr& sa, int64_t b, int64_t tau0, uint8_t* x8) {

@@ -524,12 +524,13 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   return 0;
 }
 
-// variant choice: the compact kernel when the backward shares the GPU with a concurrent rollout
-// (engine overlap mode), the LDS-DMA prefetching one otherwise.  Thread-local switch set by the
-// engine around its enqueue calls (captured into the graphs).
-static thread_local bool t_conv_bwd_compact = false;
-bool a3c_conv_bwd_compact() { return t_conv_bwd_compact; }
-void a3c_conv_bwd_set_compact(bool v) { t_conv_bwd_compact = v; }
+// Kernel variant choice: a3c_shared_gpu() is true while the engine enqueues work that will run
+// concurrently with another stream (overlap mode) -- then the kernels take their smaller-footprint
+// variants so both streams' workgroups co-reside on the CUs.  Thread-local switch set by the engine
+// around its enqueue calls (captured into the graphs).
+static thread_local bool t_shared_gpu = false;
+bool a3c_shared_gpu() { return t_shared_gpu; }
+void a3c_set_shared_gpu(bool v) { t_shared_gpu = v; }
 
 int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,
                         const float* dl2, float* ws, hipStream_t s) {
@@ -537,11 +538,11 @@ int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa,
   // sync: the DMA-prefetching kernel at 8 waves (2 per SIMD) owns the GPU; overlap: the compact
   // 4-wave kernel leaves registers and LDS for the concurrent rollout (measured, tools/ab.sh)
   static const int env_nw = getenv("A3C_CB_WAVES") ? atoi(getenv("A3C_CB_WAVES")) : 0;
-  const int nw = env_nw ? env_nw : (a3c_conv_bwd_compact() ? 4 : 8);
-  if (a3c_conv_bwd_compact() && nw == 4)
+  const int nw = env_nw ? env_nw : (a3c_shared_gpu() ? 4 : 8);
+  if (a3c_shared_gpu() && nw == 4)
     hipLaunchKernelGGL((k_conv_bwd<false, 4>), dim3((unsigned)p.nwg), dim3(256), CB_SMEM_COMPACT, s, sa, B, p.per_wg,
                        act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
-  else if (a3c_conv_bwd_compact())
+  else if (a3c_shared_gpu())
     hipLaunchKernelGGL((k_conv_bwd<false, 8>), dim3((unsigned)p.nwg), dim3(512), CB_SMEM_COMPACT, s, sa, B, p.per_wg,
                        act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
   else if (nw == 4)

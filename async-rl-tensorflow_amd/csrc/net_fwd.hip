@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, 
 // engine rollout step tail, one workgroup per env: head + action draw + env act (wave 0), then
 // the whole workgroup computes Environment.screen (environment.py:49-53, bit-exact) of the
 // post-act frame straight from the HBM pool into the env's frame-ring slot
-#define HS_THREADS 512
+template <int HS_THREADS>
 __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restrict__ h3,
                                                             const float* __restrict__ Wp,
                                                             const float* __restrict__ bp,
@@ -362,8 +362,7 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
   const float* Wv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VW] : nullptr;
   const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
   if (sel.mode >= 0 && sel.env_on && sel.ring)
-    hipLaunchKernelGGL(k_head_screen, dim3((unsigned)B), dim3(HS_THREADS), SCREEN_FRAME_SMEM, s, act_l3,
-                       P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel);
+    return a3c_head_screen_launch(L, P, act_l3, B, z, sel, s);
   else
     hipLaunchKernelGGL(k_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, act_l3, B,
                        P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel);
@@ -376,8 +375,15 @@ int a3c_head_screen_launch(const NetLayout& L, const float* P, const float* act_
                            const HeadSelect& sel, hipStream_t s) {
   const float* Wv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VW] : nullptr;
   const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
-  hipLaunchKernelGGL(k_head_screen, dim3((unsigned)B), dim3(HS_THREADS), SCREEN_FRAME_SMEM, s, act_l3,
-                     P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel);
+  // 1024 threads when the step owns the GPU; 512 leave room for the concurrent backward
+  static const int env_t = getenv("A3C_HS_THREADS") ? atoi(getenv("A3C_HS_THREADS")) : 0;
+  const int nt = env_t ? env_t : (a3c_shared_gpu() ? 512 : 1024);
+  if (nt == 1024)
+    hipLaunchKernelGGL(k_head_screen<1024>, dim3((unsigned)B), dim3(1024), SCREEN_FRAME_SMEM, s, act_l3,
+                       P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel);
+  else
+    hipLaunchKernelGGL(k_head_screen<512>, dim3((unsigned)B), dim3(512), SCREEN_FRAME_SMEM, s, act_l3,
+                       P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
@@ -406,7 +412,10 @@ int a3c_select_launch(const float* z, int64_t B, int zs, int A, const HeadSelect
 void a3c_conv12_set_smem() {
   (void)hipFuncSetAttribute((const void*)k_conv12_fwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize, CONV12_SMEM);
   (void)hipFuncSetAttribute((const void*)k_conv12_fwd<false>, hipFuncAttributeMaxDynamicSharedMemorySize, CONV12_SMEM);
-  (void)hipFuncSetAttribute((const void*)k_head_screen, hipFuncAttributeMaxDynamicSharedMemorySize, SCREEN_FRAME_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_head_screen<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SCREEN_FRAME_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_head_screen<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SCREEN_FRAME_SMEM);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -534,7 +543,8 @@ __global__ void __launch_bounds__(256) k_fc_fwd_rows(const float* __restrict__ A
 int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s,
                       const float* Wrows) {
   if (M <= 0) return 0;
-  static const int nw = getenv("A3C_FC_WAVES") ? atoi(getenv("A3C_FC_WAVES")) : 4;
+  static const int env_nw = getenv("A3C_FC_WAVES") ? atoi(getenv("A3C_FC_WAVES")) : -1;
+  const int nw = env_nw >= 0 ? env_nw : (a3c_shared_gpu() ? 4 : 8);
   if (nw == 0 && Wrows)
     hipLaunchKernelGGL(k_fc_fwd_rows, dim3(FC / 16, (unsigned)((M + 15) / 16)), dim3(256), 0, s, A, Wrows, bias, C,
                        (int)M);

@@ -172,7 +172,9 @@ def _same_act_grads(slot, planes, P, algo, A, n, E, tgt):
 
 def test_overlap_with_zero_lr_equals_sync():
     """With learning_rate 0 staleness is invisible: the pipelined engine must reproduce the
-    synchronous engine's rollouts, losses and gradients bit for bit, one call later."""
+    synchronous engine's rollouts exactly (actions, rewards) one call later, and its returns,
+    losses and gradients to fp32 summation order (the two modes run different-footprint kernel
+    variants, see a3c_shared_gpu)."""
     s, _, _ = build('a3c', 6, 16, 5, 0, seed=31, learning_rate=0.0)
     o, _, _ = build('a3c', 6, 16, 5, 0, seed=31, learning_rate=0.0, overlap=True)
     assert o.ring_slots == 2 * 5 + 4 and s.ring_slots == 5 + 4
@@ -187,10 +189,10 @@ def test_overlap_with_zero_lr_equals_sync():
         prev = o.slot((k - 1) & 1)
         assert torch.equal(prev['actions'], s.actions), k
         assert torch.equal(prev['rewards'], s.rewards), k
-        assert torch.equal(prev['returns'], s.returns), k
-        assert torch.equal(o.grads, s.grads), k
-        assert torch.equal(o.loss, s.loss), k
-        assert torch.equal(o.params, s.params), k
+        torch.testing.assert_close(prev['returns'], s.returns, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(o.loss, s.loss, rtol=1e-5, atol=1e-5)
+        assert rel_l2(o.grads.cpu().numpy(), s.grads.cpu().numpy()) < 1e-5, k
+        assert torch.equal(o.params, s.params), k          # lr = 0: parameters never move
     assert int(o.counters[0].item()) == int(s.counters[0].item()) + 5     # one rollout ahead
     assert int(o.counters[1].item()) == int(s.counters[1].item())
 
