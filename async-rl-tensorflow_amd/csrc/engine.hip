@@ -73,6 +73,8 @@ struct a3c_engine {
   bool captured[5];
   // overlap pipeline
   hipStream_t rs;          // rollout stream
+  hipStream_t gs;          // backward side stream (weight-gradient GEMMs beside the conv backward)
+  hipEvent_t ev_gfork, ev_gjoin;
   hipEvent_t ev_start, ev_roll[2];
   int64_t iter;            // rollouts issued since reset
   bool grad_ready;         // the last rollout_grad call computed a gradient
@@ -133,6 +135,9 @@ extern "C" int a3c_engine_destroy(a3c_engine* e) {
       (void)hipGraphDestroy(e->graph[i]);
     }
   if (e->rs) (void)hipStreamDestroy(e->rs);
+  if (e->gs) (void)hipStreamDestroy(e->gs);
+  if (e->ev_gfork) (void)hipEventDestroy(e->ev_gfork);
+  if (e->ev_gjoin) (void)hipEventDestroy(e->ev_gjoin);
   if (e->ev_start) (void)hipEventDestroy(e->ev_start);
   for (int k = 0; k < 2; ++k) {
     if (e->ev_roll[k]) (void)hipEventDestroy(e->ev_roll[k]);
@@ -223,6 +228,15 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   if (a3c_make_tab(L.nt, L.off, L.size, L.total, &e->tt)) {
     a3c_engine_destroy(e);
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "tensor table");
+  }
+  {
+    bool ok = hipStreamCreateWithFlags(&e->gs, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&e->ev_gfork, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&e->ev_gjoin, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+      a3c_engine_destroy(e);
+      return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "stream/event creation failed");
+    }
   }
   if (e->overlap) {
     // the rollout is a serial chain of small kernels: give its stream the higher priority so
@@ -412,8 +426,11 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
     ra.rewards = sl.rewards; ra.terms = sl.terms; ra.boot = sl.z + e->nE * zs + L.A; ra.boot_stride = zs;
     ra.n = n; ra.E = E; ra.gamma = c.gamma; ra.R_out = sl.R_buf;
   }
+  static const bool fork_env = getenv("A3C_BWD_FORK") ? atoi(getenv("A3C_BWD_FORK")) != 0 : false;  // measured slower
+  const bool fork = fork_env;
   rc = a3c_backward_launch(L, sl.P, ring_addr(e, 0, sl.tau), e->nE, sl.act_l1, sl.act_l2, sl.act_l3, sl.z,
-                           sl.actions, sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra);
+                           sl.actions, sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra,
+                           fork ? e->gs : nullptr, fork ? e->ev_gfork : nullptr, fork ? e->ev_gjoin : nullptr);
   if (rc) return rc;
   // per-tensor squared norms (+ lr / target-sync schedule from the device step counter)
   OptParams op = opt_params(e);

@@ -45,7 +45,8 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
                         const float* act_l1, const float* act_l2, const float* act_l3,
                         const float* z, const int32_t* actions, const float* target, float beta,
                         int literal, float* grads, float* loss_out, float* ws, hipStream_t s,
-                        const ReturnsArgs* ra = nullptr);
+                        const ReturnsArgs* ra = nullptr,
+                        hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr);
 int a3c_returns_launch(const float* rewards, const uint8_t* terms, const float* boot, int64_t boot_stride,
                        int n, int64_t E, double gamma, float* R, hipStream_t s);
 int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float* qn, int64_t B, int A,

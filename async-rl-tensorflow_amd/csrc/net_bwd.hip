@@ -444,7 +444,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
                         const float* act_l1, const float* act_l2, const float* act_l3,
                         const float* z, const int32_t* actions, const float* target, float beta,
                         int literal, float* grads, float* loss_out, float* ws, hipStream_t s,
-                        const ReturnsArgs* ra_in) {
+                        const ReturnsArgs* ra_in, hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join) {
   ReturnsArgs ra = {};
   if (ra_in) ra = *ra_in;
   if (B <= 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "B must be > 0");
@@ -461,6 +461,15 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
                      literal, 1.0f / (float)B, B, dz, dh3, terms, ra);
   A3C_CHECK(hipGetLastError());
 
+  // The weight-gradient GEMMs (head, fc) only need dz / dl3 from k_head_bwd: with a side stream
+  // they run concurrently with the dl2 GEMM + conv backward (graph branches), joined before the
+  // slab reductions.
+  const bool fork = side && ev_fork && ev_join;
+  hipStream_t ws_s = fork ? side : s;
+  if (fork) {
+    A3C_CHECK(hipEventRecord(ev_fork, s));
+    A3C_CHECK(hipStreamWaitEvent(side, ev_fork, 0));
+  }
   // head weights: dWh[256][zs] = l3^T dz ; dbh = colsum(dz)
   GemmArgs g = {};
   g.A = act_l3; g.lda = FC;          // A(m=feature, k=b) = l3[b][m]  (m contiguous)
@@ -468,7 +477,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   g.C = ws + p.hgrad; g.ldc = L.zs;
   g.M = FC; g.N = L.zs; g.K = (int)B;
   g.epi = EPI_STORE; g.slab = ws + p.hslab; g.nsplit = p.head_split; g.colsum = ws + p.hcol;
-  int rc = a3c_gemm(false, true, g, s);
+  int rc = a3c_gemm(false, true, g, ws_s);
   if (rc) return rc;
 
   // fc weights: dW[2592][256] = l2^T dl3 -> grads directly ; db = colsum(dl3)
@@ -478,8 +487,10 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   g.C = grads + L.off[T_FCW]; g.ldc = FC;
   g.M = FLAT; g.N = FC; g.K = (int)B;
   g.epi = EPI_STORE; g.slab = ws + p.fcslab; g.nsplit = p.fc_split; g.colsum = ws + p.fccol;
-  rc = a3c_gemm(false, true, g, s);
+  rc = a3c_gemm(false, true, g, ws_s);
   if (rc) return rc;
+
+  if (fork) A3C_CHECK(hipEventRecord(ev_join, side));
 
   // dl2[B][2592] = (dl3 W^T) * (l2 > 0)
   g = GemmArgs{};
@@ -502,6 +513,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     q.src = src; q.split_stride = stride; q.nsplit = nsplit; q.rows = rows; q.src_ld = src_ld;
     q.col0 = col0; q.ncols = ncols; q.dst_off = dst_off; q.dst_ld = dst_ld; q.scale = scale;
   };
+  if (fork) A3C_CHECK(hipStreamWaitEvent(s, ev_join, 0));
   // conv slabs: nwg partials -> p.groups partials (pass 1), folded by k_finalize (pass 2)
   const int per = (p.nwg + p.groups - 1) / p.groups;
   hipLaunchKernelGGL(k_slab_group, dim3((CB_SLAB + 255) / 256, p.groups), dim3(256), 0, s, ws + p.cslab, p.nwg, per,
