@@ -53,6 +53,9 @@ def parse():
                          'sharded IPC parameter server, no collective (BASELINE config 4)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
+                    help='process group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the '
+                         'multi-rank path with several ranks on one GPU)')
     ap.add_argument('--no-kernel-timing', action='store_true')
     return ap.parse_args()
 
@@ -92,9 +95,13 @@ def main():
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, args.game, args.algo)    # before any HIP initialisation
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local % max(ndev, 1))
     if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group('gloo')
 
     from src import _lib
     from src.engine import Engine
