@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(64 * NW) k_conv_bwd(StateAddr sa, int64_t B, i
       const int pc = 16 * mt + i16;
       const int pcc = pc < 100 ? pc : 99;
       const int ay = pcc / 10, cx = pcc - ay * 10;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accb = {0.f, 0.f, 0.f, 0.f};   // two chains (nb)
 #pragma unroll
       for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
@@ -287,11 +287,13 @@ __global__ void __launch_bounds__(64 * NW) k_conv_bwd(StateAddr sa, int64_t B, i
           for (int nb = 0; nb < 2; ++nb) {
             f32x4 a = *(const f32x4*)(dl2s + qq * CB_DL2_LD + 16 * nb + 4 * j4);
             if (!v) a = (f32x4){0.f, 0.f, 0.f, 0.f};
+            f32x4& c = nb ? accb : acc;
 #pragma unroll
             for (int c4 = 0; c4 < 4; ++c4)
-              acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c4], w2c[(dy * 2 + dx) * 8 + nb * 4 + c4], acc, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c4], w2c[(dy * 2 + dx) * 8 + nb * 4 + c4], c, 0, 0, 0);
           }
         }
+      acc += accb;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int pr = 16 * mt + 4 * j4 + r;

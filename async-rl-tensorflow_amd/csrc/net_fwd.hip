@@ -128,16 +128,18 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
     const int p = 16 * m + i16;
     const int oy = p / C1_O, ox = p - oy * C1_O;
     const uint16_t* row = xb + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;    // cin = j4
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accb = {0.f, 0.f, 0.f, 0.f};   // two chains by kh parity
 #pragma unroll
     for (int kh = 0; kh < C1_K; ++kh) {
       const uint2* q = (const uint2*)(row + kh * IMG);                        // 8-byte aligned
       const uint2 lo = q[0], hi = q[1];
       const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][0], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][1], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][2], acc, 0, 0, 0);
+      f32x4& c = (kh & 1) ? accb : acc;
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][2], c, 0, 0, 0);
     }
+    acc += accb;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int pos = 16 * m + 4 * j4 + r;
@@ -167,9 +169,9 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
     int oy = q / C2_O, ox = q - oy * C2_O;
     pos0[mi] = (C2_S * oy) * C1_O + C2_S * ox;
   }
-  f32x4 acc2[2];
+  f32x4 acc2[2], acc2b[2];                         // two chains per tile (kw parity)
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi) acc2[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int mi = 0; mi < 2; ++mi) acc2[mi] = acc2b[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int kh = 0; kh < C2_K; ++kh)
 #pragma unroll
@@ -178,10 +180,13 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
       for (int mi = 0; mi < 2; ++mi) {
         if (mi >= nm) break;
         f32x4 a = *(const f32x4*)(l1s + (pos0[mi] + kh * C1_O + kw) * L1S_LD + 4 * j4);
+        f32x4& c = (kw & 1) ? acc2b[mi] : acc2[mi];
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4)
-          acc2[mi] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c4], w2r[(kh * 4 + kw) * 4 + c4], acc2[mi], 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c4], w2r[(kh * 4 + kw) * 4 + c4], c, 0, 0, 0);
       }
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) acc2[mi] += acc2b[mi];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi) {
     if (mi >= nm) break;
@@ -441,7 +446,7 @@ __global__ void __launch_bounds__(64 * NW) k_fc_fwd(const float* __restrict__ A,
   constexpr int D = 8;
   const float* a = A + (int64_t)m * FLAT + 4 * j4;
   const f32x4* b = (const f32x4*)Wp + (int64_t)ct * FC_CH * 64 + lane;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   f32x4 ra[D], rb[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
@@ -452,9 +457,11 @@ __global__ void __launch_bounds__(64 * NW) k_fc_fwd(const float* __restrict__ A,
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       if (c + d < c1) {
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4)
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][c4], rb[d][c4], acc, 0, 0, 0);
+        // two independent accumulation chains (MFMA dependent latency > issue interval)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][0], rb[d][0], acc, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][1], rb[d][1], acc1, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][2], rb[d][2], acc, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][3], rb[d][3], acc1, 0, 0, 0);
         const int cn = c + d + D;                 // refill this slot with chunk cn
         if (cn < c1) {
           ra[d] = *(const f32x4*)(a + 16 * cn);
@@ -463,6 +470,7 @@ __global__ void __launch_bounds__(64 * NW) k_fc_fwd(const float* __restrict__ A,
       }
     }
   }
+  acc += acc1;
   if (wid > 0) red[wid - 1][lane] = acc;
   __syncthreads();
   if (wid == 0) {
