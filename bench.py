@@ -110,6 +110,8 @@ def main():
 
     A, lives = GAMES[args.game]
     E, n = args.envs, args.n_step
+    if args.algo == 'q' and args.update == 'overlap':
+        args.update = 'sync'              # the stale-1 pipeline is an A3C (policy-gradient) mode
     eng = Engine(num_envs=E, n_step=n, action_size=A, algo=args.algo, start_lives=lives, num_frames=args.frames,
                  seed=123, env_id_base=rank * E, world_size=world, use_graph=not args.no_graph,
                  overlap=args.update == 'overlap')
