@@ -420,7 +420,13 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   BwdPlan p;
   int64_t o = 0;
   auto take = [&](int64_t floats) { int64_t r = o; o += (floats + 63) & ~(int64_t)63; return r; };
-  p.nwg = (int)(B < 256 ? B : 256);
+  // conv-backward workgroups: one per CU when the backward owns the GPU; in overlap mode ~7/8 of
+  // the CUs (224 -> 6 samples per workgroup at B = 1280) so the concurrent rollout keeps some
+  // CUs to itself (measured: 3.22M vs 3.15M env-steps/s at 256).  The workspace is sized for
+  // the larger count (a3c_bwd_plan with shared = false).
+  static const int env_nwg = getenv("A3C_CB_NWG") ? atoi(getenv("A3C_CB_NWG")) : 0;
+  const int nwg_max = env_nwg ? env_nwg : (a3c_shared_gpu() ? 224 : 256);
+  p.nwg = (int)(B < nwg_max ? B : nwg_max);
   if (p.nwg < 1) p.nwg = 1;
   p.per_wg = (int)((B + p.nwg - 1) / p.nwg);
   p.nwg = (int)((B + p.per_wg - 1) / p.per_wg);
