@@ -100,10 +100,43 @@ __device__ inline uint4 lum16(const uint4 a, const uint4 b, const uint4 c) {
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// Horizontal pass of one gray row for output columns [X0, X0 + NX): the row window is read
+// as 6 dwords x 4 from LDS once and every tap is a compile-time byte of it (kH is constexpr);
+// the outputs are packed 4 per dword.  Half 0 = columns 0..43 (bytes 0..95), half 1 = 44..83
+// (bytes 80..175; taps past a row's count have weight 0, so bytes past the row are harmless).
+template <int H>
+__device__ inline void hpass_row(const uint8_t* __restrict__ grow, uint8_t* __restrict__ trow) {
+  constexpr int X0 = H ? 44 : 0, NX = H ? 40 : 44, BASE = H ? 80 : 0;
+  uint32_t w[24];
+  const uint4* src = (const uint4*)(grow + BASE);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const uint4 v = src[i];
+    w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+  }
+#pragma unroll
+  for (int q = 0; q < NX / 4; ++q) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int xx = X0 + 4 * q + u;
+      int acc = 1 << (A3C_PRECISION_BITS - 1);
+#pragma unroll
+      for (int x = 0; x < KH; ++x) {
+        const int bi = kH.xmin[xx] + x - BASE;
+        acc += (int)((w[bi >> 2] >> (8 * (bi & 3))) & 255u) * kH.k[xx][x];
+      }
+      packed |= (uint32_t)a3c_clip8(acc) << (8 * u);
+    }
+    *(uint32_t*)(trow + X0 + 4 * q) = packed;
+  }
+}
+
 // Whole-frame Environment.screen by one workgroup of NT threads (gray 210x160 and the
 // horizontal-pass 210x84 in LDS, SCREEN_FRAME_SMEM bytes); the RGB frame streams from HBM
-// straight into registers (all of a thread's loads issued before any use).
-#define SCREEN_FRAME_SMEM (210 * 160 + 210 * 84)
+// straight into registers (all of a thread's loads issued before any use).  The resampling
+// passes read LDS a dword (H: 24 per half row) or a column quad (V) at a time.
+#define SCREEN_FRAME_SMEM (210 * 160 + 210 * 84 + 96)
 template <int NT>
 __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __restrict__ out, uint8_t* smem) {
   uint8_t* gray = smem;
@@ -125,35 +158,35 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
     if (u < NUNIT) *(uint4*)(gray + 16 * u) = lum16(r[j][0], r[j][1], r[j][2]);
   }
   __syncthreads();
-  constexpr int RP = NT / OW;                          // row phases
-  const int xx = tid % OW, rp = tid / OW;
-  if (rp < RP) {
-    const int x0 = cH.xmin[xx];
-    int kk[KH], off[KH];
-#pragma unroll
-    for (int x = 0; x < KH; ++x) {
-      kk[x] = cH.k[xx][x];
-      off[x] = min(x0 + x, IW - 1);
-    }
-    for (int rr = rp; rr < IH; rr += RP) {
-      const uint8_t* s = gray + rr * IW;
-      int acc = 1 << (A3C_PRECISION_BITS - 1);
-#pragma unroll
-      for (int x = 0; x < KH; ++x) acc += (int)s[off[x]] * kk[x];
-      tmp[rr * OW + xx] = a3c_clip8(acc);
-    }
+  // horizontal: items (row, half), 420 of them
+  for (int it = tid; it < 2 * IH; it += NT) {
+    const int rr = it >> 1;
+    if (it & 1) hpass_row<1>(gray + rr * IW, tmp + rr * OW);
+    else hpass_row<0>(gray + rr * IW, tmp + rr * OW);
   }
   __syncthreads();
-  if (rp < RP) {
-    for (int yy = rp; yy < OH; yy += RP) {
+  // vertical: items (column quad cq, band of 7 output rows), 21 x 12
+  for (int it = tid; it < (OW / 4) * (OH / 7); it += NT) {
+    const int cq = it % (OW / 4), band = it / (OW / 4);
+#pragma unroll
+    for (int yy7 = 0; yy7 < 7; ++yy7) {
+      const int yy = band * 7 + yy7;
       const int b0 = cV.xmin[yy];
-      int acc = 1 << (A3C_PRECISION_BITS - 1);
+      int acc[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = 1 << (A3C_PRECISION_BITS - 1);
 #pragma unroll
       for (int y = 0; y < KV; ++y) {
         const int ry = min(b0 + y, IH - 1);
-        acc += (int)tmp[ry * OW + xx] * cV.k[yy][y];
+        const uint32_t q = *(const uint32_t*)(tmp + ry * OW + 4 * cq);
+        const int k = cV.k[yy][y];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] += (int)((q >> (8 * c)) & 255u) * k;
       }
-      out[yy * OW + xx] = a3c_clip8(acc);
+      uint32_t packed = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) packed |= (uint32_t)a3c_clip8(acc[c]) << (8 * c);
+      *(uint32_t*)(out + yy * OW + 4 * cq) = packed;
     }
   }
 }

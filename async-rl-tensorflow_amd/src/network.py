@@ -41,7 +41,7 @@ class Network(object):
                action_size, activation_fn=ops.relu,
                initializer=ops.truncated_normal_initializer(0, 0.02),
                gamma=0.01, beta=0.0, global_network=None, global_optim=None, DQN_type='',
-               literal_adv=False, device='cuda'):
+               literal_adv=False, device='cuda', seed=None):
     self.sess = sess
     if data_format not in ('NHWC', 'NCHW'):
       raise ValueError("unknown data_format : %s" % data_format)       # network.py:21
@@ -78,10 +78,13 @@ class Network(object):
         off = _align(off + n)
       total = off
     self.flat = torch.zeros(total, dtype=torch.float32, device=device)
+    if seed is not None and initializer is Network.__init__.__defaults__[1]:
+      initializer = ops.truncated_normal_initializer(0, 0.02, seed=seed)
+    lin_init = ops.random_normal_initializer(stddev=0.02, seed=None if seed is None else seed + 1)
     for (name, shp), o, n in zip(self.names_shapes, self.offsets, self.sizes):
       if name.endswith('_b'):
         continue
-      init = initializer if len(shp) == 4 else ops.random_normal_initializer(stddev=0.02)   # ops.py:37
+      init = initializer if len(shp) == 4 else lin_init   # ops.py:37
       self.flat[o:o + n] = torch.as_tensor(init(list(shp))).reshape(-1).to(device)
     self.w = {name: self.flat[o:o + n].view(shp)
               for (name, shp), o, n in zip(self.names_shapes, self.offsets, self.sizes)}
