@@ -80,7 +80,7 @@ int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipSt
 // of 16 positions x K = 256 (8 steps of (kh; cin x kw 0..7)) on v_mfma_f32_16x16x32_bf16 with the
 // three weight terms; conv1 + relu to LDS (and HBM when the backward needs it); conv2 (4x4/2,
 // 16->32, K = 256) in fp32 MFMA from LDS, 12 (M-tile, N-tile) pairs over the 8 waves.
-template <bool SAVE_L1>
+template <bool SAVE_L1, bool EW>
 __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
                                                     const uint16_t* __restrict__ w1s,
                                                     const float* __restrict__ b1,
@@ -96,10 +96,12 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
   const int i16 = lane & 15, j4 = lane >> 4;
   const int64_t tau0 = sa.tau_ptr ? *sa.tau_ptr : 0;
 
-  // stage: u8 planes -> bf16 planes (integers 0..255 are exact in bf16)
-  for (int i = threadIdx.x; i < HIST * (PLANE / 16); i += 512) {
+  // stage: u8 planes -> bf16 planes (integers 0..255 are exact in bf16).  EW: all of a thread's
+  // loads issued before the first conversion; otherwise a load-convert loop (fewer live VGPRs)
+  constexpr int NCH = HIST * (PLANE / 16);             // 1764 chunks of 16 pixels
+  constexpr int PER = (NCH + 511) / 512;               // 4
+  auto stage_chunk = [&](int i, const uint4 v) {
     const int c = i / (PLANE / 16), j = i - c * (PLANE / 16);
-    const uint4 v = ((const uint4*)state_plane(sa, b, c, tau0))[j];
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint32_t o[8];
 #pragma unroll
@@ -112,6 +114,36 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
     uint4* dst = (uint4*)(xb + c * PLANE + 16 * j);
     dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
     dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+  };
+  auto chunk_src = [&](int i) -> uint4 {
+    const int c = i / (PLANE / 16), j = i - c * (PLANE / 16);
+    return ((const uint4*)state_plane(sa, b, c, tau0))[j];
+  };
+  uint4 sv[PER];
+  if (EW) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) sv[k] = chunk_src(min((int)threadIdx.x + 512 * k, NCH - 1));
+  } else {
+    for (int i = threadIdx.x; i < NCH; i += 512) stage_chunk(i, chunk_src(i));
+  }
+  // conv2 weights for this wave's N tile (W2[kh][kw][4*j4 + c4][16*nt + i16]).  EW: issued here,
+  // their latency hidden behind the staging and conv1 (+64 VGPRs live across conv1); otherwise
+  // loaded after conv1 (the small-footprint variant for overlap mode)
+  const int nt = wid & 1, grp = wid >> 1;          // M-tiles grp and grp + 4 (when < 6)
+  float w2r[64];
+  if (EW) {
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) w2r[kk * 4 + c4] = W2[(kk * C1_N + 4 * j4 + c4) * C2_N + 16 * nt + i16];
+  }
+  const float bias2 = b2[16 * nt + i16];
+  if (EW) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = threadIdx.x + 512 * k;
+      if (i < NCH) stage_chunk(i, sv[k]);
+    }
   }
 
   // conv1 weight fragments (3 bf16 terms per K step)
@@ -149,14 +181,12 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
     }
   }
 
-  // conv2 weights for this wave's N tile: W2[kh][kw][4*j4 + c4][16*nt + i16]
-  const int nt = wid & 1, grp = wid >> 1;          // M-tiles grp and grp + 4 (when < 6)
-  float w2r[64];
+  if (!EW) {
 #pragma unroll
-  for (int kk = 0; kk < 16; ++kk)
+    for (int kk = 0; kk < 16; ++kk)
 #pragma unroll
-    for (int c4 = 0; c4 < 4; ++c4) w2r[kk * 4 + c4] = W2[(kk * C1_N + 4 * j4 + c4) * C2_N + 16 * nt + i16];
-  const float bias2 = b2[16 * nt + i16];
+      for (int c4 = 0; c4 < 4; ++c4) w2r[kk * 4 + c4] = W2[(kk * C1_N + 4 * j4 + c4) * C2_N + 16 * nt + i16];
+  }
   __syncthreads();
 
   // ---- conv2: 6 M-tiles (81 rows padded to 96) x 2 N-tiles, K = 16 (kh,kw) x 16 cin ----
@@ -397,12 +427,17 @@ int a3c_conv12_launch(const NetLayout& L, const float* P, const uint8_t* prep, c
                       float* act_l1, float* act_l2, hipStream_t s) {
   if (!prep) return a3c_set_error(A3C_ERR_INVALID, "a3c_conv12_launch", "prepared forward weights missing");
   const uint16_t* w1s = (const uint16_t*)prep;
-  if (act_l1)
-    hipLaunchKernelGGL((k_conv12_fwd<true>), dim3((unsigned)B), dim3(512), CONV12_SMEM, s, sa, B, w1s,
-                       P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2);
+  const bool ew = !a3c_shared_gpu();
+#define CONV12_ARGS sa, B, w1s, P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2
+  if (act_l1 && ew)
+    hipLaunchKernelGGL((k_conv12_fwd<true, true>), dim3((unsigned)B), dim3(512), CONV12_SMEM, s, CONV12_ARGS);
+  else if (act_l1)
+    hipLaunchKernelGGL((k_conv12_fwd<true, false>), dim3((unsigned)B), dim3(512), CONV12_SMEM, s, CONV12_ARGS);
+  else if (ew)
+    hipLaunchKernelGGL((k_conv12_fwd<false, true>), dim3((unsigned)B), dim3(512), CONV12_SMEM, s, CONV12_ARGS);
   else
-    hipLaunchKernelGGL((k_conv12_fwd<false>), dim3((unsigned)B), dim3(512), CONV12_SMEM, s, sa, B, w1s,
-                       P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2);
+    hipLaunchKernelGGL((k_conv12_fwd<false, false>), dim3((unsigned)B), dim3(512), CONV12_SMEM, s, CONV12_ARGS);
+#undef CONV12_ARGS
   A3C_CHECK(hipGetLastError());
   return 0;
 }
@@ -415,8 +450,14 @@ int a3c_select_launch(const float* z, int64_t B, int zs, int A, const HeadSelect
 }
 
 void a3c_conv12_set_smem() {
-  (void)hipFuncSetAttribute((const void*)k_conv12_fwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize, CONV12_SMEM);
-  (void)hipFuncSetAttribute((const void*)k_conv12_fwd<false>, hipFuncAttributeMaxDynamicSharedMemorySize, CONV12_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_conv12_fwd<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            CONV12_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_conv12_fwd<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            CONV12_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_conv12_fwd<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            CONV12_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_conv12_fwd<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            CONV12_SMEM);
   (void)hipFuncSetAttribute((const void*)k_head_screen<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             SCREEN_FRAME_SMEM);
   (void)hipFuncSetAttribute((const void*)k_head_screen<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
