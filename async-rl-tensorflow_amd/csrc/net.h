@@ -3,6 +3,13 @@
 #include "a3c_common.h"
 #include "../../include/a3c_hip.h"
 
+// round-to-nearest-even bf16 bits of a finite float
+__device__ inline uint32_t bf16_rn_bits(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
 // fixed trunk geometry: 84x84x4 -> conv 8x8/4 16 -> conv 4x4/2 32 -> fc 256
 #define IMG 84
 #define PLANE (IMG * IMG)      // 7056 bytes per u8 frame plane

@@ -10,8 +10,11 @@
 //  k_conv_bwd    one workgroup per group of samples, three MFMA phases on LDS-resident tiles:
 //                dW2 += patches(l1)^T dl2, dl1 = col2im(dl2 W2^T) * (l1 > 0) computed per
 //                stride-2 parity class (4 waves = 4 classes, K = 2x2 taps x 32), and
-//                dW1 += patches(x/255)^T dl1 (conv1 gets weight grads only).  Per-workgroup
-//                partial slabs, reduced deterministically by k_finalize.
+//                dW1 += patches(x/255)^T dl1 (conv1 gets weight grads only) on the bf16
+//                matrix cores: u8 pixels are exact in bf16 and dl1 is split into three bf16
+//                terms, so every product is exact in the fp32 accumulator (5x fewer MFMA
+//                cycles than fp32 16x16x4).  Per-workgroup partial slabs, reduced
+//                deterministically by k_finalize.
 #include "net.h"
 #include "gemm.h"
 #include "net_bwd.h"
@@ -134,15 +137,25 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ z, i
 #define CB_L1_LD 20
 #define CB_L1 (C1_P * CB_L1_LD * 4)          // 32000
 #define CB_DL2_LD 36
-#define CB_DL2 (C2_Q * CB_DL2_LD * 4)        // 11664
+#define CB_DL2 ((C2_Q + 1) * CB_DL2_LD * 4)  // 11808: row C2_Q stays zero (phase (b) off-grid taps)
 #define CB_L1ST (C1_P * C1_N * 4)            // 25600: linear DMA staging of l1
 #define CB_DL2ST (FLAT * 4)                  // 10368: linear DMA staging of dl2
-// LDS: x8[2] | l1 stage | dl2 stage | l1s (dl1 written in place) | dl2s | red
 #define CB_RED (8 * 64 * 4)
-#define CB_SMEM_DMA (2 * CB_X8 + CB_L1ST + CB_DL2ST + CB_L1 + CB_DL2 + CB_RED)   // 138128
-// compact variant (no prefetch): x8 | l1s | dl2s | red -- leaves LDS for co-resident rollout
-// kernels when the backward overlaps the next rollout (engine overlap mode)
-#define CB_SMEM_COMPACT (CB_X8 + CB_L1 + CB_DL2 + CB_RED)                              // 73936
+// dl1 as three bf16 terms, dlb[term][n][k] with k = 24 oy + ox (ox 20..23 padding, masked in
+// the MFMA operand): rows of 60 16-byte slots (8 k each), slot G of row n stored at
+// 4 (G >> 2) + ((G + ((n >> 1) & 2)) & 3) so that each 16-lane group of a ds_read_b128 in phase
+// (c) covers the 64 banks once
+#define CB_DLB_LD 480
+#define CB_DLB (3 * C1_N * CB_DLB_LD * 2)    // 46080
+__device__ inline int dlb_slot(int G, int n) { return 4 * (G >> 2) + ((G + ((n >> 1) & 2)) & 3); }
+// l1s | dl2s | red, overlaid after phase (b) by dlb
+#define CB_TAIL_RAW (CB_L1 + CB_DL2 + CB_RED)
+#define CB_TAIL (CB_TAIL_RAW > CB_DLB ? CB_TAIL_RAW : CB_DLB)
+// LDS: x8[2] | l1 stage | dl2 stage | tail
+#define CB_SMEM_DMA (2 * CB_X8 + CB_L1ST + CB_DL2ST + CB_TAIL)                         // 138496
+// compact variant (no prefetch): x8 | tail -- leaves LDS for co-resident rollout kernels when
+// the backward overlaps the next rollout (engine overlap mode)
+#define CB_SMEM_COMPACT (CB_X8 + CB_TAIL)                                               // 74304
 
 // one 16-byte-per-lane global -> LDS DMA wave-instruction: lane l's 16 bytes land at
 // lds_base + 16 l (lds_base wave-uniform), no VGPR destination
@@ -163,7 +176,7 @@ __device__ inline void glds_copy(const uint8_t* g, uint8_t* dst, int nbytes, int
 __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <bool DMA, int NW>
-__global__ void __launch_bounds__(64 * NW) k_conv_bwd(StateAddr sa, int64_t B, int per_wg,
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) k_conv_bwd(StateAddr sa, int64_t B, int per_wg,
                                                   const float* __restrict__ act_l1,
                                                   const float* __restrict__ dl2,
                                                   const float* __restrict__ W2,
@@ -174,7 +187,7 @@ __global__ void __launch_bounds__(64 * NW) k_conv_bwd(StateAddr sa, int64_t B, i
   uint8_t* dl2st = l1st + (DMA ? CB_L1ST : 0);
   float* l1s = (float*)(dl2st + (DMA ? CB_DL2ST : 0));
   float* dl2s = (float*)((uint8_t*)l1s + CB_L1);
-  float* dl1s = l1s;                                                 // dl1 overwrites l1 in place
+  uint16_t* dlb = (uint16_t*)l1s;                                    // dl1 terms after phase (b)
   float* red = (float*)((uint8_t*)dl2s + CB_DL2);                    // [NW waves][64]
   constexpr int NT = 64 * NW;
   constexpr int T = 16 / NW;          // (kh,kw) tiles of dW2 and K1 tiles of dW1 per wave
@@ -189,6 +202,7 @@ __global__ void __launch_bounds__(64 * NW) k_conv_bwd(StateAddr sa, int64_t B, i
   const int py = (wid & 3) >> 1, px = wid & 1;
   const int mt_lo = NW == 8 ? (wid >> 2) * 4 : 0, mt_hi = NW == 8 ? (wid >> 2 ? 7 : 4) : 7;
   // W2 taps for the class: w2c[(dy*2+dx)*8 + nb*4 + c4] = W2[py+2dy][px+2dx][ci=i16][16nb+4j4+c4]
+  const float* w2lane = W2 + ((py * C2_K + px) * C1_N + i16) * C2_N + 4 * j4;
   float w2c[32];
 #pragma unroll
   for (int dy = 0; dy < 2; ++dy)
@@ -196,18 +210,23 @@ __global__ void __launch_bounds__(64 * NW) k_conv_bwd(StateAddr sa, int64_t B, i
     for (int dx = 0; dx < 2; ++dx)
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
-        const int kh = py + 2 * dy, kw = px + 2 * dx;
-        f32x4 w = *(const f32x4*)(W2 + ((kh * C2_K + kw) * C1_N + i16) * C2_N + 16 * nb + 4 * j4);
+        const f32x4 w = *(const f32x4*)(w2lane + (2 * dy * C2_K + 2 * dx) * C1_N * C2_N + 16 * nb);
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4) w2c[(dy * 2 + dx) * 8 + nb * 4 + c4] = w[c4];
       }
 
   f32x4 accW2[T][2];
-  f32x4 accW1[T];
+  f32x4 accW1[4];
 #pragma unroll
-  for (int t = 0; t < T; ++t) {
-    accW2[t][0] = accW2[t][1] = accW1[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  }
+  for (int t = 0; t < T; ++t) accW2[t][0] = accW2[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) accW1[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // phase (c) tiles: wave w4 = wid & 3 owns the 4 M-tiles (kh = 4 (w4 >> 1) + (row >> 2),
+  // kw = t + 4 (w4 & 1), cin = row & 3), t = 0..3; with 8 waves, waves w4 and w4 + 4 split the
+  // K chunks (even / odd)
+  const int w4 = wid & 3;
+  const int c_first = NW == 8 ? wid >> 2 : 0, c_step = NW == 8 ? 2 : 1;
+  const int xoff_c = (i16 & 3) * PLANE + (4 * (w4 >> 1) + (i16 >> 2)) * IMG + 4 * (w4 & 1);
   float db1acc = 0.f, db2acc = 0.f;
 
   // Operands of sample b+1 (x planes, l1, dl2: 64 KB) are DMA'd global -> LDS while sample b
@@ -234,6 +253,7 @@ __global__ void __launch_bounds__(64 * NW) k_conv_bwd(StateAddr sa, int64_t B, i
         const int q = i >> 3, q4 = i & 7;
         *(f32x4*)(dl2s + q * CB_DL2_LD + 4 * q4) = ((const f32x4*)dl2st)[i];
       }
+      if (tid < 8) *(f32x4*)(dl2s + C2_Q * CB_DL2_LD + 4 * tid) = (f32x4){0.f, 0.f, 0.f, 0.f};
       __syncthreads();                                    // staging buffers free again
       if (b + 1 < b1) issue(b + 1, x8buf + ((b + 1 - b0) & 1) * CB_X8);
     } else {
@@ -247,6 +267,7 @@ __global__ void __launch_bounds__(64 * NW) k_conv_bwd(StateAddr sa, int64_t B, i
         const int q = i >> 3, q4 = i & 7;
         *(f32x4*)(dl2s + q * CB_DL2_LD + 4 * q4) = *(const f32x4*)(dl2 + b * FLAT + q * C2_N + 4 * q4);
       }
+      if (tid < 8) *(f32x4*)(dl2s + C2_Q * CB_DL2_LD + 4 * tid) = (f32x4){0.f, 0.f, 0.f, 0.f};
       __syncthreads();
     }
 
@@ -271,22 +292,30 @@ __global__ void __launch_bounds__(64 * NW) k_conv_bwd(StateAddr sa, int64_t B, i
     lds_barrier();   // every wave done reading l1 in (a): (b) overwrites it with dl1
 
     // ---- (b) dl1 for parity class (py,px): 100 positions in 7 M-tiles of 16 ----
-    for (int mt = mt_lo; mt < mt_hi; ++mt) {
-      const int pc = 16 * mt + i16;
+    constexpr int MTB = NW == 8 ? 4 : 7;
+    // per-sample copies of the lane coordinates: keeps the compiler from hoisting every tile's
+    // LDS addresses out of the sample loop (they would pin ~80 VGPRs)
+    int bj4 = j4, bi16 = i16;
+    asm volatile("" : "+v"(bj4), "+v"(bi16));
+#pragma unroll
+    for (int u = 0; u < MTB; ++u) {
+      const int mt = mt_lo + u;
+      if (mt >= mt_hi) break;
+      const int pc = 16 * mt + bi16;
       const int pcc = pc < 100 ? pc : 99;
       const int ay = pcc / 10, cx = pcc - ay * 10;
+      const int base = ay * C2_O + cx;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accb = {0.f, 0.f, 0.f, 0.f};   // two chains (nb)
 #pragma unroll
       for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
         for (int dx = 0; dx < 2; ++dx) {
-          const int oy = ay - dy, ox = cx - dx;
-          const bool v = oy >= 0 && oy < C2_O && ox >= 0 && ox < C2_O && pc < 100;
-          const int qq = v ? oy * C2_O + ox : 0;
+          // dl2 position (ay - dy, cx - dx); off the 9x9 grid -> the zero row
+          const bool v = (dy ? ay > 0 : ay < C2_O) && (dx ? cx > 0 : cx < C2_O);
+          const int qq = v ? base - C2_O * dy - dx : C2_Q;
 #pragma unroll
           for (int nb = 0; nb < 2; ++nb) {
-            f32x4 a = *(const f32x4*)(dl2s + qq * CB_DL2_LD + 16 * nb + 4 * j4);
-            if (!v) a = (f32x4){0.f, 0.f, 0.f, 0.f};
+            const f32x4 a = *(const f32x4*)(dl2s + qq * CB_DL2_LD + 16 * nb + 4 * bj4);
             f32x4& c = nb ? accb : acc;
 #pragma unroll
             for (int c4 = 0; c4 < 4; ++c4)
@@ -296,12 +325,12 @@ __global__ void __launch_bounds__(64 * NW) k_conv_bwd(StateAddr sa, int64_t B, i
       acc += accb;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int pr = 16 * mt + 4 * j4 + r;
-        if (pr < 100) {
-          const int yy = 2 * (pr / 10) + py, xx = 2 * (pr % 10) + px;
-          const int p = yy * C1_O + xx;
-          const float g = l1s[p * CB_L1_LD + i16] > 0.f ? acc[r] : 0.f;
-          dl1s[p * CB_L1_LD + i16] = g;
+        const int pr = 16 * mt + 4 * bj4 + r;
+        const int prc = pr < 100 ? pr : 99;
+        const int p = (2 * (prc / 10) + py) * C1_O + 2 * (prc % 10) + px;
+        if (pr < 100) {                          // dl1 in place over l1 (this lane's own slot)
+          const float g = l1s[p * CB_L1_LD + bi16] > 0.f ? acc[r] : 0.f;
+          l1s[p * CB_L1_LD + bi16] = g;
           db1acc += g;
         }
       }
@@ -312,25 +341,86 @@ __global__ void __launch_bounds__(64 * NW) k_conv_bwd(StateAddr sa, int64_t B, i
       for (int q = 0; q < C2_Q; ++q) s2 += dl2s[q * CB_DL2_LD + tid];
       db2acc += s2;
     }
-    lds_barrier();   // dl1 complete (the DMA for sample b+1 stays in flight)
+    lds_barrier();   // dl1 complete in l1s
+    // dl1 -> three bf16 terms in dlb, which overlays l1s / dl2s: all reads first
+    {
+      constexpr int PER = (C1_P * C1_N + NT - 1) / NT;
+      float v[PER];
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int e = min(tid + NT * i, C1_P * C1_N - 1);
+        v[i] = l1s[(e >> 4) * CB_L1_LD + (e & 15)];
+      }
+      lds_barrier();   // (the DMA for b+1 stays in flight)
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int e = tid + NT * i;
+        if (e < C1_P * C1_N) {
+          // dl1 = hi + mid + lo (round-to-nearest bf16 terms, ~2^-24 relative)
+          const int pos = e >> 4, n = e & 15;
+          const int oy = pos / C1_O, k = pos + 4 * oy;           // k = 24 oy + ox
+          const __bf16 h = (__bf16)v[i];
+          const float r1 = v[i] - (float)h;
+          const __bf16 m = (__bf16)r1;
+          const __bf16 l = (__bf16)(r1 - (float)m);
+          __bf16* d = (__bf16*)dlb + n * CB_DLB_LD + 8 * dlb_slot(k >> 3, n) + (k & 7);
+          d[0] = h;
+          d[C1_N * CB_DLB_LD] = m;
+          d[2 * C1_N * CB_DLB_LD] = l;
+        }
+      }
+    }
+    // zero padding k = 24 oy + 20..23 (slot 3 oy + 2, elements 4..7) of every term row
+    for (int i = tid; i < 3 * C1_N * C1_O; i += NT) {
+      const int row = i / C1_O, oy = i - row * C1_O;
+      *(uint2*)(dlb + row * CB_DLB_LD + 8 * dlb_slot(3 * oy + 2, row & 15) + 4) = make_uint2(0u, 0u);
+    }
+    lds_barrier();   // dl1 terms complete
 
     // ---- (c) dW1[(kh,kw,cin)][n] += sum_p x[cin][4oy+kh][4ox+kw] * dl1[p][n]  (x unscaled) ----
-    int koff[T];
+    // v_mfma_f32_16x16x32_bf16: a u8 pixel is exact in bf16, dl1 = three bf16 terms, so every
+    // product is exact in the fp32 accumulator.  K = 15 chunks of 32 padded positions: lane group
+    // g takes 8 consecutive ox of (oy, ox block) G = 4 chunk + g (oy = G / 3, ox = 8 (G % 3) + j).
+    // One dword of x holds the pixels of kw & 3 = 0..3 for one ox: 8 dwords feed the 4 tiles.
+    // operands of chunk c: 8 x dwords and the 3 dl1-term fragments (next chunk's prefetched
+    // while this one's MFMAs run)
+    auto load_chunk = [&](int c, uint32_t (&d)[8], bf16x8 (&bv)[3]) {
+      const int G = 4 * c + j4;
+      const int oy = G / 3, blk = G - 3 * oy;
+      const uint32_t* xp = (const uint32_t*)(x8 + xoff_c + 4 * oy * IMG + 32 * blk);
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const int k = 16 * (T * wid + t) + i16;
-      const int s8 = k >> 2, cin = k & 3;
-      const int kh = s8 >> 3, kw = s8 & 7;
-      koff[t] = cin * PLANE + kh * IMG + kw;
-    }
-    for (int s = 0; s < C1_P / 4; ++s) {
-      const int p = 4 * s + j4;
-      const int oy = p / C1_O, ox = p - oy * C1_O;
-      const int base = (C1_S * oy) * IMG + C1_S * ox;
-      const float bv = dl1s[p * CB_L1_LD + i16];
+      for (int j = 0; j < 8; ++j) d[j] = xp[j];
 #pragma unroll
-      for (int t = 0; t < T; ++t)
-        accW1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)x8[base + koff[t]], bv, accW1[t], 0, 0, 0);
+      for (int term = 0; term < 3; ++term)
+        bv[term] = *(const bf16x8*)(dlb + (term * C1_N + i16) * CB_DLB_LD + 8 * dlb_slot(G, i16));
+    };
+    auto mma_chunk = [&](const uint32_t (&d)[8], const bf16x8 (&bt)[3]) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        uint32_t a[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float f0 = (float)((d[2 * jj] >> (8 * t)) & 255u);
+          const float f1 = (float)((d[2 * jj + 1] >> (8 * t)) & 255u);
+          a[jj] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
+        }
+        const bf16x8 av = __builtin_bit_cast(bf16x8, make_uint4(a[0], a[1], a[2], a[3]));
+        accW1[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bt[0], accW1[t], 0, 0, 0);
+        accW1[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bt[1], accW1[t], 0, 0, 0);
+        accW1[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bt[2], accW1[t], 0, 0, 0);
+      }
+    };
+    // two operand sets in flight: chunk c + step loads while chunk c multiplies
+    uint32_t d0[8], d1[8];
+    bf16x8 b0[3], b1[3];
+    load_chunk(c_first, d0, b0);
+#pragma unroll 1
+    for (int c = c_first; c < 15; c += 2 * c_step) {
+      const bool has1 = c + c_step < 15;
+      if (has1) load_chunk(c + c_step, d1, b1);
+      mma_chunk(d0, b0);
+      if (c + 2 * c_step < 15) load_chunk(c + 2 * c_step, d0, b0);
+      if (has1) mma_chunk(d1, b1);
     }
   }
 
@@ -341,11 +431,31 @@ __global__ void __launch_bounds__(64 * NW) k_conv_bwd(StateAddr sa, int64_t B, i
     const int mt = T * wid + t;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int krow = 16 * mt + 4 * j4 + r;     // dW1 row (kh,kw,cin) / dW2 row (kh,kw,ci)
-      out[CB_OFF_W1 + krow * C1_N + i16] = accW1[t][r];
+      const int krow = 16 * mt + 4 * j4 + r;     // dW2 row (kh,kw,ci)
       out[CB_OFF_W2 + krow * C2_N + i16] = accW2[t][0][r];
       out[CB_OFF_W2 + krow * C2_N + 16 + i16] = accW2[t][1][r];
     }
+  }
+  if constexpr (NW == 8) {                       // fold the odd-chunk half of dW1 (waves 4..7)
+    __syncthreads();                             // LDS free: every wave past its last phase (c)
+    f32x4* part = (f32x4*)smem;
+    if (wid >= 4)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) part[(w4 * 4 + t) * 64 + lane] = accW1[t];
+    __syncthreads();
+    if (wid < 4)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) accW1[t] += part[(w4 * 4 + t) * 64 + lane];
+  }
+  if (wid < 4) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        // D row 4 j4 + r of tile t: kh = 4 (w4 >> 1) + j4, kw = t + 4 (w4 & 1), cin = r
+        const int krow = ((4 * (w4 >> 1) + j4) * C1_K + t + 4 * (w4 & 1)) * HIST + r;
+        out[CB_OFF_W1 + krow * C1_N + i16] = accW1[t][r];
+      }
   }
   // db1: lanes with equal i16 (4 j4 groups) then the waves, in a fixed order
   db1acc += __shfl_xor(db1acc, 16, 64);

@@ -30,12 +30,6 @@
 // Fragment-ordered buffer w1s[kh][term][lane][j] (bf16): lane l = (cin g = l>>4, cout i = l&15)
 // holds B[k = 8g + j][i] = W1[kh][kw = j][cin = g][cout = i] (ops.py:21 layout).
 // ---------------------------------------------------------------------------------------
-__device__ inline uint32_t bf16_rn_bits(float f) {
-  uint32_t u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return u >> 16;
-}
-
 // Forward weight preparation, once per parameter version (rollout start): the conv1 bf16
 // terms above and the fc weights in MFMA fragment order, Wp[ct][c][lane][c4] =
 // W[16c + 4(lane>>4) + c4][16ct + (lane&15)], so a lane's B operands for 4 MFMAs are one 16-byte load.

@@ -12,7 +12,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), 'lib', 'liba3c_hip.so')
+# A3C_LIB: alternative build of the same library (kernel A/B experiments, tools/ab.sh)
+LIB_PATH = os.environ.get('A3C_LIB') or os.path.join(os.path.dirname(_HERE), 'lib', 'liba3c_hip.so')
 
 A3C_ALGO_A3C = 0
 A3C_ALGO_Q = 1
