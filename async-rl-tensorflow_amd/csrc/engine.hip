@@ -624,7 +624,8 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
       case A3C_KER_ENV_STEP:
         return a3c_env_screen_launch(E, sl.frames, e->pool, e->ring, e->R, e->counters, 0, s);
       case A3C_KER_HEAD_SCREEN: {
-        // head + action draw + Environment.screen of the last step's frames (env not stepped)
+        // head + action draw + env act + Environment.screen as in rollout step 0 (idempotent:
+        // the env state is read from the tau-parity half and written to the other one)
         HeadSelect sel = {};
         sel.mode = L.algo == A3C_ALGO_Q ? 1 : 0;
         sel.k0 = e->k0; sel.k1 = e->k1;
@@ -632,7 +633,9 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
         sel.env_id_base = e->cfg.env_id_base; sel.E = E; sel.par_E = E;
         sel.eps = e->eps;
         sel.actions = sl.actions;
-        sel.env_on = 0;
+        sel.env_on = 1;
+        sel.envp = e->envp; sel.envb = e->env;
+        sel.rewards = sl.rewards; sel.terms = sl.terms;
         sel.frames_out = sl.frames;
         sel.pool = e->pool; sel.ring = e->ring; sel.R = e->R;
         return a3c_head_screen_launch(L, e->params, sl.act_l3, E, sl.z, sel, s);

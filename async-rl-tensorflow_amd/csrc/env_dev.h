@@ -20,9 +20,10 @@ __device__ inline EnvState env_load(const EnvBufs& b, int64_t i) {
   return s;
 }
 
-__device__ inline void env_store(const EnvBufs& b, int64_t i, const EnvState& s) {
+__device__ inline void env_store(const EnvBufs& b, int64_t i, const EnvState& s, bool frame = true) {
   b.episode[i] = s.episode; b.ep_step[i] = s.ep_step; b.ep_len[i] = s.ep_len;
-  b.lives[i] = s.lives; b.frame[i] = s.frame; b.reward[i] = s.reward; b.terminal[i] = (uint8_t)s.terminal;
+  b.lives[i] = s.lives; b.reward[i] = s.reward; b.terminal[i] = (uint8_t)s.terminal;
+  if (frame) b.frame[i] = s.frame;
 }
 
 // self.env.reset() (environment.py:76)
@@ -35,13 +36,17 @@ __device__ inline void env_reset(EnvState& s, const EnvParams& p, uint32_t id) {
   s.frame = (int32_t)(x.y % (uint32_t)p.P);
 }
 
-// self.env.step(action) (environment.py:88-89)
-__device__ inline void env_step_raw(EnvState& s, const EnvParams& p, uint32_t id, uint32_t action) {
+// frame index of a step whose draw was x.x, for `action`
+__device__ inline int32_t env_frame_of(uint32_t xx, uint32_t action, const EnvParams& p) {
+  return (int32_t)((xx + action * GOLDEN_MULT) % (uint32_t)p.P);
+}
+
+// self.env.step(action) (environment.py:88-89) without the frame: nothing here depends on the
+// action, which only picks the frame (env_frame_of(returned x.x, action))
+__device__ inline uint32_t env_step_core(EnvState& s, const EnvParams& p, uint32_t id) {
   const uint32_t st = s.ep_step + 1u;
   s.ep_step = st;
   u32x4 x = philox4x32(st, id, s.episode, P_STEP, p.k0, p.k1);
-  const uint32_t mix = x.x + action * GOLDEN_MULT;
-  s.frame = (int32_t)(mix % (uint32_t)p.P);
   const float u = u01(x.y);
   const float rp = 0.02f;
   s.reward = u < rp ? 1.0f : (u >= 1.0f - rp ? -1.0f : 0.0f);
@@ -51,6 +56,12 @@ __device__ inline void env_step_raw(EnvState& s, const EnvParams& p, uint32_t id
   if (over) lives = 0;
   s.lives = lives;
   s.terminal = (over || (p.L0 > 0 && lives == 0)) ? 1u : 0u;
+  return x.x;
+}
+
+// self.env.step(action) (environment.py:88-89)
+__device__ inline void env_step_raw(EnvState& s, const EnvParams& p, uint32_t id, uint32_t action) {
+  s.frame = env_frame_of(env_step_core(s, p, id), action, p);
 }
 
 // Environment.new_random_game (environment.py:81-86) via new_game (:74-79)
@@ -62,12 +73,15 @@ __device__ inline void env_new_random_game(EnvState& s, const EnvParams& p, uint
   for (uint32_t i = 0; i < k; ++i) env_step_raw(s, p, id, 0u);
 }
 
-// GymEnvironment.act (environment.py:124-142)
-__device__ inline void env_act(EnvState& s, const EnvParams& p, uint32_t id, uint32_t action, bool training) {
+// GymEnvironment.act (environment.py:124-142) up to the frame: the repeats' rewards, lives
+// and terminal do not depend on the action; returns the last executed step's draw, whose
+// frame is env_frame_of(draw, action) (so the act can run before the action is drawn)
+__device__ inline uint32_t env_act_pre(EnvState& s, const EnvParams& p, uint32_t id, bool training) {
   float cum = 0.f;
   const int32_t start_lives = s.lives;
+  uint32_t xx = 0;
   for (int r = 0; r < p.action_repeat; ++r) {
-    env_step_raw(s, p, id, action);
+    xx = env_step_core(s, p, id);
     cum = cum + s.reward;
     if (training && start_lives > s.lives) {
       cum -= 1.0f;
@@ -76,5 +90,11 @@ __device__ inline void env_act(EnvState& s, const EnvParams& p, uint32_t id, uin
     if (s.terminal) break;
   }
   s.reward = cum;
+  return xx;
+}
+
+// GymEnvironment.act (environment.py:124-142)
+__device__ inline void env_act(EnvState& s, const EnvParams& p, uint32_t id, uint32_t action, bool training) {
+  s.frame = env_frame_of(env_act_pre(s, p, id, training), action, p);
 }
 

@@ -275,7 +275,7 @@ __device__ inline float head_row(const float* __restrict__ h3, int64_t b, const 
       const bool val = o == A;
       const float* w = val ? Wv + 32 * c : Wp + (int64_t)(32 * c) * A + o;
       const int st = val ? 1 : A;
-#pragma unroll 8
+#pragma unroll
       for (int k = 0; k < 32; ++k) p += hp[k] * w[k * st];
     }
     p += __shfl_xor(p, 8, 64);
@@ -339,9 +339,10 @@ __global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, 
   if (sel.mode >= 0) (void)head_act(myz, lane, A, sel, b);
 }
 
-// engine rollout step tail, one workgroup per env: head + action draw + env act (wave 0), then
-// the whole workgroup computes Environment.screen (environment.py:49-53, bit-exact) of the
-// post-act frame straight from the HBM pool into the env's frame-ring slot
+// engine rollout step tail, one workgroup per env: head + action draw (wave 0) while wave 1
+// runs the env act up to the frame (env_act_pre: nothing but the frame depends on the action),
+// then the whole workgroup computes Environment.screen (environment.py:49-53, bit-exact) of
+// the post-act frame straight from the HBM pool into the env's frame-ring slot
 template <int HS_THREADS>
 __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restrict__ h3,
                                                             const float* __restrict__ Wp,
@@ -350,18 +351,66 @@ __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restr
                                                             const float* __restrict__ bv, int A, int zs,
                                                             float* __restrict__ z, HeadSelect sel) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  __shared__ int32_t s_frame;
-  const int lane = threadIdx.x & 63;
+  __shared__ int32_t s_act;
+  __shared__ uint32_t s_draw, s_term;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t b = blockIdx.x;
-  if (threadIdx.x < 64) {
+  const int64_t tau = *sel.tau_ptr + sel.tau_add;
+  const int e = (int)b;
+  const int64_t nxt = ((tau + 1) & 1) * (int64_t)sel.par_E + e;
+#ifdef HS_TIMES
+  uint64_t* dbg = blockIdx.x == HS_TIMES ? (uint64_t*)z : nullptr;
+  if (dbg && threadIdx.x == 0) dbg[0] = __builtin_readcyclecounter();
+#endif
+  if (wid == 0) {
     const float myz = head_row(h3, b, Wp, bp, Wv, bv, A, lane);
+#ifdef HS_TIMES
+    if (dbg && lane == 0) dbg[1] = __builtin_readcyclecounter() + (uint64_t)(myz * 0.f);
+#else
     if (lane < zs) z[b * zs + lane] = myz;
-    const int32_t f = head_act(myz, lane, A, sel, b);
-    if (lane == 0) s_frame = f >= 0 ? f : sel.frames_out[b];   // env_on = 0 (kernel timing): last frame
+#endif
+    const int32_t a = select_from_lanes(myz, lane, A, sel, b);
+    if (lane == 0) {
+      sel.actions[b] = a;
+      s_act = a;
+    }
+#ifdef HS_TIMES
+    if (dbg && lane == 0) dbg[2] = __builtin_readcyclecounter() + (uint64_t)a * 0;
+#endif
+  } else if (wid == 1 && lane == 0 && sel.env_on) {
+    const int64_t cur = (tau & 1) * (int64_t)sel.par_E + e;
+    const uint32_t id = (uint32_t)(sel.env_id_base + e);
+    EnvState s = env_load(sel.envb, cur);
+    const uint32_t draw = env_act_pre(s, sel.envp, id, true);
+    sel.rewards[e] = fmaxf(-1.0f, fminf(1.0f, s.reward));   // observe clip, agent.py:154
+    sel.terms[e] = (uint8_t)s.terminal;
+    s_draw = draw;
+    s_term = s.terminal;
+    if (s.terminal) {
+      env_new_random_game(s, sel.envp, id);                  // agent.py:66-67
+      env_store(sel.envb, nxt, s);
+    } else {
+      env_store(sel.envb, nxt, s, false);                    // frame: after the action draw
+    }
   }
   __syncthreads();
-  const int64_t tau = *sel.tau_ptr + sel.tau_add;
-  atari::screen_frame<HS_THREADS>(sel.pool + (int64_t)s_frame * (atari::IH * atari::IW * 3),
+  int32_t frame;
+  if (sel.env_on) {
+    frame = env_frame_of(s_draw, (uint32_t)s_act, sel.envp);
+    if (threadIdx.x == 0) {
+      sel.frames_out[e] = frame;
+      if (!s_term) sel.envb.frame[nxt] = frame;
+    }
+  } else {
+    frame = sel.frames_out[b];                               // last frame (no env act)
+  }
+#ifdef HS_TIMES
+  if (dbg && threadIdx.x == 0) dbg[3] = __builtin_readcyclecounter();
+  atari::screen_frame<HS_THREADS>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3),
+                                  sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE, smem, dbg);
+  return;
+#endif
+  atari::screen_frame<HS_THREADS>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3),
                                   sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE, smem);
 }
 

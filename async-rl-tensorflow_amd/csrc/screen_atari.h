@@ -100,22 +100,23 @@ __device__ inline uint4 lum16(const uint4 a, const uint4 b, const uint4 c) {
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
-// Horizontal pass of one gray row for output columns [X0, X0 + NX): the row window is read
-// as 6 dwords x 4 from LDS once and every tap is a compile-time byte of it (kH is constexpr);
-// the outputs are packed 4 per dword.  Half 0 = columns 0..43 (bytes 0..95), half 1 = 44..83
-// (bytes 80..175; taps past a row's count have weight 0, so bytes past the row are harmless).
-template <int H>
-__device__ inline void hpass_row(const uint8_t* __restrict__ grow, uint8_t* __restrict__ trow) {
-  constexpr int X0 = H ? 44 : 0, NX = H ? 40 : 44, BASE = H ? 80 : 0;
-  uint32_t w[24];
+// Horizontal pass of output columns [X0, X1) of one gray row (segments 0..3 = [0,24), [24,44),
+// [44,64), [64,84)): the 64-byte window from the 16-aligned byte below kH.xmin[X0] is read as
+// four ds_read_b128 and every tap is a compile-time byte of it; outputs packed 4 per dword.
+template <int SEG>
+__device__ inline void hpass_seg(const uint8_t* __restrict__ grow, uint8_t* __restrict__ trow) {
+  constexpr int X0 = SEG == 0 ? 0 : 4 + 20 * SEG, X1 = SEG == 0 ? 24 : X0 + 20;
+  constexpr int BASE = kH.xmin[X0] & ~15;
+  static_assert(kH.xmin[X1 - 1] + KH - 1 - BASE < 64, "horizontal window exceeds 64 bytes");
+  uint32_t w[16];
   const uint4* src = (const uint4*)(grow + BASE);
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
+  for (int i = 0; i < 4; ++i) {
     const uint4 v = src[i];
     w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
   }
 #pragma unroll
-  for (int q = 0; q < NX / 4; ++q) {
+  for (int q = 0; q < (X1 - X0) / 4; ++q) {
     uint32_t packed = 0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -132,16 +133,23 @@ __device__ inline void hpass_row(const uint8_t* __restrict__ grow, uint8_t* __re
   }
 }
 
-// Whole-frame Environment.screen by one workgroup of NT threads (gray 210x160 and the
-// horizontal-pass 210x84 in LDS, SCREEN_FRAME_SMEM bytes); the RGB frame streams from HBM
-// straight into registers (all of a thread's loads issued before any use).  The resampling
-// passes read LDS a dword (H: 24 per half row) or a column quad (V) at a time.
-#define SCREEN_FRAME_SMEM (210 * 160 + 210 * 84 + 96)
+// Whole-frame Environment.screen by one workgroup of NT threads (gray 210x160, the
+// horizontal-pass 210x84 and the vertical taps in LDS, SCREEN_FRAME_SMEM bytes); the RGB frame
+// streams from HBM straight into registers (all of a thread's loads issued before any use).
+// Both resampling passes give every wave the same amount of work with wave-uniform code:
+// horizontal = 16 tasks (column segment, block of 64 rows), lane = row; vertical = 28 tasks
+// of 3 output rows x 21 column quads, lane = (row, quad), taps read from the LDS table.
+#define SCREEN_KV_BYTES (84 * 8 * 4)
+#define SCREEN_FRAME_SMEM (210 * 160 + 210 * 84 + 96 + SCREEN_KV_BYTES)
 template <int NT>
-__device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __restrict__ out, uint8_t* smem) {
+__device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __restrict__ out, uint8_t* smem,
+                                    uint64_t* dbg = nullptr) {
   uint8_t* gray = smem;
   uint8_t* tmp = smem + IH * IW;
-  const int tid = threadIdx.x;
+  int* kvs = (int*)(tmp + IH * OW + 96);              // [yy][8]: 7 taps, xmin
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr int NWV = NT / 64;
   constexpr int NUNIT = IH * IW / 16;                  // 2100 units of 16 pixels
   constexpr int PER = (NUNIT + NT - 1) / NT;
   uint4 r[PER][3];
@@ -152,26 +160,35 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
     r[j][1] = s[1];
     r[j][2] = s[2];
   }
+  for (int i = tid; i < OH * 8; i += NT) kvs[i] = (i & 7) < KV ? cV.k[i >> 3][i & 7] : cV.xmin[i >> 3];
+  if (dbg && tid == 0) dbg[4] = __builtin_readcyclecounter() + (r[0][0].x & 0);   // first unit landed
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int u = tid + NT * j;
     if (u < NUNIT) *(uint4*)(gray + 16 * u) = lum16(r[j][0], r[j][1], r[j][2]);
   }
+  if (dbg && tid == 0) dbg[5] = __builtin_readcyclecounter();
   __syncthreads();
-  // horizontal: items (row, half), 420 of them
-  for (int it = tid; it < 2 * IH; it += NT) {
-    const int rr = it >> 1;
-    if (it & 1) hpass_row<1>(gray + rr * IW, tmp + rr * OW);
-    else hpass_row<0>(gray + rr * IW, tmp + rr * OW);
+  if (dbg && tid == 0) dbg[6] = __builtin_readcyclecounter();
+  for (int task = wid; task < 16; task += NWV) {
+    const int seg = task & 3, rr = (task >> 2) * 64 + lane;
+    if (rr < IH) {
+      const uint8_t* g = gray + rr * IW;
+      uint8_t* t = tmp + rr * OW;
+      if (seg == 0) hpass_seg<0>(g, t);
+      else if (seg == 1) hpass_seg<1>(g, t);
+      else if (seg == 2) hpass_seg<2>(g, t);
+      else hpass_seg<3>(g, t);
+    }
   }
   __syncthreads();
-  // vertical: items (column quad cq, band of 7 output rows), 21 x 12
-  for (int it = tid; it < (OW / 4) * (OH / 7); it += NT) {
-    const int cq = it % (OW / 4), band = it / (OW / 4);
-#pragma unroll
-    for (int yy7 = 0; yy7 < 7; ++yy7) {
-      const int yy = band * 7 + yy7;
-      const int b0 = cV.xmin[yy];
+  if (dbg && tid == 0) dbg[7] = __builtin_readcyclecounter();
+  const int sub = lane / (OW / 4), cq = lane - sub * (OW / 4);
+  for (int task = wid; task < OH / 3; task += NWV) {
+    if (sub < 3) {
+      const int yy = 3 * task + sub;
+      const int* kc = kvs + yy * 8;
+      const int b0 = kc[7];
       int acc[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) acc[c] = 1 << (A3C_PRECISION_BITS - 1);
@@ -179,7 +196,7 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
       for (int y = 0; y < KV; ++y) {
         const int ry = min(b0 + y, IH - 1);
         const uint32_t q = *(const uint32_t*)(tmp + ry * OW + 4 * cq);
-        const int k = cV.k[yy][y];
+        const int k = kc[y];
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[c] += (int)((q >> (8 * c)) & 255u) * k;
       }
@@ -188,6 +205,10 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
       for (int c = 0; c < 4; ++c) packed |= (uint32_t)a3c_clip8(acc[c]) << (8 * c);
       *(uint32_t*)(out + yy * OW + 4 * cq) = packed;
     }
+  }
+  if (dbg) {
+    __syncthreads();
+    if (tid == 0) dbg[8] = __builtin_readcyclecounter();
   }
 }
 
