@@ -35,8 +35,19 @@ static void launch_atari(const uint8_t* rgb, const int32_t* idx, int64_t n, uint
 
 // luminance step of Environment.screen alone (environment.py:97-98), the exact integer form the
 // Atari kernel uses: out[i] = truncated fp64 0.2126 R + 0.7152 G + 0.0722 B of pixel i
+// (groups of 4 pixels through atari::lum4 when the buffers are 4-byte aligned, else per pixel).
 __global__ void k_luminance(const uint8_t* __restrict__ rgb, int64_t npix, uint8_t* __restrict__ out) {
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x, t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t done = 0;
+  if ((((uintptr_t)rgb | (uintptr_t)out) & 3) == 0) {
+    const int64_t ng = npix / 4;
+    for (int64_t g = t0; g < ng; g += stride) {
+      const uint32_t* s = (const uint32_t*)(rgb + 12 * g);
+      ((uint32_t*)out)[g] = atari::lum4(s[0], s[1], s[2]);
+    }
+    done = 4 * ng;
+  }
+  for (int64_t p = done + t0; p < npix; p += stride)
     out[p] = (uint8_t)atari::lum_exact(rgb[3 * p], rgb[3 * p + 1], rgb[3 * p + 2]);
 }
 

@@ -60,6 +60,22 @@ constexpr Coef<IH, OH> kV{};
 constexpr int KH = Coef<IW, OW>::K;   // 5
 constexpr int KV = Coef<IH, OH>::K;   // 7
 
+// Bilinear taps are >= 0 and each output's sum stays below (2^30 - 2^21) / 255, so
+// 2^21 + sum(v k) for 8-bit v never leaves [0, 256 * 2^22): Pillow's clip is a plain shift here
+template <int IN, int OUT>
+constexpr bool taps_shift_only(const Coef<IN, OUT>& c) {
+  for (int xx = 0; xx < OUT; ++xx) {
+    long sum = 0;
+    for (int x = 0; x < Coef<IN, OUT>::K; ++x) {
+      if (c.k[xx][x] < 0) return false;
+      sum += c.k[xx][x];
+    }
+    if (255L * sum + (1L << (A3C_PRECISION_BITS - 1)) >= (256L << A3C_PRECISION_BITS)) return false;
+  }
+  return true;
+}
+static_assert(taps_shift_only(kH) && taps_shift_only(kV), "resampling taps need Pillow's clip");
+
 __constant__ Coef<IW, OW> cH = kH;
 __constant__ Coef<IH, OH> cV = kV;
 
@@ -83,6 +99,31 @@ __device__ inline uint32_t lum_exact(uint32_t r, uint32_t g, uint32_t b) {
   const uint32_t q = (uint32_t)(((uint64_t)y * 3518437209ull) >> 45);   // y / 10000 (exact for y < 2^32/..)
   if (q * 10000u == y) return a3c_lum(r, g, b);               // exact multiple: fp64 decides
   return q;
+}
+
+// 4 pixels (3 dwords of RGB) -> 4 luminance bytes, the same exact integer form:
+// y = 2126 R + 7152 G + 722 B from two v_dot4_u32_u8 over the weights' low / high bytes
+// (2126 = 8*256 + 78, 7152 = 27*256 + 240, 722 = 2*256 + 210), floor(y / 10^4) by a
+// multiply-high; a group with a multiple of 10^4 redoes its pixels with lum_exact.
+__device__ inline uint32_t lum4(uint32_t d0, uint32_t d1, uint32_t d2) {
+  constexpr uint32_t WLO = 78u | (240u << 8) | (210u << 16);
+  constexpr uint32_t WHI = 8u | (27u << 8) | (2u << 16);
+  const uint32_t px[4] = {d0, __builtin_amdgcn_alignbyte(d1, d0, 3), __builtin_amdgcn_alignbyte(d2, d1, 2), d2 >> 8};
+  uint32_t out = 0;
+  bool mult = false;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t y = __builtin_amdgcn_udot4(px[i], WLO, __builtin_amdgcn_udot4(px[i], WHI, 0u, false) << 8, false);
+    const uint32_t q = __umulhi(y, 3518437209u) >> 13;
+    mult |= q * 10000u == y;
+    out |= q << (8 * i);
+  }
+  if (mult) {
+    out = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out |= lum_exact(px[i] & 255u, (px[i] >> 8) & 255u, (px[i] >> 16) & 255u) << (8 * i);
+  }
+  return out;
 }
 
 // 16 pixels (48 bytes of RGB) -> 16 luminance bytes
@@ -127,7 +168,7 @@ __device__ inline void hpass_seg(const uint8_t* __restrict__ grow, uint8_t* __re
         const int bi = kH.xmin[xx] + x - BASE;
         acc += (int)((w[bi >> 2] >> (8 * (bi & 3))) & 255u) * kH.k[xx][x];
       }
-      packed |= (uint32_t)a3c_clip8(acc) << (8 * u);
+      packed |= (uint32_t)(acc >> A3C_PRECISION_BITS) << (8 * u);   // clip-free (taps_shift_only)
     }
     *(uint32_t*)(trow + X0 + 4 * q) = packed;
   }
@@ -150,22 +191,20 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr int NWV = NT / 64;
-  constexpr int NUNIT = IH * IW / 16;                  // 2100 units of 16 pixels
+  constexpr int NUNIT = IH * IW / 4;                   // 8400 units of 4 pixels (12 bytes)
   constexpr int PER = (NUNIT + NT - 1) / NT;
-  uint4 r[PER][3];
+  uint3 r[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    const uint4* s = (const uint4*)(rgb + 48 * min(tid + NT * j, NUNIT - 1));
-    r[j][0] = s[0];
-    r[j][1] = s[1];
-    r[j][2] = s[2];
+    const uint32_t* s = (const uint32_t*)(rgb + 12 * min(tid + NT * j, NUNIT - 1));
+    r[j] = make_uint3(s[0], s[1], s[2]);
   }
   for (int i = tid; i < OH * 8; i += NT) kvs[i] = (i & 7) < KV ? cV.k[i >> 3][i & 7] : cV.xmin[i >> 3];
-  if (dbg && tid == 0) dbg[4] = __builtin_readcyclecounter() + (r[0][0].x & 0);   // first unit landed
+  if (dbg && tid == 0) dbg[4] = __builtin_readcyclecounter() + (r[0].x & 0);   // first unit landed
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int u = tid + NT * j;
-    if (u < NUNIT) *(uint4*)(gray + 16 * u) = lum16(r[j][0], r[j][1], r[j][2]);
+    if (u < NUNIT) *(uint32_t*)(gray + 4 * u) = lum4(r[j].x, r[j].y, r[j].z);
   }
   if (dbg && tid == 0) dbg[5] = __builtin_readcyclecounter();
   __syncthreads();
@@ -202,7 +241,7 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
       }
       uint32_t packed = 0;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) packed |= (uint32_t)a3c_clip8(acc[c]) << (8 * c);
+      for (int c = 0; c < 4; ++c) packed |= (uint32_t)(acc[c] >> A3C_PRECISION_BITS) << (8 * c);
       *(uint32_t*)(out + yy * OW + 4 * cq) = packed;
     }
   }
