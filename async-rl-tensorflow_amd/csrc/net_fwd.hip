@@ -225,13 +225,52 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
 // ---------------------------------------------------------------------------------------
 // action selection from a head row held one-value-per-lane (lane j holds z[j])
 // ---------------------------------------------------------------------------------------
-__device__ inline int32_t select_from_lanes(float myz, int lane, int A, const HeadSelect& sel,
-                                            int64_t b) {
-  const int64_t tau = (sel.tau_ptr ? *sel.tau_ptr : 0) + sel.tau_add;
+// the action draw's counter-based random words for state b at step tau
+__device__ inline u32x4 action_draw(const HeadSelect& sel, int64_t b, int64_t tau) {
   const int e = (int)(b % sel.E);
   const uint32_t env = sel.env_ids ? (uint32_t)sel.env_ids[b] : (uint32_t)(sel.env_id_base + e);
-  u32x4 x = philox4x32((uint32_t)tau, (uint32_t)((uint64_t)tau >> 32), env, P_ACTION, sel.k0, sel.k1);
-  if (sel.mode == 0) {
+  return philox4x32((uint32_t)tau, (uint32_t)((uint64_t)tau >> 32), env, P_ACTION, sel.k0, sel.k1);
+}
+
+// x = action_draw(sel, b, tau); eps = the env's exploration rate (Q mode)
+__device__ inline int32_t select_with(float myz, int lane, int A, int mode, u32x4 x, float eps) {
+  if (A <= 8) {
+    // the logits to every lane via v_readlane (wave-uniform values, no cross-lane round trips)
+    float zv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) zv[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(myz), j));
+    if (mode == 0) {
+      float m = zv[0];
+#pragma unroll
+      for (int j = 1; j < 8; ++j) m = j < A ? fmaxf(m, zv[j]) : m;
+      // lane j: exp and probability of action j (one expf / divide per lane, in parallel)
+      const float ex = lane < A ? expf(myz - m) : 0.f;
+      float ssum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ssum += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ex), j));
+      const float pi = ex / ssum;
+      const float u = u01(x.x);
+      float cdf = 0.f;
+      int32_t act = A - 1;
+      bool found = false;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (j < A) {
+          cdf += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pi), j));
+          if (!found && cdf > u) { act = j; found = true; }
+        }
+      }
+      return act;
+    }
+    if (u01(x.x) < eps) return (int32_t)(x.y % (uint32_t)A);
+    float best = zv[0];
+    int32_t arg = 0;
+#pragma unroll
+    for (int j = 1; j < 8; ++j)
+      if (j < A && zv[j] > best) { best = zv[j]; arg = j; }
+    return arg;
+  }
+  if (mode == 0) {
     float l = lane < A ? myz : -INFINITY;
     float m = wave_max(l);
     float ex = lane < A ? expf(myz - m) : 0.f;
@@ -246,7 +285,6 @@ __device__ inline int32_t select_from_lanes(float myz, int lane, int A, const He
     }
     return act;
   } else {
-    float eps = sel.eps ? sel.eps[e] : 0.f;
     if (u01(x.x) < eps) return (int32_t)(x.y % (uint32_t)A);
     float best = __shfl(myz, 0, 64);
     int32_t arg = 0;
@@ -258,11 +296,21 @@ __device__ inline int32_t select_from_lanes(float myz, int lane, int A, const He
   }
 }
 
-// head: one wave per state.  z[b][j] = h3[b] . W[:,j] + bias[j]
-// logits / value (or q) of row b by one wave: lane j returns z[b][j] (0 past the outputs)
+__device__ inline int32_t select_from_lanes(float myz, int lane, int A, const HeadSelect& sel, int64_t b) {
+  const int64_t tau = (sel.tau_ptr ? *sel.tau_ptr : 0) + sel.tau_add;
+  const float eps = sel.mode != 0 && sel.eps ? sel.eps[b % sel.E] : 0.f;
+  return select_with(myz, lane, A, sel.mode, action_draw(sel, b, tau), eps);
+}
+
+struct NoMid {
+  __device__ void operator()() const {}
+};
+
+// mid(): work to overlap with the head's load latency (runs after the loads are issued)
+template <typename Mid = NoMid>
 __device__ inline float head_row(const float* __restrict__ h3, int64_t b, const float* __restrict__ Wp,
                                  const float* __restrict__ bp, const float* __restrict__ Wv,
-                                 const float* __restrict__ bv, int A, int lane) {
+                                 const float* __restrict__ bv, int A, int lane, Mid mid = Mid()) {
   float myz = 0.f;
   const int nout = A + (Wv ? 1 : 0);
   if (nout <= 8) {
@@ -270,21 +318,29 @@ __device__ inline float head_row(const float* __restrict__ h3, int64_t b, const 
     // then a 3-step butterfly over the 8 chunks
     const int o = lane & 7, c = lane >> 3;
     const float* hp = h3 + b * FC + 32 * c;
-    float p = 0.f;
-    if (o < nout) {
-      const bool val = o == A;
-      const float* w = val ? Wv + 32 * c : Wp + (int64_t)(32 * c) * A + o;
-      const int st = val ? 1 : A;
+    const bool val = Wv && o == A;                 // (lanes o >= nout read column 0, result dropped)
+    const int oc = o < nout ? o : 0;
+    const float* w = val ? Wv + 32 * c : Wp + (int64_t)(32 * c) * A + oc;
+    const int st = val ? 1 : A;
+    float hv[32], wv[32];
 #pragma unroll
-      for (int k = 0; k < 32; ++k) p += hp[k] * w[k * st];
+    for (int k = 0; k < 32; ++k) {
+      hv[k] = hp[k];
+      wv[k] = w[k * st];
     }
+    const float bias = lane < A ? bp[lane] : (Wv && lane == A ? bv[0] : 0.f);
+    mid();
+    float p = 0.f;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) p += hv[k] * wv[k];
+    if (o >= nout) p = 0.f;
     p += __shfl_xor(p, 8, 64);
     p += __shfl_xor(p, 16, 64);
     p += __shfl_xor(p, 32, 64);
     const float zj = __shfl(p, lane & 7, 64);
-    if (lane < A) myz = zj + bp[lane];
-    else if (Wv && lane == A) myz = zj + bv[0];
+    if (lane < A || (Wv && lane == A)) myz = zj + bias;
   } else {
+    mid();
     f32x4 h = *(const f32x4*)(h3 + b * FC + 4 * lane);
     for (int j = 0; j < A; ++j) {
       const float* w = Wp + (int64_t)(4 * lane) * A + j;
@@ -363,13 +419,16 @@ __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restr
   if (dbg && threadIdx.x == 0) dbg[0] = __builtin_readcyclecounter();
 #endif
   if (wid == 0) {
-    const float myz = head_row(h3, b, Wp, bp, Wv, bv, A, lane);
+    const float eps = sel.mode != 0 && sel.eps ? sel.eps[e] : 0.f;
+    u32x4 x;
+    // the action draw does not depend on the head: computed under its load latency
+    const float myz = head_row(h3, b, Wp, bp, Wv, bv, A, lane, [&]() { x = action_draw(sel, b, tau); });
 #ifdef HS_TIMES
     if (dbg && lane == 0) dbg[1] = __builtin_readcyclecounter() + (uint64_t)(myz * 0.f);
 #else
     if (lane < zs) z[b * zs + lane] = myz;
 #endif
-    const int32_t a = select_from_lanes(myz, lane, A, sel, b);
+    const int32_t a = select_with(myz, lane, A, sel.mode, x, eps);
     if (lane == 0) {
       sel.actions[b] = a;
       s_act = a;
