@@ -81,7 +81,7 @@ extern "C" int a3c_forward(const a3c_net_desc* net, const float* params, const u
                            float* act_l1, float* act_l2, float* act_l3, float* z, void* workspace,
                            void* stream) {
   NetLayout L;
-  if (a3c_make_layout(net, &L) || !params || !states || !act_l2 || !act_l3 || !z || B < 0 ||
+  if (a3c_make_layout(net, &L) || L.lstm || !params || !states || !act_l2 || !act_l3 || !z || B < 0 ||
       B > 0x7fffffff || (((uintptr_t)states) & 15))
     return a3c_set_error(A3C_ERR_INVALID, "a3c_forward", "bad argument");
   if (B == 0) return 0;
@@ -136,7 +136,7 @@ extern "C" int a3c_loss_backward(const a3c_net_desc* net, const float* params, c
                                  const int32_t* actions, const float* target, float beta, int literal_adv,
                                  float* grads, float* loss_out, void* workspace, void* stream) {
   NetLayout L;
-  if (a3c_make_layout(net, &L) || !params || !states || !act_l1 || !act_l2 || !act_l3 || !z || !actions ||
+  if (a3c_make_layout(net, &L) || L.lstm || !params || !states || !act_l1 || !act_l2 || !act_l3 || !z || !actions ||
       !target || !grads || !workspace || B <= 0 || B > 0x7fffffff || (((uintptr_t)states) & 15))
     return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "bad argument");
   a3c_init_once();

@@ -40,6 +40,9 @@ struct Slot {
   float *act_l1, *act_l2, *act_l3;
   float *scr_l2, *scr_l3;  // bootstrap / target forward scratch
   uint8_t* prep;           // forward weights of P prepared for the kernels (k_prep_fwd)
+  // C5 LSTM head: per step h_t, c_t, masked inputs hp, cp [n][E][U], gates [n][E][4U];
+  // bootstrap-step h, c [E][U]
+  float *lh, *lc, *lhp, *lcp, *lg, *lhb, *lcb;
 };
 
 struct a3c_engine {
@@ -64,6 +67,8 @@ struct a3c_engine {
   float* eps;              // q: per env epsilon
   float* ep_end;           // q: per env final epsilon
   float* ws;               // backward workspace
+  float* lws;              // LSTM BPTT workspace (a3c_lstm_ws_floats)
+  float* ldh;              // LSTM: dL/dh_t from the heads [nE][U]
   double* opt_part;
   float* sched;            // [0] lr, [1] target-sync flag (device)
   TensorTab tt;
@@ -155,7 +160,9 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   e->cfg = *cfg;
   if (a3c_make_layout(&cfg->net, &e->L) || cfg->num_envs < 1 || cfg->n_step < 1 || cfg->n_step > 64 ||
       cfg->num_frames < 1 || cfg->random_start < 1 || cfg->action_repeat < 1 || cfg->world_size < 1 ||
-      (cfg->overlap && cfg->net.algo != A3C_ALGO_A3C)) {
+      (cfg->overlap && cfg->net.algo != A3C_ALGO_A3C) ||
+      (cfg->net.lstm_units && !cfg->overlap && cfg->n_step < 2)) {   // sync n=1 would read and
+                                                                       // write one state buffer
     delete e;
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "bad config");
   }
@@ -215,6 +222,19 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     ALLOC(sl.scr_l2, scrB * FLAT * 4);
     ALLOC(sl.scr_l3, scrB * FC * 4);
     ALLOC(sl.prep, PREP_BYTES);
+    if (L.lstm) {
+      ALLOC(sl.lh, nE * LSTM_U * 4);
+      ALLOC(sl.lc, nE * LSTM_U * 4);
+      ALLOC(sl.lhp, nE * LSTM_U * 4);
+      ALLOC(sl.lcp, nE * LSTM_U * 4);
+      ALLOC(sl.lg, nE * LSTM_G * 4);
+      ALLOC(sl.lhb, E * LSTM_U * 4);
+      ALLOC(sl.lcb, E * LSTM_U * 4);
+    }
+  }
+  if (L.lstm) {
+    ALLOC(e->lws, a3c_lstm_ws_floats(e->n, E) * 4);
+    ALLOC(e->ldh, nE * LSTM_U * 4);
   }
   ALLOC(e->prep_t, PREP_BYTES);
   ALLOC(e->zt, scrB * zs * 4);
@@ -334,11 +354,18 @@ static int enqueue_rollout(a3c_engine* e, const Slot& sl, hipStream_t s) {
   return rc;
 }
 
+// the slot holding the rollout before sl's (its last LSTM state is sl's carry-in)
+static const Slot& prev_slot(const a3c_engine* e, const Slot& sl) {
+  return e->nslot == 2 ? e->slot[&sl == &e->slot[0] ? 1 : 0] : sl;
+}
+
 static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
   const NetLayout& L = e->L;
   const int E = e->E, n = e->n, zs = L.zs;
   const bool q = L.algo == A3C_ALGO_Q;
+  const Slot& pv = prev_slot(e, sl);
+  const int64_t lastE = (int64_t)(n - 1) * E;
   int rc = a3c_prep_fwd_launch(L, sl.P, sl.prep, s);   // params are fixed for the rollout
   if (rc) return rc;
   if (q) {
@@ -367,8 +394,17 @@ static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
       sel.ring = e->ring;
       sel.R = e->R;
     }
+    LstmStep ls = {};
+    if (L.lstm) {   // carry-in: step t-1 of this rollout, or the last step of the previous one
+      const Slot& src = t > 0 ? sl : pv;
+      const int64_t so = t > 0 ? o - E : lastE;
+      ls.h_src = src.lh + so * LSTM_U; ls.c_src = src.lc + so * LSTM_U; ls.prev_terms = src.terms + so;
+      ls.hp = sl.lhp + o * LSTM_U; ls.cp = sl.lcp + o * LSTM_U; ls.gates = sl.lg + o * LSTM_G;
+      ls.h = sl.lh + o * LSTM_U; ls.c = sl.lc + o * LSTM_U;
+    }
     rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
-                            sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s);
+                            sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s,
+                            L.lstm ? &ls : nullptr);
     if (rc) return rc;
     if (!e->fused_screen) {
       rc = a3c_env_screen_launch(E, sl.frames + o, e->pool, e->ring, e->R, e->counters, t, s);
@@ -380,8 +416,13 @@ static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
     HeadSelect none = {};
     none.mode = -1;
     none.E = E;
+    LstmStep ls = {};
+    if (L.lstm) {
+      ls.h_src = sl.lh + lastE * LSTM_U; ls.c_src = sl.lc + lastE * LSTM_U; ls.prev_terms = sl.terms + lastE;
+      ls.h = sl.lhb; ls.c = sl.lcb;
+    }
     rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, n, e->counters), E, nullptr, sl.scr_l2, sl.scr_l3,
-                            sl.z + e->nE * zs, none, s);
+                            sl.z + e->nE * zs, none, s, L.lstm ? &ls : nullptr);
     if (rc) return rc;
   }
   if (e->overlap) {
@@ -427,10 +468,17 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
     ra.n = n; ra.E = E; ra.gamma = c.gamma; ra.R_out = sl.R_buf;
   }
   static const bool fork_env = getenv("A3C_BWD_FORK") ? atoi(getenv("A3C_BWD_FORK")) != 0 : false;  // measured slower
-  const bool fork = fork_env;
+  const bool fork = fork_env && !L.lstm;
+  LstmBwd lb = {};
+  if (L.lstm) {
+    lb.n = n; lb.E = E;
+    lb.h = sl.lh; lb.c = sl.lc; lb.hp = sl.lhp; lb.cp = sl.lcp; lb.gates = sl.lg;
+    lb.dh = e->ldh; lb.ws = e->lws;
+  }
   rc = a3c_backward_launch(L, sl.P, ring_addr(e, 0, sl.tau), e->nE, sl.act_l1, sl.act_l2, sl.act_l3, sl.z,
                            sl.actions, sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra,
-                           fork ? e->gs : nullptr, fork ? e->ev_gfork : nullptr, fork ? e->ev_gjoin : nullptr);
+                           fork ? e->gs : nullptr, fork ? e->ev_gfork : nullptr, fork ? e->ev_gjoin : nullptr,
+                           L.lstm ? &lb : nullptr);
   if (rc) return rc;
   // per-tensor squared norms (+ lr / target-sync schedule from the device step counter)
   OptParams op = opt_params(e);
@@ -503,6 +551,12 @@ extern "C" int a3c_engine_reset(a3c_engine* e, const float* host_params, void* s
   if (e->overlap)
     for (int k = 0; k < 2; ++k)
       A3C_CHECK(hipMemcpyAsync(e->slot[k].P, e->params, L.total * 4, hipMemcpyDeviceToDevice, s));
+  if (L.lstm)   // zero LSTM state (the first rollout's carry-in) and terminals
+    for (int k = 0; k < e->nslot; ++k) {
+      A3C_CHECK(hipMemsetAsync(e->slot[k].lh, 0, (size_t)e->nE * LSTM_U * 4, s));
+      A3C_CHECK(hipMemsetAsync(e->slot[k].lc, 0, (size_t)e->nE * LSTM_U * 4, s));
+      A3C_CHECK(hipMemsetAsync(e->slot[k].terms, 0, (size_t)e->nE, s));
+    }
   e->iter = 0;
   e->grad_ready = false;
   e->reset_done = true;
@@ -578,6 +632,10 @@ extern "C" int a3c_engine_slot_buffers(a3c_engine* e, int slot, a3c_engine_buffe
   b->zs = e->L.zs; b->n_tensors = e->L.nt;
   for (int i = 0; i < e->L.nt; ++i) { b->offsets[i] = e->L.off[i]; b->sizes[i] = e->L.size[i]; }
   b->sched = e->sched;
+  if (e->L.lstm) {
+    b->lstm_h = sl.lh; b->lstm_c = sl.lc; b->lstm_hp = sl.lhp; b->lstm_cp = sl.lcp; b->lstm_gates = sl.lg;
+    b->lstm_units = LSTM_U;
+  }
   return 0;
 }
 
@@ -638,7 +696,7 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
         sel.rewards = sl.rewards; sel.terms = sl.terms;
         sel.frames_out = sl.frames;
         sel.pool = e->pool; sel.ring = e->ring; sel.R = e->R;
-        return a3c_head_screen_launch(L, e->params, sl.act_l3, E, sl.z, sel, s);
+        return a3c_head_screen_launch(L, e->params, L.lstm ? sl.lh : sl.act_l3, E, sl.z, sel, s);
       }
       case A3C_KER_CONV_BWD: {
         const BwdPlan p = a3c_bwd_plan(L, e->nE);

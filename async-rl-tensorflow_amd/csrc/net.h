@@ -30,10 +30,14 @@ __device__ inline uint32_t bf16_rn_bits(float f) {
 #define KC2 (C2_K * C2_K * C1_N) // 256 = conv2 reduction length
 #define L1S_LD 20               // LDS row stride (floats) of the conv1 output tile
 
-enum { T_L1W = 0, T_L1B, T_L2W, T_L2B, T_FCW, T_FCB, T_HW, T_HB, T_VW, T_VB };
+enum { T_L1W = 0, T_L1B, T_L2W, T_L2B, T_FCW, T_FCB, T_HW, T_HB, T_VW, T_VB, T_LW, T_LB };
+#define LSTM_U 256              // C5 LSTM head width (A3C_LSTM_UNITS)
+#define LSTM_K (FC + LSTM_U)    // 512 = [x, h] rows of the gate matrix
+#define LSTM_G (4 * LSTM_U)     // 1024 gate columns (i, j, f, o)
 
 struct NetLayout {
   int algo, A, zs;
+  int lstm;                 // 1: LSTM head (tensors T_LW, T_LB; heads read the LSTM's h)
   int nt;
   int64_t off[A3C_MAX_TENSORS], size[A3C_MAX_TENSORS];
   int64_t total;
@@ -48,15 +52,17 @@ inline int a3c_make_layout(const a3c_net_desc* d, NetLayout* L) {
   if (!d) return -1;
   if (d->trunk != A3C_TRUNK_NIPS || d->history_length != HIST || d->screen_h != IMG ||
       d->screen_w != IMG || d->action_size < 1 || d->action_size > 31 ||
-      (d->algo != A3C_ALGO_A3C && d->algo != A3C_ALGO_Q))
+      (d->algo != A3C_ALGO_A3C && d->algo != A3C_ALGO_Q) ||
+      (d->lstm_units != 0 && (d->lstm_units != LSTM_U || d->algo != A3C_ALGO_A3C)))
     return -1;
   const int A = d->action_size;
   L->algo = d->algo;
   L->A = A;
   L->zs = a3c_zs(d->algo, A);
-  int64_t sizes[10] = {(int64_t)KC1 * C1_N, C1_N, (int64_t)KC2 * C2_N, C2_N, (int64_t)FLAT * FC, FC,
-                       (int64_t)FC * A, A, FC, 1};
-  L->nt = d->algo == A3C_ALGO_A3C ? 10 : 8;
+  L->lstm = d->lstm_units != 0;
+  int64_t sizes[12] = {(int64_t)KC1 * C1_N, C1_N, (int64_t)KC2 * C2_N, C2_N, (int64_t)FLAT * FC, FC,
+                       (int64_t)FC * A, A, FC, 1, (int64_t)LSTM_K * LSTM_G, LSTM_G};
+  L->nt = d->algo == A3C_ALGO_A3C ? (L->lstm ? 12 : 10) : 8;
   int64_t o = 0;
   for (int i = 0; i < L->nt; ++i) {
     L->off[i] = o;
@@ -116,9 +122,11 @@ struct HeadSelect {
 #define PREP_W1S_BYTES (W1S_ELEMS * 2)  // 24576
 #define FC_CH (FLAT / 16)               // 162 K-chunks of 16
 #define PREP_BYTES (PREP_W1S_BYTES + FLAT * FC * 4)
+struct LstmStep;
+// ls (LSTM head, C5): the cell step runs on act_l3 and the heads read ls->h
 int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* prep, const StateAddr& sa,
                        int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
-                       hipStream_t s);
+                       hipStream_t s, const LstmStep* ls = nullptr);
 int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s);
 // true while enqueuing work that runs concurrently with another stream (engine overlap mode)
 bool a3c_shared_gpu();

@@ -1,5 +1,6 @@
 #pragma once
 #include "net.h"
+#include "lstm.h"
 
 // per-workgroup partial slab of k_conv_bwd: dW1 [256][16] (unscaled by 1/255), dW2 [256][32],
 // db1 [16], db2 [32]
@@ -40,13 +41,24 @@ struct ReturnsArgs {
   float* R_out;              // [n*E] the returns (inspection)
 };
 
+// C5 LSTM head: the rollout's sequence buffers (engine slot) for the truncated BPTT; the
+// terminals come from ReturnsArgs.terms
+struct LstmBwd {
+  int n;
+  int64_t E;
+  const float *h, *c, *hp, *cp, *gates;   // [n][E][...]
+  float* dh;                              // [n*E][U] scratch: dL/dh_t from the heads
+  float* ws;                              // a3c_lstm_ws_floats(n, E) floats
+};
+
 BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B);
 int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
                         const float* act_l1, const float* act_l2, const float* act_l3,
                         const float* z, const int32_t* actions, const float* target, float beta,
                         int literal, float* grads, float* loss_out, float* ws, hipStream_t s,
                         const ReturnsArgs* ra = nullptr,
-                        hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr);
+                        hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr,
+                        const LstmBwd* lb = nullptr);
 int a3c_returns_launch(const float* rewards, const uint8_t* terms, const float* boot, int64_t boot_stride,
                        int n, int64_t E, double gamma, float* R, hipStream_t s);
 int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float* qn, int64_t B, int A,

@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ z, i
                                                   const float* __restrict__ Wv, float beta,
                                                   int literal, float invB, int64_t B,
                                                   float* __restrict__ dz, float* __restrict__ dh3,
-                                                  float* __restrict__ terms, ReturnsArgs ra) {
+                                                  float* __restrict__ terms, ReturnsArgs ra, int relu) {
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
@@ -124,9 +124,11 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ z, i
 #pragma unroll
     for (int i = 0; i < 4; ++i) g[i] += wv[i] * dV;
   }
-  f32x4 h = *(const f32x4*)(h3 + b * FC + 4 * lane);
+  if (relu) {    // feed-forward head: through the fc ReLU; LSTM head: dL/dh as is
+    f32x4 h = *(const f32x4*)(h3 + b * FC + 4 * lane);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) g[i] = h[i] > 0.f ? g[i] : 0.f;
+    for (int i = 0; i < 4; ++i) g[i] = h[i] > 0.f ? g[i] : 0.f;
+  }
   *(f32x4*)(dh3 + b * FC + 4 * lane) = g;
 }
 
@@ -562,7 +564,8 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
                         const float* act_l1, const float* act_l2, const float* act_l3,
                         const float* z, const int32_t* actions, const float* target, float beta,
                         int literal, float* grads, float* loss_out, float* ws, hipStream_t s,
-                        const ReturnsArgs* ra_in, hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join) {
+                        const ReturnsArgs* ra_in, hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join,
+                        const LstmBwd* lb) {
   ReturnsArgs ra = {};
   if (ra_in) ra = *ra_in;
   if (B <= 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "B must be > 0");
@@ -574,15 +577,26 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   float* terms = ws + p.terms;
   const bool a3c = L.algo == A3C_ALGO_A3C;
 
+  if (L.lstm != (lb != nullptr) || (lb && !ra.terms))
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "the LSTM head needs its rollout sequence");
+  // head input: the fc ReLU output, or the LSTM's h (C5)
+  const float* head_in = lb ? lb->h : act_l3;
   hipLaunchKernelGGL(k_head_bwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, z, L.zs, L.A, L.algo,
-                     actions, target, act_l3, P + L.off[T_HW], a3c ? P + L.off[T_VW] : nullptr, beta,
-                     literal, 1.0f / (float)B, B, dz, dh3, terms, ra);
+                     actions, target, head_in, P + L.off[T_HW], a3c ? P + L.off[T_VW] : nullptr, beta,
+                     literal, 1.0f / (float)B, B, dz, lb ? lb->dh : dh3, terms, ra, lb ? 0 : 1);
   A3C_CHECK(hipGetLastError());
+  if (lb) {
+    // truncated BPTT: dL/dh_t -> dl3 (masked by the fc ReLU) + the gate-matrix gradients
+    LstmSeq q = {act_l3, lb->hp, lb->cp, lb->gates, lb->c, ra.terms};
+    int rc0 = a3c_lstm_bptt_launch(P + L.off[T_LW], lb->n, lb->E, q, lb->dh, dh3, grads + L.off[T_LW],
+                                   grads + L.off[T_LB], lb->ws, s);
+    if (rc0) return rc0;
+  }
 
   // The weight-gradient GEMMs (head, fc) only need dz / dl3 from k_head_bwd: with a side stream
   // they run concurrently with the dl2 GEMM + conv backward (graph branches), joined before the
   // slab reductions.
-  const bool fork = side && ev_fork && ev_join;
+  const bool fork = side && ev_fork && ev_join && !lb;
   hipStream_t ws_s = fork ? side : s;
   if (fork) {
     A3C_CHECK(hipEventRecord(ev_fork, s));
@@ -590,7 +604,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   }
   // head weights: dWh[256][zs] = l3^T dz ; dbh = colsum(dz)
   GemmArgs g = {};
-  g.A = act_l3; g.lda = FC;          // A(m=feature, k=b) = l3[b][m]  (m contiguous)
+  g.A = head_in; g.lda = FC;         // A(m=feature, k=b) = l3[b][m]  (m contiguous)
   g.B = dz; g.ldb = L.zs;            // B(k=b, n=j) = dz[b][j]
   g.C = ws + p.hgrad; g.ldc = L.zs;
   g.M = FC; g.N = L.zs; g.K = (int)B;

@@ -13,6 +13,7 @@
 //  k_head_fwd   : one wave per state: logits/value (network.py:458,475) or q (agent.py:252),
 //                 then the action draw (softmax sample / epsilon-greedy argmax).
 #include "net.h"
+#include "lstm.h"
 #include "gemm.h"
 #include "net_bwd.h"
 #include "env_dev.h"
@@ -488,20 +489,28 @@ int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* 
 
 int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* prep, const StateAddr& sa,
                        int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
-                       hipStream_t s) {
+                       hipStream_t s, const LstmStep* ls) {
   if (B <= 0) return 0;
+  if (L.lstm != (ls != nullptr))
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_forward", "the LSTM head needs its recurrent state");
   const float* P = params;
   int rc0 = a3c_conv12_launch(L, P, prep, sa, B, act_l1, act_l2, s);
   if (rc0) return rc0;
   int rc = a3c_fc_fwd_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), P + L.off[T_FCB], act_l3, B, s,
                              P + L.off[T_FCW]);
   if (rc) return rc;
+  const float* head_in = act_l3;
+  if (ls) {   // C5: LSTM cell on the fc output, heads on its h
+    rc = a3c_lstm_fwd_launch(P + L.off[T_LW], P + L.off[T_LB], act_l3, *ls, B, s);
+    if (rc) return rc;
+    head_in = ls->h;
+  }
   const float* Wv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VW] : nullptr;
   const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
   if (sel.mode >= 0 && sel.env_on && sel.ring)
-    return a3c_head_screen_launch(L, P, act_l3, B, z, sel, s);
+    return a3c_head_screen_launch(L, P, head_in, B, z, sel, s);
   else
-    hipLaunchKernelGGL(k_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, act_l3, B,
+    hipLaunchKernelGGL(k_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, head_in, B,
                        P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel);
   A3C_CHECK(hipGetLastError());
   return 0;

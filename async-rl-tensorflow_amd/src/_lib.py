@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get('A3C_LIB') or os.path.join(os.path.dirname(_HERE), 'li
 A3C_ALGO_A3C = 0
 A3C_ALGO_Q = 1
 A3C_TRUNK_NIPS = 0
+A3C_LSTM_UNITS = 256
 MAX_TENSORS = 16
 
 c_int, c_i64, c_u64, c_float, c_double, c_void_p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint64,
@@ -26,7 +27,7 @@ c_int, c_i64, c_u64, c_float, c_double, c_void_p = (ctypes.c_int, ctypes.c_int64
 
 class NetDesc(ctypes.Structure):
     _fields_ = [('algo', c_int), ('trunk', c_int), ('action_size', c_int),
-                ('history_length', c_int), ('screen_h', c_int), ('screen_w', c_int)]
+                ('history_length', c_int), ('screen_h', c_int), ('screen_w', c_int), ('lstm_units', c_int)]
 
 
 class EngineConfig(ctypes.Structure):
@@ -49,7 +50,9 @@ class EngineBuffers(ctypes.Structure):
                 ('frame_pool', c_void_p), ('env_frame', c_void_p), ('env_lives', c_void_p),
                 ('env_episode', c_void_p), ('env_step', c_void_p), ('env_len', c_void_p),
                 ('zs', c_int), ('n_tensors', c_int), ('offsets', c_i64 * MAX_TENSORS),
-                ('sizes', c_i64 * MAX_TENSORS), ('sched', c_void_p)]
+                ('sizes', c_i64 * MAX_TENSORS), ('sched', c_void_p),
+                ('lstm_h', c_void_p), ('lstm_c', c_void_p), ('lstm_hp', c_void_p), ('lstm_cp', c_void_p),
+                ('lstm_gates', c_void_p), ('lstm_units', c_int)]
 
 
 # name -> (restype, argtypes)
@@ -87,6 +90,9 @@ SIGNATURES = {
     'a3c_matmul': (c_int, [c_void_p, c_i64, c_i64, c_void_p, c_i64, c_i64, c_void_p, c_i64, c_int, c_int, c_int,
                            c_void_p, c_int, c_int, c_void_p]),
     'a3c_copy_params': (c_int, [c_void_p, c_void_p, c_i64, c_void_p]),
+    'a3c_lstm_step': (c_int, [c_void_p] * 6 + [c_i64] + [c_void_p] * 6),
+    'a3c_lstm_workspace_bytes': (c_int, [c_int, c_i64, ctypes.POINTER(c_i64)]),
+    'a3c_lstm_bptt': (c_int, [c_void_p, c_int, c_i64] + [c_void_p] * 12),
     'a3c_env_create': (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_u64, c_int, ctypes.POINTER(c_void_p)]),
     'a3c_env_destroy': (c_int, [c_void_p]),
     'a3c_env_new_game': (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
@@ -156,8 +162,10 @@ def stream_handle(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-def net_desc(action_size, algo='a3c'):
-    return NetDesc(A3C_ALGO_A3C if algo == 'a3c' else A3C_ALGO_Q, A3C_TRUNK_NIPS, int(action_size), 4, 84, 84)
+def net_desc(action_size, algo='a3c', lstm=False):
+    """lstm: the C5 LSTM head (a3c only; build-defined, the reference has no recurrent code)."""
+    return NetDesc(A3C_ALGO_A3C if algo == 'a3c' else A3C_ALGO_Q, A3C_TRUNK_NIPS, int(action_size), 4, 84, 84,
+                   A3C_LSTM_UNITS if lstm else 0)
 
 
 def param_layout(desc):

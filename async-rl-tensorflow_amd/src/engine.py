@@ -43,11 +43,14 @@ def _view(ptr, shape, dtype):
 
 class Engine:
     def __init__(self, num_envs=256, n_step=5, action_size=6, algo='a3c', start_lives=0, num_frames=1024,
-                 seed=123, env_id_base=0, world_size=1, use_graph=True, overlap=False, **overrides):
+                 seed=123, env_id_base=0, world_size=1, use_graph=True, overlap=False, lstm=False, **overrides):
         _lib.require_device()
+        if lstm and algo != 'a3c':
+            raise ValueError('the LSTM head is an a3c head')
         cfg = _lib.EngineConfig()
         lib().a3c_engine_config_default(ctypes.byref(cfg))
-        cfg.net = _lib.net_desc(action_size, algo)
+        cfg.net = _lib.net_desc(action_size, algo, lstm)
+        self.lstm = bool(lstm)
         cfg.num_envs = int(num_envs)
         cfg.n_step = int(n_step)
         cfg.start_lives = int(start_lives)
@@ -102,7 +105,15 @@ class Engine:
         b = _lib.EngineBuffers()
         check(lib().a3c_engine_slot_buffers(self._h, k, ctypes.byref(b)), 'a3c_engine_slot_buffers')
         E, n = self.E, self.n
-        return dict(actions=_view(b.actions, (n, E), torch.int32),
+        lstm = {}
+        if self.lstm:
+            U = int(b.lstm_units)
+            lstm = dict(lstm_h=_view(b.lstm_h, (n, E, U), torch.float32),
+                        lstm_c=_view(b.lstm_c, (n, E, U), torch.float32),
+                        lstm_hp=_view(b.lstm_hp, (n, E, U), torch.float32),
+                        lstm_cp=_view(b.lstm_cp, (n, E, U), torch.float32),
+                        lstm_gates=_view(b.lstm_gates, (n, E, 4 * U), torch.float32))
+        return dict(**lstm, actions=_view(b.actions, (n, E), torch.int32),
                     rewards=_view(b.rewards, (n, E), torch.float32),
                     terminals=_view(b.terminals, (n, E), torch.uint8),
                     z=_view(b.z, (n + 1, E, self.zs), torch.float32),

@@ -78,8 +78,9 @@ def history_get(hist, nhwc=True):
     return out
 
 
-def param_names_shapes(action_size, algo='a3c'):
-    """TF variable names/shapes in flat order (agent.py:226-252 q-net, network.py:443-475 a3c)."""
+def param_names_shapes(action_size, algo='a3c', lstm=False):
+    """TF variable names/shapes in flat order (agent.py:226-252 q-net, network.py:443-475 a3c);
+    lstm: the C5 LSTM head's gate matrix and bias appended (include/a3c_hip.h layout)."""
     A = int(action_size)
     fc = 'l4' if algo == 'a3c' else 'l3'
     out = [('l1_w', (8, 8, 4, 16)), ('l1_b', (16,)), ('l2_w', (4, 4, 16, 32)), ('l2_b', (32,)),
@@ -88,7 +89,47 @@ def param_names_shapes(action_size, algo='a3c'):
         out += [('p_w', (FC, A)), ('p_b', (A,)), ('q_w', (FC, 1)), ('q_b', (1,))]
     else:
         out += [('q_w', (FC, A)), ('q_b', (A,))]
+    if lstm:
+        if algo != 'a3c':
+            raise ValueError('the LSTM head is an a3c head')
+        U = _lib.A3C_LSTM_UNITS
+        out += [('lstm_w', (FC + U, 4 * U)), ('lstm_b', (4 * U,))]
     return out
+
+
+def lstm_step(w, b, x, h_src, c_src, prev_terms=None, save=True):
+    """One C5 LSTM cell step (a3c_lstm_step) for B envs: x [B,256], (h_src, c_src) [B,U] the previous
+    step's outputs (zeroed where prev_terms [B] u8 is set).  Returns dict h, c (+ hp, cp, gates)."""
+    B, U = int(x.shape[0]), _lib.A3C_LSTM_UNITS
+    for t, nm in ((w, 'w'), (b, 'b'), (x, 'x'), (h_src, 'h_src'), (c_src, 'c_src')):
+        _dev(t, torch.float32, nm)
+    if prev_terms is not None:
+        _dev(prev_terms, torch.uint8, 'prev_terms')
+    new = lambda *s: torch.empty(s, dtype=torch.float32, device=x.device)  # noqa: E731
+    out = dict(h=new(B, U), c=new(B, U))
+    if save:
+        out.update(hp=new(B, U), cp=new(B, U), gates=new(B, 4 * U))
+    check(lib().a3c_lstm_step(ptr(w), ptr(b), ptr(x), ptr(h_src), ptr(c_src), ptr(prev_terms), B,
+                              ptr(out.get('hp')), ptr(out.get('cp')), ptr(out.get('gates')), ptr(out['h']),
+                              ptr(out['c']), stream_handle()), 'a3c_lstm_step')
+    return out
+
+
+def lstm_bptt(w, x, hp, cp, gates, c, terms, dh):
+    """Truncated BPTT (a3c_lstm_bptt) over [n,E,...] sequences; returns (dx masked by x > 0, dw, db)."""
+    n, E = int(terms.shape[0]), int(terms.shape[1])
+    for t, nm in ((w, 'w'), (x, 'x'), (hp, 'hp'), (cp, 'cp'), (gates, 'gates'), (c, 'c'), (dh, 'dh')):
+        _dev(t, torch.float32, nm)
+    _dev(terms, torch.uint8, 'terms')
+    nb = _lib.c_i64()
+    check(lib().a3c_lstm_workspace_bytes(n, E, ctypes.byref(nb)), 'a3c_lstm_workspace_bytes')
+    ws = torch.empty(int(nb.value), dtype=torch.uint8, device=x.device)
+    dx = torch.empty_like(x)
+    dw = torch.empty_like(w)
+    db = torch.empty(w.shape[-1], dtype=torch.float32, device=x.device)
+    check(lib().a3c_lstm_bptt(ptr(w), n, E, ptr(x), ptr(hp), ptr(cp), ptr(gates), ptr(c), ptr(terms), ptr(dh),
+                              ptr(dx), ptr(dw), ptr(db), ptr(ws), stream_handle()), 'a3c_lstm_bptt')
+    return dx, dw, db
 
 
 class Net:

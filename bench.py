@@ -45,6 +45,8 @@ def parse():
     ap.add_argument('--n-step', type=int, default=5)
     ap.add_argument('--game', default='Pong-v0', choices=sorted(GAMES))
     ap.add_argument('--algo', default='a3c', choices=['a3c', 'q'])
+    ap.add_argument('--lstm', action='store_true',
+                    help='C5 LSTM policy head (BASELINE config 5: SpaceInvaders-v0, 256-cell LSTM after the fc)')
     ap.add_argument('--frames', type=int, default=16384, help='HBM frame pool (16384 = 1.65 GB > L3)')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--update', default='overlap', choices=['overlap', 'sync', 'hogwild'],
@@ -112,10 +114,12 @@ def main():
     E, n = args.envs, args.n_step
     if args.algo == 'q' and args.update == 'overlap':
         args.update = 'sync'              # the stale-1 pipeline is an A3C (policy-gradient) mode
+    if args.lstm and args.algo != 'a3c':
+        raise SystemExit('--lstm is an a3c head')
     eng = Engine(num_envs=E, n_step=n, action_size=A, algo=args.algo, start_lives=lives, num_frames=args.frames,
                  seed=123, env_id_base=rank * E, world_size=world, use_graph=not args.no_graph,
-                 overlap=args.update == 'overlap')
-    ns = param_names_shapes(A, args.algo)
+                 overlap=args.update == 'overlap', lstm=args.lstm)
+    ns = param_names_shapes(A, args.algo, lstm=args.lstm)
     params = flatten_host(ns, eng.offsets, eng.params.numel(), init_params(ns, seed=123))
     eng.reset(params)     # every rank starts from the same parameters
     torch.cuda.synchronize()
@@ -208,8 +212,9 @@ def main():
             'data': f'synthetic: HBM-resident hashed RGB 210x160x3 frame pool ({args.frames} frames) stepped by '
                     f'the on-device synthetic Atari env; random-init NIPS A3C conv net',
             'config': {'workload': f'{args.game}, {E} envs batched per MI355X, n-step={n}, '
-                                   f'{"A3C" if args.algo == "a3c" else "one-step Q"} conv net (nips trunk)',
-                       'game': args.game, 'envs_per_gpu': E, 'n_step': n, 'action_size': A, 'algo': args.algo,
+                                   f'{"A3C" if args.algo == "a3c" else "one-step Q"} conv net (nips trunk'
+                                   f'{" + 256-cell LSTM head" if args.lstm else ""})',
+                       'game': args.game, 'head': 'lstm' if args.lstm else 'feed-forward', 'envs_per_gpu': E, 'n_step': n, 'action_size': A, 'algo': args.algo,
                        'env_steps_per_step': world * E * n,
                        'parallelism': (f'dp{world} hogwild: unlocked RMSProp pushes into {world} IPC-mapped HBM '
                                        f'shards over xGMI, pull at rollout start, no collective'

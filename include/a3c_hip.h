@@ -34,6 +34,8 @@ extern "C" {
 #define A3C_ALGO_Q 1            /* one-step Q-learning head (src/agent.py:251-254) */
 
 #define A3C_TRUNK_NIPS 0        /* 16/32/256 trunk: agent.py:226-251, network.py:439-448 */
+#define A3C_LSTM_UNITS 256      /* C5 LSTM head width (build-defined: the reference has no
+                                   recurrent code)                 */
 
 const char* a3c_version(void);
 const char* a3c_last_error(void);
@@ -47,6 +49,9 @@ int a3c_device_ok(void);
  * padding floats are zero and stay zero.
  *  a3c : l1_w[8,8,4,16] l1_b l2_w[4,4,16,32] l2_b l4_w[2592,256] l4_b p_w[256,A] p_b q_w[256,1] q_b
  *  q   : l1_w l1_b l2_w l2_b l3_w[2592,256] l3_b q_w[256,A] q_b
+ *  a3c + LSTM head (lstm_units = 256, BASELINE config 5): the a3c list, then
+ *        lstm_w[256+U, 4U] lstm_b[4U]   (TF1 BasicLSTMCell "Matrix"/"Bias", gate columns
+ *        i, j, f, o, forget_bias 1.0); the policy / value heads read the LSTM's h.
  * -------------------------------------------------------------------------- */
 typedef struct a3c_net_desc {
   int algo;            /* A3C_ALGO_*                                       */
@@ -55,6 +60,10 @@ typedef struct a3c_net_desc {
   int history_length;  /* 4 (config.py:22)                                 */
   int screen_h;        /* 84                                               */
   int screen_w;        /* 84                                               */
+  int lstm_units;      /* 0: feed-forward head; A3C_LSTM_UNITS: LSTM head (a3c only).  The
+                          batch-independent a3c_forward / a3c_loss_backward reject it (a
+                          recurrent head needs the sequence: a3c_lstm_step / a3c_lstm_bptt
+                          or the engine). */
 } a3c_net_desc;
 
 #define A3C_MAX_TENSORS 16
@@ -170,6 +179,26 @@ int a3c_conv2d_backward(const float* x, const float* w, const float* dy, float* 
                         int H, int W, int C, int KH, int KW, int SH, int SW, int OC, int nhwc, void* stream);
 int a3c_matmul(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn, float* C,
                int64_t ldc, int M, int N, int K, const float* bias, int relu, int accumulate, void* stream);
+
+/* ----------------------------------------------------------------------------
+ * C5  LSTM head (BASELINE config 5; no reference code -- build-defined after TF1
+ *     BasicLSTMCell, forget_bias 1.0, and the A3C-LSTM of assets/a3c.png's paper).
+ *  a3c_lstm_step: one cell step for B envs.  x [B][256] (fc ReLU output), h_src/c_src [B][U]
+ *    the previous step's outputs; prev_terms [B] (nullable): state zeroed where the previous
+ *    transition was terminal.  Writes h/c [B][U]; hp/cp (the masked inputs it used) and gates
+ *    ([B][4U], activated i, j, f, o) are nullable (only the backward needs them).
+ *  a3c_lstm_bptt: truncated BPTT over n steps of E envs (b = t*E + e), given dh [n*E][U] =
+ *    dL/dh_t from the heads.  dx [n*E][256] = dL/dx_t masked by x > 0 (the fc ReLU: ready for
+ *    the fc backward); dw [256+U][4U], db [4U] OVERWRITTEN.  terms [n][E] (transition t
+ *    terminal -> no gradient flows from step t+1 into step t's state).
+ * -------------------------------------------------------------------------- */
+int a3c_lstm_step(const float* w, const float* b, const float* x, const float* h_src, const float* c_src,
+                  const uint8_t* prev_terms, int64_t B, float* hp, float* cp, float* gates, float* h,
+                  float* c, void* stream);
+int a3c_lstm_workspace_bytes(int n, int64_t E, int64_t* bytes);
+int a3c_lstm_bptt(const float* w, int n, int64_t E, const float* x, const float* hp, const float* cp,
+                  const float* gates, const float* c, const uint8_t* terms, const float* dh, float* dx,
+                  float* dw, float* db, void* workspace, void* stream);
 
 /* K12  target sync (agent.py:342-344) / theta' <- theta (network.py:96-107). */
 int a3c_copy_params(float* dst, const float* src, int64_t n, void* stream);
@@ -291,6 +320,10 @@ typedef struct a3c_engine_buffers {
   uint32_t* env_len;
   int zs; int n_tensors; int64_t offsets[A3C_MAX_TENSORS]; int64_t sizes[A3C_MAX_TENSORS];
   float* sched;            /* device: [0] learning rate of the last gradient (agent.py:393-395) */
+  /* LSTM head (net.lstm_units > 0), per rollout step t: h_t, c_t [n][E][U]; the masked state
+   * inputs hp, cp [n][E][U]; activated gates [n][E][4U].  NULL without the LSTM head. */
+  float* lstm_h; float* lstm_c; float* lstm_hp; float* lstm_cp; float* lstm_gates;
+  int lstm_units;
 } a3c_engine_buffers;
 int a3c_engine_get_buffers(a3c_engine* eng, a3c_engine_buffers* out);
 /* same, with the rollout buffers (actions .. act_l3) of slot 0 or 1 (overlap: rollout k

@@ -24,7 +24,7 @@ class EngineRef:
                  gamma=0.99, beta=0.01, learning_rate=0.0007, max_step=80_000_000, decay=0.99,
                  momentum=0.0, epsilon=0.1, clip_norm=40.0, literal_adv=False, ep_start=1.0,
                  ep_end_t=4_000_000, learn_start=32, target_q_update_step=40_000, discount=0.99,
-                 dtype=np.float64):
+                 dtype=np.float64, lstm=False):
         self.algo, self.A, self.E, self.n = algo, int(action_size), int(num_envs), int(n_step)
         self.seed = int(seed)
         self.k0, self.k1 = px.seed_key(seed)
@@ -44,6 +44,13 @@ class EngineRef:
                       ep_start=ep_start, ep_end_t=ep_end_t, learn_start=learn_start,
                       target_q_update_step=target_q_update_step, discount=discount)
         self.dtype = dtype
+        # C5 LSTM head (ref_cpu.lstm_*): recurrent state carried across iterations, zeroed after a
+        # terminal transition
+        self.lstm = bool(lstm)
+        if self.lstm and algo != 'a3c':
+            raise ValueError('the LSTM head is an a3c head')
+        U = R.LSTM_UNITS
+        self.hc = (np.zeros((self.E, U), dtype), np.zeros((self.E, U), dtype))
         x0 = px.philox4x32(self.ids, 0, 0, 11, self.k0, self.k1)[0]
         self.ep_end = EP_END_CHOICES[x0 % 3]
         self._screens = {}
@@ -65,6 +72,19 @@ class EngineRef:
             for c in range(4):
                 self.ring[e, c % self.R] = s
         self.tau, self.global_step = 3, 0
+        if self.lstm:
+            self.hc = (np.zeros_like(self.hc[0]), np.zeros_like(self.hc[1]))
+
+    def _step_z(self, st, carry):
+        """per-step forward: z [E, zs] (and the LSTM head's new state when lstm)."""
+        if not self.lstm:
+            return R.forward(self.params, st, self.algo, dtype=self.dtype, keep=False)['z'], None
+        P, dt = self.params, self.dtype
+        h3 = R.forward(P, st, 'a3c', dtype=dt, keep=False)['h3']
+        h, c, _ = R.lstm_cell(h3, carry[0], carry[1], P['lstm_w'], P['lstm_b'])
+        z = np.concatenate([h @ P['p_w'].astype(dt) + P['p_b'].astype(dt),
+                            h @ P['q_w'].astype(dt) + P['q_b'].astype(dt)], axis=1)
+        return z, (h, c)
 
     def states(self, tau):
         """[E,84,84,4] NHWC u8 state s_tau (frames tau-3..tau)."""
@@ -99,9 +119,10 @@ class EngineRef:
         rewards = np.zeros((n, E), np.float32)
         terms = np.zeros((n, E), np.uint8)
         zs, pis, frames = [], [], []
+        h0c0 = self.hc
         for t in range(n):
             st = self.states(self.tau + t)
-            z = R.forward(self.params, st, self.algo, dtype=self.dtype, keep=False)['z']
+            z, hc = self._step_z(st, self.hc)
             a, pi = self._draw(z, t)
             sampled[t] = a
             acts[t] = a if forced_actions is None else forced_actions[t]
@@ -110,6 +131,9 @@ class EngineRef:
             frame, reward, term = self.env.act(acts[t], is_training=True)
             rewards[t] = np.clip(reward, -1.0, 1.0)                      # agent.py:154
             terms[t] = term
+            if self.lstm:
+                keep = (1.0 - term.astype(np.float64))[:, None].astype(self.dtype)
+                self.hc = (hc[0] * keep, hc[1] * keep)
             frames.append(frame.copy())
             for e in range(E):
                 self.ring[e, (self.tau + t + 1) % self.R] = self.screen_of(frame[e])
@@ -120,7 +144,7 @@ class EngineRef:
         out = dict(actions=acts, sampled=sampled, rewards=rewards, terminals=terms, z=np.stack(zs),
                    pi=pis, frames=np.stack(frames))
         if self.algo == 'a3c':
-            zb = R.forward(self.params, self.states(self.tau + n), 'a3c', dtype=self.dtype, keep=False)['z']
+            zb, _ = self._step_z(self.states(self.tau + n), self.hc)
             Rt = R.nstep_returns(rewards, terms, zb[:, A].astype(np.float32), h['gamma'])
             target = Rt.astype(np.float32)
             out['bootstrap_z'] = zb
@@ -130,7 +154,11 @@ class EngineRef:
             target = R.td_target(rewards.reshape(-1), terms.reshape(-1), qn.astype(np.float32),
                                  h['discount']).astype(np.float32)
         out['target'] = target.reshape(n, E)
-        fwd = R.forward(self.params, states, self.algo, dtype=self.dtype)
+        if self.lstm:
+            fwd = R.lstm_a3c_forward(self.params, states, n, h0c0[0], h0c0[1], terms, dtype=self.dtype)
+            out['lstm'] = fwd['lstm']
+        else:
+            fwd = R.forward(self.params, states, self.algo, dtype=self.dtype)
         flat_acts = acts.reshape(-1)
         if self.algo == 'a3c':
             losses, dz = R.a3c_loss_and_dz(fwd['z'], flat_acts, target.reshape(-1).astype(self.dtype),
@@ -138,7 +166,10 @@ class EngineRef:
         else:
             loss, dz = R.q_loss_and_dz(fwd['z'], flat_acts, target.reshape(-1).astype(self.dtype))
             losses = dict(loss=loss, q_mean=fwd['z'][np.arange(B), flat_acts].mean())
-        g = R.backward(self.params, fwd, dz, self.algo)
+        if self.lstm:
+            g = R.lstm_a3c_backward(self.params, fwd, dz, terms)
+        else:
+            g = R.backward(self.params, fwd, dz, self.algo)
         grads = {k: np.asarray(v, np.float32).reshape(self.params[k].shape) for k, v in g.items()}
         sumsq = {k: np.float32(np.sum(v.astype(np.float64) ** 2)) for k, v in grads.items()}
         clipped = {k: R.clip_by_norm(v, h['clip_norm']) for k, v in grads.items()}

@@ -154,7 +154,7 @@ def trunk_spec(dqn_type='nips', history_length=4, h=84, w=84):
     return layers, hh * ww * cin, spec['fc']
 
 
-def param_shapes(action_size, algo='a3c', dqn_type='nips', history_length=4):
+def param_shapes(action_size, algo='a3c', dqn_type='nips', history_length=4, lstm=False):
     """TF variable order/shapes (ops.py:21-24 conv ``w`` [kh,kw,cin,cout] + ``biases``;
     ops.py:36-39 linear ``Matrix`` [in,out] + ``bias``).  a3c: network.py names
     (l*_w/l*_b, p_w/p_b policy, q_w/q_b value); q: agent.py names (l*_w/l*_b, q_w/q_b)."""
@@ -171,6 +171,8 @@ def param_shapes(action_size, algo='a3c', dqn_type='nips', history_length=4):
                    ('q_w', (fc, 1)), ('q_b', (1,))]
     else:
         shapes += [('q_w', (fc, action_size)), ('q_b', (action_size,))]
+    if lstm:
+        shapes += lstm_param_shapes(LSTM_UNITS, fc)
     return shapes
 
 
@@ -351,6 +353,14 @@ def backward(params, fwd, dz, algo='a3c', dqn_type='nips'):
         g['q_b'] = dz.sum(0)
         dh3 = dz @ params['q_w'].astype(dtype).T
     dh3 = dh3 * (h3 > 0)
+    return trunk_backward(params, fwd, dh3, g, algo, dqn_type)
+
+
+def trunk_backward(params, fwd, dh3, g, algo='a3c', dqn_type='nips'):
+    """Reverse pass from dL/d(fc pre-ReLU-masked output) ``dh3`` down through fc, conv2, conv1
+    (shared by the feed-forward head and the LSTM head); fills and returns ``g``."""
+    convs, flat, fc = trunk_spec(dqn_type)
+    dtype = fwd['z'].dtype
     fcname = 'l4' if algo == 'a3c' else 'l3'
     g[f'{fcname}_w'] = fwd['flat'].T @ dh3
     g[f'{fcname}_b'] = dh3.sum(0)
@@ -410,3 +420,124 @@ def learning_rate(step, max_step=80_000_000, learning_rate=0.0007):
 def epsilon_schedule(step, ep_start=1., ep_end=0.1, ep_end_t=4_000_000, learn_start=32):
     """agent.py:142-144."""
     return ep_end + max(0., (ep_start - ep_end) * (ep_end_t - max(0., step - learn_start)) / ep_end_t)
+
+
+# --------------------------------------------------------------------------------------
+# C5  LSTM policy head (BASELINE config 5).  The reference has NO recurrent code (SURVEY §8(f)
+# rank 4): this is a build-defined head, restated from TF1's ``BasicLSTMCell`` (tf.nn.rnn_cell,
+# state_is_tuple, forget_bias=1.0; third-party, not in the reference) and the A3C-LSTM of the
+# paper the reference implements (assets/a3c.png; Mnih et al. 2016: one 256-cell LSTM after
+# the last hidden layer).  Parity unpinned against any reference execution; cross-checked
+# against torch CPU autograd (tests/test_oracle_autograd.py).
+#   gates a = [x, h_prev] @ W + b, W [256+U, 4U], columns (i, j, f, o)
+#   c = c_prev * sigmoid(f + forget_bias) + sigmoid(i) * tanh(j);  h = tanh(c) * sigmoid(o)
+# The recurrent state carried from step t to t+1 is zeroed when transition t was terminal
+# (h_prev = h_t * (1 - term_t)).  Truncated BPTT over the n-step rollout: no gradient into the
+# rollout's initial state.
+# --------------------------------------------------------------------------------------
+LSTM_UNITS = 256
+FORGET_BIAS = 1.0
+
+
+def lstm_param_shapes(units=LSTM_UNITS, fc=256):
+    """flat order: appended after the a3c head (build-defined)."""
+    return [('lstm_w', (fc + units, 4 * units)), ('lstm_b', (4 * units,))]
+
+
+def _sigmoid(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def lstm_cell(x, h, c, W, b, forget_bias=FORGET_BIAS):
+    """One BasicLSTMCell step; returns (h', c', gates) with gates = activated (i, j, f, o)."""
+    dtype = x.dtype
+    a = np.concatenate([x, h], axis=1) @ W.astype(dtype) + b.astype(dtype)
+    U = h.shape[1]
+    si = _sigmoid(a[:, :U])
+    tj = np.tanh(a[:, U:2 * U])
+    sf = _sigmoid(a[:, 2 * U:3 * U] + forget_bias)
+    so = _sigmoid(a[:, 3 * U:])
+    c2 = c * sf + si * tj
+    h2 = np.tanh(c2) * so
+    return h2, c2, np.concatenate([si, tj, sf, so], axis=1)
+
+
+def lstm_forward_seq(params, x_seq, h0, c0, terms):
+    """x_seq [n,E,256] (the fc ReLU outputs), (h0, c0) [E,U] the already-masked carry-in,
+    terms [n,E].  Returns dict H, C (cell outputs per step), HP, CP (masked inputs per step),
+    G (activated gates) and the carry-out (h, c) after masking by terms[n-1]."""
+    n = x_seq.shape[0]
+    W, b = params['lstm_w'], params['lstm_b']
+    hp, cp = h0, c0
+    H, C, HP, CP, G = [], [], [], [], []
+    for t in range(n):
+        HP.append(hp)
+        CP.append(cp)
+        h, c, g = lstm_cell(x_seq[t], hp, cp, W, b)
+        H.append(h)
+        C.append(c)
+        G.append(g)
+        keep = (1.0 - np.asarray(terms[t], np.float64))[:, None].astype(h.dtype)
+        hp, cp = h * keep, c * keep
+    return dict(H=np.stack(H), C=np.stack(C), HP=np.stack(HP), CP=np.stack(CP), G=np.stack(G),
+                carry=(hp, cp))
+
+
+def lstm_backward_seq(params, seq, x_seq, dH, terms):
+    """Truncated BPTT of ``lstm_forward_seq``: dH [n,E,U] = dL/dh_t from the heads.  Returns
+    (dX [n,E,256], dW, db)."""
+    n, E, U = dH.shape
+    W = params['lstm_w'].astype(dH.dtype)
+    G, C, CP, HP = seq['G'], seq['C'], seq['CP'], seq['HP']
+    dX = np.zeros(x_seq.shape, dH.dtype)
+    dW = np.zeros(W.shape, dH.dtype)
+    db = np.zeros(W.shape[1], dH.dtype)
+    dh_next = np.zeros((E, U), dH.dtype)    # dL/d(masked h input of step t+1)
+    dc_next = np.zeros((E, U), dH.dtype)
+    for t in range(n - 1, -1, -1):
+        keep = (1.0 - np.asarray(terms[t], np.float64))[:, None].astype(dH.dtype)
+        dh = dH[t] + dh_next * keep
+        i, j, f, o = (G[t][:, k * U:(k + 1) * U] for k in range(4))
+        tc = np.tanh(C[t])
+        dc = dc_next * keep + dh * o * (1.0 - tc * tc)
+        da = np.concatenate([dc * j * i * (1.0 - i), dc * i * (1.0 - j * j),
+                             dc * CP[t] * f * (1.0 - f), dh * tc * o * (1.0 - o)], axis=1)
+        xh = np.concatenate([x_seq[t], HP[t]], axis=1)
+        dW += xh.T @ da
+        db += da.sum(0)
+        dxh = da @ W.T
+        dX[t] = dxh[:, :x_seq.shape[2]]
+        dh_next = dxh[:, x_seq.shape[2]:]
+        dc_next = dc * f
+    return dX, dW, db
+
+
+def lstm_a3c_forward(params, states_u8, n, h0, c0, terms, dtype=np.float64):
+    """Trunk over the n*E states (b = t*E + e), the LSTM over the n steps, and the policy /
+    value heads on h_t.  Returns the trunk dict of ``forward`` with z replaced by the LSTM
+    head's z, plus 'lstm' (the sequence) and 'x_seq'."""
+    fwd = forward(params, states_u8, 'a3c', dtype=dtype)
+    E = states_u8.shape[0] // n
+    x_seq = fwd['h3'].reshape(n, E, -1)
+    seq = lstm_forward_seq(params, x_seq, h0.astype(dtype), c0.astype(dtype), terms)
+    Hf = seq['H'].reshape(n * E, -1)
+    logits = Hf @ params['p_w'].astype(dtype) + params['p_b'].astype(dtype)
+    value = Hf @ params['q_w'].astype(dtype) + params['q_b'].astype(dtype)
+    fwd['z'] = np.concatenate([logits, value], axis=1)
+    fwd['lstm'] = seq
+    fwd['x_seq'] = x_seq
+    return fwd
+
+
+def lstm_a3c_backward(params, fwd, dz, terms):
+    """Heads on h_t, BPTT through the LSTM, then the ReLU-masked fc/conv trunk."""
+    dtype = fwd['z'].dtype
+    seq, x_seq = fwd['lstm'], fwd['x_seq']
+    n, E, U = seq['H'].shape
+    A = dz.shape[1] - 1
+    Hf = seq['H'].reshape(n * E, U)
+    g = {'p_w': Hf.T @ dz[:, :A], 'p_b': dz[:, :A].sum(0), 'q_w': Hf.T @ dz[:, A:], 'q_b': dz[:, A:].sum(0)}
+    dH = dz[:, :A] @ params['p_w'].astype(dtype).T + dz[:, A:] @ params['q_w'].astype(dtype).T
+    dX, g['lstm_w'], g['lstm_b'] = lstm_backward_seq(params, seq, x_seq, dH.reshape(n, E, U), terms)
+    dh3 = dX.reshape(n * E, -1) * (fwd['h3'] > 0)
+    return trunk_backward(params, fwd, dh3, g, 'a3c')

@@ -83,3 +83,61 @@ def test_rmsprop_differs_from_torch_default_as_documented():
     assert not np.isclose(w[0], tw.item(), rtol=1e-3)
     exp = 0.5 - 0.1 * 2.0 / np.sqrt(1.0 + (4.0 - 1.0) * 0.01 + 0.1)
     assert np.isclose(w[0], exp, rtol=1e-6)
+
+
+def test_lstm_oracle_matches_torch_autograd():
+    """C5 LSTM head (build-defined, no reference code): the oracle's hand-written truncated BPTT
+    (ref_cpu.lstm_a3c_backward) against torch autograd in float64 over an n-step sequence with
+    in-rollout terminals (state zeroed after a terminal transition) and a nonzero carry-in."""
+    rng = np.random.default_rng(5)
+    n, E, A, U = 4, 3, 6, R.LSTM_UNITS
+    p = R.init_params(R.param_shapes(A, 'a3c', lstm=True), seed=9, stddev=0.05)
+    for k in p:
+        if k.endswith('_b'):
+            p[k] = (rng.standard_normal(p[k].shape) * 0.05).astype(np.float32)
+    states = rng.integers(0, 256, (n * E, 84, 84, 4), dtype=np.uint8)
+    terms = np.zeros((n, E), np.uint8)
+    terms[1, 0] = 1
+    terms[2, 2] = 1
+    h0 = rng.standard_normal((E, U)) * 0.3
+    c0 = rng.standard_normal((E, U)) * 0.3
+    actions = rng.integers(0, A, n * E)
+    target = rng.standard_normal(n * E)
+    fwd = R.lstm_a3c_forward(p, states, n, h0, c0, terms)
+    losses, dz = R.a3c_loss_and_dz(fwd['z'], actions, target, 0.01)
+    g = R.lstm_a3c_backward(p, fwd, dz, terms)
+
+    T, _ = torch_forward({k: v for k, v in p.items() if not k.startswith('lstm')}, states, 'a3c')
+    for k in ('lstm_w', 'lstm_b'):
+        T[k] = torch.as_tensor(p[k], dtype=torch.float64).requires_grad_(True)
+    # recompute the trunk from the same leaves (torch_forward's z used h3 directly)
+    x = torch.as_tensor(states, dtype=torch.float64).permute(0, 3, 1, 2) / 255.0
+    h = F.relu(F.conv2d(x, T['l1_w'].permute(3, 2, 0, 1), T['l1_b'], stride=4))
+    h = F.relu(F.conv2d(h, T['l2_w'].permute(3, 2, 0, 1), T['l2_b'], stride=2))
+    h3 = F.relu(h.permute(0, 2, 3, 1).reshape(n * E, -1) @ T['l4_w'] + T['l4_b']).reshape(n, E, -1)
+    hp, cp = torch.as_tensor(h0), torch.as_tensor(c0)
+    hs = []
+    for t in range(n):
+        a = torch.cat([h3[t], hp], 1) @ T['lstm_w'] + T['lstm_b']
+        i, j, f, o = a.split(U, dim=1)
+        c = cp * torch.sigmoid(f + 1.0) + torch.sigmoid(i) * torch.tanh(j)
+        hh = torch.tanh(c) * torch.sigmoid(o)
+        hs.append(hh)
+        keep = torch.as_tensor(1.0 - terms[t].astype(np.float64))[:, None]
+        hp, cp = hh * keep, c * keep
+    H = torch.cat(hs, 0)
+    z = torch.cat([H @ T['p_w'] + T['p_b'], H @ T['q_w'] + T['q_b']], dim=1)
+    np.testing.assert_allclose(z.detach().numpy(), fwd['z'], rtol=1e-10, atol=1e-12)
+    logpi = F.log_softmax(z[:, :A], dim=1)
+    pi = logpi.exp()
+    Hent = -(pi * logpi).sum(1)
+    adv = torch.as_tensor(target) - z[:, A]
+    lp_a = logpi[torch.arange(n * E), torch.as_tensor(actions)]
+    loss = (-(lp_a * adv.detach()) - 0.01 * Hent + 0.5 * adv * adv).sum()
+    assert np.isclose(loss.item(), losses['total'], rtol=1e-12)
+    loss.backward()
+    for k in p:
+        np.testing.assert_allclose(np.asarray(g[k]).reshape(p[k].shape), T[k].grad.numpy(), rtol=1e-9,
+                                   atol=1e-12, err_msg=k)
+    carry = fwd['lstm']['carry']
+    np.testing.assert_allclose(carry[0], hp.detach().numpy(), rtol=1e-12, atol=1e-14)
