@@ -3,7 +3,7 @@
 // clip, then (after the host's optional RCCL all-reduce of the clipped gradients) RMSProp apply.
 //
 // Reference loop it replaces (per worker): agent.py:52-67 train -> predict (:141-151) ->
-// env.act (environment.py:124-142) -> observe (:153-167) -> batch_update (:169-207) with the
+// env.act (environment.py:78-96) -> observe (:153-167) -> batch_update (:169-207) with the
 // shared RMSProp apply on the parameter server (main.py:60-66).  A3C (network.py + assets/a3c.png)
 // uses n-step returns instead of the TD target; algo Q keeps agent.py's target network.
 //
@@ -281,7 +281,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   e->envp.random_start = cfg->random_start;
   e->envp.action_repeat = cfg->action_repeat;
   e->envp.env_id_base = cfg->env_id_base;
-  // per-env final epsilon (main.py:369 samples ep_end per worker from {0.1, 0.01, 0.5})
+  // per-env final epsilon (main.py:68 samples ep_end per worker from {0.1, 0.01, 0.5})
   std::vector<float> ee(E);
   static const float choices[3] = {0.1f, 0.01f, 0.5f};
   for (int64_t i = 0; i < E; ++i) {

@@ -1,8 +1,8 @@
 // Batched synthetic Atari stand-in on device (gym/ALE is absent; SURVEY §2 OUT OF SCOPE) with the
 // reference's interface semantics, bit-identical to oracle/synthetic_env.py:
-//   new_game          environment.py:74-79
-//   new_random_game   environment.py:81-86
-//   act               environment.py:124-142 (action repeat, life-loss terminal when training)
+//   new_game          environment.py:28-33
+//   new_random_game   environment.py:35-40
+//   act               environment.py:78-96 (action repeat, life-loss terminal when training)
 //   observe clip      agent.py:154
 // k_env_step fuses one env step with K1 (Environment.screen) and the K2 history push: the new
 // 84x84 screen is written straight into the env's frame-ring slot, so the "shift" of
@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(256) k_env_init_screens(EnvBufs b, int E, cons
 }
 
 // screen of env e's post-act frame (written by the fused head+act kernel) into ring slot
-// (tau + t + 1) mod R: Environment.screen (environment.py:95-99) + History.add (history.py:13-15).
+// (tau + t + 1) mod R: Environment.screen (environment.py:49-53) + History.add (history.py:13-15).
 // grid (bands, E): one output band per workgroup.
 template <int ROWS>
 __global__ void __launch_bounds__(256) k_env_screen(int E, const int32_t* __restrict__ frames,

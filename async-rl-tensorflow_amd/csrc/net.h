@@ -1,4 +1,4 @@
-// NIPS trunk geometry (agent.py:226-252, network.py:439-448) and the flat parameter layout.
+// NIPS trunk geometry (agent.py:226-252, network.py:43-52) and the flat parameter layout.
 #pragma once
 #include "a3c_common.h"
 #include "../../include/a3c_hip.h"

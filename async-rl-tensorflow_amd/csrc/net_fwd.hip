@@ -10,7 +10,7 @@
 //                 conv2 (4x4/2, 16->32, K = 256) reads it back as 16-byte fragments, W2 in
 //                 registers, and writes the (h,w,c)-flattened l2 (agent.py:231-232).
 //  fc layer     : gemm.hip (M = B, N = 256, K = 2592, split-K, bias+relu epilogue).
-//  k_head_fwd   : one wave per state: logits/value (network.py:458,475) or q (agent.py:252),
+//  k_head_fwd   : one wave per state: logits/value (network.py:62,475) or q (agent.py:252),
 //                 then the action draw (softmax sample / epsilon-greedy argmax).
 #include "net.h"
 #include "lstm.h"
@@ -576,7 +576,7 @@ void a3c_conv12_set_smem() {
 }
 
 // ---------------------------------------------------------------------------------------
-// fc layer of the rollout (agent.py:251 / network.py:447): l3 = relu(l2 @ W + b) for a
+// fc layer of the rollout (agent.py:251 / network.py:51-52): l3 = relu(l2 @ W + b) for a
 // skinny batch (M = E states, N = 256, K = 2592).  One workgroup per 16x16 output tile; the
 // 4 waves split the 162 K-chunks of 16 and meet in LDS.  Per chunk a lane loads one 16-byte A
 // fragment (4 consecutive k of its row) and one 16-byte B fragment from the fragment-packed

@@ -33,7 +33,7 @@ static void launch_atari(const uint8_t* rgb, const int32_t* idx, int64_t n, uint
                      atari::Smem<ROWS>::BYTES, s, rgb, idx, out, stride);
 }
 
-// luminance step of Environment.screen alone (environment.py:97-98), the exact integer form the
+// luminance step of Environment.screen alone (environment.py:51-52), the exact integer form the
 // Atari kernel uses: out[i] = truncated fp64 0.2126 R + 0.7152 G + 0.0722 B of pixel i
 // (groups of 4 pixels through atari::lum4 when the buffers are 4-byte aligned, else per pixel).
 __global__ void k_luminance(const uint8_t* __restrict__ rgb, int64_t npix, uint8_t* __restrict__ out) {

@@ -1,4 +1,4 @@
-// K1: Environment.screen (reference src/environment.py:95-99) as a block-cooperative
+// K1: Environment.screen (reference src/environment.py:49-53) as a block-cooperative
 // device routine: fp64 luminance with u8 truncation, then Pillow's two-pass BILINEAR
 // fixed-point resample (what scipy<1.3 imresize runs, environment.py:5-8,99).
 // Bit-exact against tests/golden/screen_golden.npz (generated from the reference).

@@ -166,7 +166,7 @@ class GymEnvironment(Environment):
   def __init__(self, config):
     super(GymEnvironment, self).__init__(config)
 
-  def act(self, action, is_training=True):       # environment.py:124-142
+  def act(self, action, is_training=True):       # environment.py:78-96
     self.env.act([int(action)], is_training=is_training)
     self._sync()
     self.after_act(action)
@@ -177,7 +177,7 @@ class SimpleGymEnvironment(Environment):
   def __init__(self, config):
     super(SimpleGymEnvironment, self).__init__(config)
 
-  def act(self, action, is_training=True):       # environment.py:148-152
+  def act(self, action, is_training=True):       # environment.py:102-106
     self.env.act([int(action)], is_training=is_training, simple=True)
     self._sync()
     self.after_act(action)

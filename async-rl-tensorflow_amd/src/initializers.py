@@ -1,11 +1,11 @@
 """Parameter initialisers of the reference (host side, numpy).
 
-* conv weights: ``tf.truncated_normal_initializer(0, 0.02)`` (agent.py:214, network.py:406,
+* conv weights: ``tf.truncated_normal_initializer(0, 0.02)`` (agent.py:214, network.py:10,
   passed to ops.conv2d ops.py:21) -- re-draw outside 2 sigma;
 * linear ``Matrix``: ``tf.random_normal_initializer(stddev=0.02)`` (ops.py:36-37);
 * biases: ``tf.constant_initializer(0.0)`` / ``bias_start`` (ops.py:24,38-39).
 TF's own op RNG is not reproducible outside TF, so draws come from numpy's PCG64 seeded by
-``random_seed`` (main.py:336).
+``random_seed`` (main.py:35).
 """
 import numpy as np
 

@@ -29,7 +29,7 @@ def _dev(t, dtype, name):
 
 
 def preprocess(rgb, frame_idx=None, out_hw=(IMG, IMG), out=None):
-    """Environment.screen (environment.py:95-99) for frames rgb [N,H,W,3] u8 (or a frame pool
+    """Environment.screen (environment.py:49-53) for frames rgb [N,H,W,3] u8 (or a frame pool
     indexed by ``frame_idx`` [n] int32).  Returns [n,oh,ow] u8, bit-exact to the reference."""
     _dev(rgb, torch.uint8, 'rgb')
     if rgb.dim() == 3:
@@ -47,7 +47,7 @@ def preprocess(rgb, frame_idx=None, out_hw=(IMG, IMG), out=None):
 
 
 def luminance(rgb):
-    """environment.py:97-98 alone: [...,3] u8 -> [...] u8 (exact integer form of the fp64 sum)."""
+    """environment.py:51-52 alone: [...,3] u8 -> [...] u8 (exact integer form of the fp64 sum)."""
     _dev(rgb, torch.uint8, 'rgb')
     out = torch.empty(rgb.shape[:-1], dtype=torch.uint8, device=rgb.device)
     check(lib().a3c_luminance_u8(ptr(rgb), out.numel(), ptr(out), stream_handle()), 'a3c_luminance_u8')
@@ -79,7 +79,7 @@ def history_get(hist, nhwc=True):
 
 
 def param_names_shapes(action_size, algo='a3c', lstm=False):
-    """TF variable names/shapes in flat order (agent.py:226-252 q-net, network.py:443-475 a3c);
+    """TF variable names/shapes in flat order (agent.py:226-252 q-net, network.py:47-79 a3c);
     lstm: the C5 LSTM head's gate matrix and bias appended (include/a3c_hip.h layout)."""
     A = int(action_size)
     fc = 'l4' if algo == 'a3c' else 'l3'
@@ -170,7 +170,7 @@ class Net:
         nbytes = _lib.workspace_bytes(self.desc, max(int(B), 1))
         return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
-    # -- forward (agent.py:217-254 / network.py:439-479) --------------------------------
+    # -- forward (agent.py:217-254 / network.py:43-79) --------------------------------
     def forward(self, params, states, save_l1=True, workspace=None):
         """states [B,4,84,84] u8 (oldest frame first).  Returns dict z/l1/l2/l3."""
         _dev(params, torch.float32, 'params')
@@ -225,7 +225,7 @@ class Net:
 
 
 def select_action(mode, z, A, seed, tau, eps=None, env_ids=None):
-    """mode 0 categorical (network.py:461-468), 1 epsilon-greedy (agent.py:141-151)."""
+    """mode 0 categorical (network.py:65-72), 1 epsilon-greedy (agent.py:141-151)."""
     _dev(z, torch.float32, 'z')
     B, zs = int(z.shape[0]), int(z.shape[1])
     actions = torch.empty(B, dtype=torch.int32, device=z.device)

@@ -4,7 +4,7 @@
 kernels.  Variables use TF's layouts: conv ``w`` [kh,kw,cin,cout] + ``biases`` (ops.py:16-24),
 linear ``Matrix`` [in,out] + ``bias`` (ops.py:36-39).
 
-Initialisers mirror the TF ones the reference passes (agent.py:214, network.py:406, ops.py:8,37).
+Initialisers mirror the TF ones the reference passes (agent.py:214, network.py:10, ops.py:8,37).
 """
 import math
 

@@ -30,10 +30,10 @@ extern "C" {
 #define A3C_ERR_INVALID 10001   /* bad argument / unsupported shape            */
 #define A3C_ERR_STATE 10002     /* engine used in the wrong order               */
 
-#define A3C_ALGO_A3C 0          /* policy + value heads (src/network.py:456-490) */
+#define A3C_ALGO_A3C 0          /* policy + value heads (src/network.py:60-94) */
 #define A3C_ALGO_Q 1            /* one-step Q-learning head (src/agent.py:251-254) */
 
-#define A3C_TRUNK_NIPS 0        /* 16/32/256 trunk: agent.py:226-251, network.py:439-448 */
+#define A3C_TRUNK_NIPS 0        /* 16/32/256 trunk: agent.py:226-251, network.py:43-52 */
 #define A3C_LSTM_UNITS 256      /* C5 LSTM head width (build-defined: the reference has no
                                    recurrent code)                 */
 
@@ -45,7 +45,7 @@ int a3c_device_ok(void);
 /* ----------------------------------------------------------------------------
  * Network description and flat parameter layout.
  * Flat fp32 vector in TF variable order (ops.py:21,24,36,38; agent.py:226-252 /
- * network.py:443-475); each tensor starts at a 64-float (256 B) aligned offset,
+ * network.py:47-79); each tensor starts at a 64-float (256 B) aligned offset,
  * padding floats are zero and stay zero.
  *  a3c : l1_w[8,8,4,16] l1_b l2_w[4,4,16,32] l2_b l4_w[2592,256] l4_b p_w[256,A] p_b q_w[256,1] q_b
  *  q   : l1_w l1_b l2_w l2_b l3_w[2592,256] l3_b q_w[256,A] q_b
@@ -74,7 +74,7 @@ int a3c_param_layout(const a3c_net_desc* net, int* n_tensors, int64_t* offsets, 
 int a3c_workspace_bytes(const a3c_net_desc* net, int64_t B, int64_t* bytes);
 
 /* ----------------------------------------------------------------------------
- * K1  Environment.screen (environment.py:95-99): fp64 luminance truncated to u8, then
+ * K1  Environment.screen (environment.py:49-53): fp64 luminance truncated to u8, then
  *     Pillow BILINEAR fixed-point resample (scipy.misc.imresize, environment.py:5-8).
  *     rgb frames [*, in_h, in_w, 3] u8; frame i reads rgb + (frame_idx ? frame_idx[i] : i)
  *     * in_h*in_w*3 and writes out + i*out_stride ([out_h][out_w] u8).  Bit-exact.
@@ -82,7 +82,7 @@ int a3c_workspace_bytes(const a3c_net_desc* net, int64_t B, int64_t* bytes);
 int a3c_preprocess_u8(const uint8_t* rgb, const int32_t* frame_idx, int64_t n, int in_h, int in_w,
                       uint8_t* out, int64_t out_stride, int out_h, int out_w, void* stream);
 
-/* luminance step alone (environment.py:97-98): out[i] = uint8(fp64 0.2126R+0.7152G+0.0722B)
+/* luminance step alone (environment.py:51-52): out[i] = uint8(fp64 0.2126R+0.7152G+0.0722B)
  * for npix RGB pixels, in the exact integer form the Atari screen kernel uses. */
 int a3c_luminance_u8(const uint8_t* rgb, int64_t npix, uint8_t* out, void* stream);
 
@@ -98,7 +98,7 @@ int a3c_history_get_f32(const uint8_t* hist, int64_t n, int L, int h, int w, int
                         void* stream);
 
 /* ----------------------------------------------------------------------------
- * Forward (agent.py:217-254 q-net / network.py:439-479 a3c net, ops.py:4-46).
+ * Forward (agent.py:217-254 q-net / network.py:43-79 a3c net, ops.py:4-46).
  *  states  [B][L][84][84] u8 (frame values; the /255 of agent.py:226 is applied inside)
  *  act_l1  [B][400][16]  f32 conv1 out (nullable: only needed for a3c_loss_backward)
  *  act_l2  [B][2592]     f32 conv2 out, (h,w,c) flatten order (agent.py:231-232)
@@ -113,7 +113,7 @@ int a3c_forward(const a3c_net_desc* net, const float* params, const uint8_t* sta
 
 /* ----------------------------------------------------------------------------
  * K6  action selection.
- *  mode 0 (a3c, network.py:461-468 softmax + batch_sample): categorical draw
+ *  mode 0 (a3c, network.py:65-72 softmax + batch_sample): categorical draw
  *        u = philox(seed; tau, env_ids[i], P_ACTION); first j with fp32 cumsum(pi)[j] > u.
  *  mode 1 (q, agent.py:141-151): if u01(x0) < eps[i]: x1 % A  else argmax_j q[j]
  *        (first maximum, tf.argmax agent.py:254).
@@ -226,7 +226,7 @@ int a3c_rmsprop_range(float* w, float* ms, float* mom, const float* grads, int64
 /* ----------------------------------------------------------------------------
  * Batched synthetic Atari env (gym/ALE is absent): the Environment / GymEnvironment interface
  * of environment.py:14-106 for E envs on device (dynamics: oracle/synthetic_env.py).
- *  new_game(random=0): environment.py:74-79; random=1: new_random_game :81-86 (mask nullable)
+ *  new_game(random=0): environment.py:28-33; random=1: new_random_game :81-86 (mask nullable)
  *  act: GymEnvironment.act :124-142 (simple=1: SimpleGymEnvironment.act :148-152); outputs
  *       reward / terminal / frame index per env (each nullable), state updated in place
  *  screen: Environment.screen :95-99 of every env's current frame -> out + e*out_stride
@@ -262,7 +262,7 @@ typedef struct a3c_engine_config {
   int action_repeat;     /* config.py:50 (1)                                          */
   int num_frames;        /* synthetic frame pool size (HBM resident RGB frames)       */
   int use_graph;         /* capture the rollout+backward into a hipGraph              */
-  uint64_t seed;         /* main.py:336 random_seed (123)                             */
+  uint64_t seed;         /* main.py:35 random_seed (123)                             */
   double gamma;          /* config.py:9 discount 0.99                                 */
   float beta;            /* config.py:16 entropy weight 0.01                          */
   float learning_rate;   /* config.py:11 7e-4                                          */
@@ -283,7 +283,7 @@ typedef struct a3c_engine_config {
 void a3c_engine_config_default(a3c_engine_config* cfg);
 int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out);
 int a3c_engine_destroy(a3c_engine* eng);
-/* fill the frame pool, reset the envs (new_random_game, environment.py:81-86), fill each
+/* fill the frame pool, reset the envs (new_random_game, environment.py:35-40), fill each
  * history with 4 copies of the first screen (agent.py:37-38) and initialise params
  * from host memory (nullable -> keep), rms slot = 1, mom = 0. */
 int a3c_engine_reset(a3c_engine* eng, const float* host_params, void* stream);

@@ -3,7 +3,7 @@ cpu_baseline leg).
 
 Restates, on the synthetic env, the batched form of the reference worker loop:
   agent.py:52-67 (train: predict -> act -> observe -> new_random_game on terminal)
-  agent.py:141-151 predict (q) / network.py:461-468 + assets/a3c.png (a3c) action draw
+  agent.py:141-151 predict (q) / network.py:65-72 + assets/a3c.png (a3c) action draw
   agent.py:153-167 observe (reward clip, history add, update cadence, target sync)
   agent.py:169-207 batch_update (TD target) / assets/a3c.png n-step returns (a3c)
   agent.py:306-321 loss, per-tensor clip_by_norm(40), RMSProp apply (main.py:63-65)
@@ -15,7 +15,7 @@ from . import philox as px
 from . import ref_cpu as R
 from .synthetic_env import SyntheticAtari, pool_frame
 
-EP_END_CHOICES = np.array([0.1, 0.01, 0.5], np.float32)   # main.py:369
+EP_END_CHOICES = np.array([0.1, 0.01, 0.5], np.float32)   # main.py:68
 
 
 class EngineRef:

@@ -1,11 +1,11 @@
 """Philox4x32-10 counter-based RNG, numpy restatement (TEST INFRASTRUCTURE ONLY).
 
 The reference draws its randomness from Python's ``random`` module
-(``agent.py:146-147`` epsilon coin / random action, ``environment.py:83`` no-op count,
-``main.py:369`` ep_end choice) and TF's op RNG (``network.py:468`` ``batch_sample``,
+(``agent.py:146-147`` epsilon coin / random action, ``environment.py:37`` no-op count,
+``main.py:68`` ep_end choice) and TF's op RNG (``network.py:72`` ``batch_sample``,
 missing).  Neither is reproducible across a batched GPU engine, so the build defines
 its randomness as Philox4x32-10 (Salmon et al., SC'11) keyed by the run seed
-(``main.py:336`` default 123) and counted by (step, env, purpose).  The HIP kernels
+(``main.py:35`` default 123) and counted by (step, env, purpose).  The HIP kernels
 in ``csrc/philox.h`` implement the same function; this module replays it so the
 oracle and the GPU agree bit for bit.
 """

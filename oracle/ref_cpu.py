@@ -16,11 +16,11 @@ import math
 import numpy as np
 
 # --------------------------------------------------------------------------------------
-# A1  Environment.screen  (environment.py:95-99)
+# A1  Environment.screen  (environment.py:49-53)
 # --------------------------------------------------------------------------------------
 
 def luminance_u8(rgb):
-    """environment.py:97-98: ``0.2126*R + 0.7152*G + 0.0722*B`` evaluated by numpy as
+    """environment.py:51-52: ``0.2126*R + 0.7152*G + 0.0722*B`` evaluated by numpy as
     u8 x python-float -> float64, left to right, then ``.astype(np.uint8)`` (truncation)."""
     rgb = np.asarray(rgb)
     r = rgb[..., 0].astype(np.float64)
@@ -101,7 +101,7 @@ def resize_bilinear_u8(img, out_h, out_w):
 
 
 def screen(rgb, out_h=84, out_w=84):
-    """environment.py:95-99 for one [H,W,3] frame or a batch [E,H,W,3]."""
+    """environment.py:49-53 for one [H,W,3] frame or a batch [E,H,W,3]."""
     rgb = np.asarray(rgb, np.uint8)
     if rgb.ndim == 3:
         return resize_bilinear_u8(luminance_u8(rgb), out_h, out_w)
@@ -177,7 +177,7 @@ def param_shapes(action_size, algo='a3c', dqn_type='nips', history_length=4, lst
 
 
 def init_params(shapes, seed=123, stddev=0.02):
-    """ops.py:21 conv weights truncated_normal(0, 0.02) (agent.py:214, network.py:406);
+    """ops.py:21 conv weights truncated_normal(0, 0.02) (agent.py:214, network.py:10);
     ops.py:36-37 linear Matrix random_normal(stddev=0.02); biases zero (ops.py:24,38).
     The draws use numpy (TF's op RNG is not reproducible here)."""
     rng = np.random.default_rng(seed)
@@ -213,7 +213,7 @@ def states_nhwc(planes):
 
 def forward(params, states_u8, algo='a3c', dqn_type='nips', dtype=np.float64, keep=True):
     """Trunk + head forward.  ``states_u8`` is [B,84,84,4] NHWC (values 0..255).
-    agent.py:226 / network.py:430 ``s_t / 255.``; conv2d+bias+relu (ops.py:22-28);
+    agent.py:226 / network.py:46 ``s_t / 255.``; conv2d+bias+relu (ops.py:22-28);
     flatten (h,w,c) (agent.py:231-232); linear relu (ops.py:41-44); head linear.
     Returns dict with 'z' [B, A(+1)] (a3c: logits then value) and saved activations."""
     convs, flat, fc = trunk_spec(dqn_type)

@@ -4,11 +4,11 @@ gym/ALE is absent from the image (SURVEY.md §2 "OUT OF SCOPE | gym/ALE emulatio
 so the build defines a deterministic emulator with the same *interface semantics*
 the reference relies on:
 
-* ``Environment.new_game``       environment.py:74-79   (reset only when lives == 0, then one no-op step)
-* ``Environment.new_random_game`` environment.py:81-86  (0..random_start-1 extra no-op steps)
-* ``GymEnvironment.act``          environment.py:124-142 (action repeat, life-loss -> reward-1 & terminal
+* ``Environment.new_game``       environment.py:28-33   (reset only when lives == 0, then one no-op step)
+* ``Environment.new_random_game`` environment.py:35-40  (0..random_start-1 extra no-op steps)
+* ``GymEnvironment.act``          environment.py:78-96 (action repeat, life-loss -> reward-1 & terminal
                                                           when training, break on terminal)
-* ``Environment.lives``           environment.py:105-107
+* ``Environment.lives``           environment.py:59-61
 
 Emulator state per env (all integers): episode, ep_step, ep_len, lives, frame.
 Screens are RGB u8 [210,160,3] frames drawn from a hashed pool of ``num_frames`` frames.
@@ -69,7 +69,7 @@ class SyntheticAtari:
 
     # -- emulator primitives --------------------------------------------------
     def _reset(self, m):
-        """``self.env.reset()`` (environment.py:76) for envs in mask m."""
+        """``self.env.reset()`` (environment.py:30) for envs in mask m."""
         self.episode[m] += 1
         self.ep_step[m] = 0
         self.lives[m] = self.L0
@@ -78,7 +78,7 @@ class SyntheticAtari:
         self.frame[m] = (x1 % self.P)[m]
 
     def _step(self, action, m):
-        """``self.env.step(action)`` (environment.py:88-89) for envs in mask m."""
+        """``self.env.step(action)`` (environment.py:42-43) for envs in mask m."""
         action = np.broadcast_to(np.asarray(action, np.uint32), (self.E,))
         self.ep_step[m] += 1
         x0, x1, x2, _ = px.philox4x32(self.ep_step, self.ids, self.episode, px.P_STEP,
@@ -99,13 +99,13 @@ class SyntheticAtari:
 
     # -- reference interface semantics ----------------------------------------
     def new_game(self, m=None):
-        """environment.py:74-79."""
+        """environment.py:28-33."""
         m = np.ones(self.E, bool) if m is None else m
         self._reset(m & (self.lives == 0))
         self._step(0, m)
 
     def new_random_game(self, m=None):
-        """environment.py:81-86."""
+        """environment.py:35-40."""
         m = np.ones(self.E, bool) if m is None else m
         self.new_game(m)
         x0, _, _, _ = px.philox4x32(self.ep_step, self.ids, self.episode, px.P_NOOP,
@@ -115,7 +115,7 @@ class SyntheticAtari:
             self._step(0, m & (k > i))
 
     def act(self, action, is_training=True):
-        """GymEnvironment.act, environment.py:124-142.  Returns (frame_idx, reward, terminal)."""
+        """GymEnvironment.act, environment.py:78-96.  Returns (frame_idx, reward, terminal)."""
         cum = np.zeros(self.E, np.float32)
         start_lives = self.lives.copy()
         active = np.ones(self.E, bool)
@@ -133,7 +133,7 @@ class SyntheticAtari:
         return self.frame.copy(), self.reward.copy(), self.terminal.copy()
 
     def simple_act(self, action):
-        """SimpleGymEnvironment.act, environment.py:148-152 (one raw step, no life-loss handling)."""
+        """SimpleGymEnvironment.act, environment.py:102-106 (one raw step, no life-loss handling)."""
         self._step(action, np.ones(self.E, bool))
         return self.frame.copy(), self.reward.copy(), self.terminal.copy()
 

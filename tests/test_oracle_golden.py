@@ -34,7 +34,7 @@ def test_resize_other_geometries_match_reference(screen_golden):
 
 
 def test_full_luminance_table_matches_reference(screen_golden):
-    """All 2^24 RGB values: fp64, left-to-right, truncating (environment.py:97-98)."""
+    """All 2^24 RGB values: fp64, left-to-right, truncating (environment.py:51-52)."""
     g = screen_golden
     rgb = np.arange(1 << 24, dtype=np.uint32)
     fr = np.stack([(rgb >> 16) & 255, (rgb >> 8) & 255, rgb & 255], -1).astype(np.uint8)
