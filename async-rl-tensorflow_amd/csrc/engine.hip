@@ -81,6 +81,11 @@ struct a3c_engine {
   hipStream_t gs;          // backward side stream (weight-gradient GEMMs beside the conv backward)
   hipEvent_t ev_gfork, ev_gjoin;
   hipEvent_t ev_start, ev_roll[2];
+  // external (host) envs: the host steps the envs between ext_act and ext_observe
+  int ext;                 // cfg.external_env
+  int ext_t;               // next rollout step (0..n; n: ready for rollout_grad)
+  bool ext_begun;          // a3c_engine_ext_begin done since reset
+  int32_t* ext_idx;        // [E] identity frame index into the staging buffer (pool)
   int64_t iter;            // rollouts issued since reset
   bool grad_ready;         // the last rollout_grad call computed a gradient
   bool reset_done;
@@ -160,7 +165,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   e->cfg = *cfg;
   if (a3c_make_layout(&cfg->net, &e->L) || cfg->num_envs < 1 || cfg->n_step < 1 || cfg->n_step > 64 ||
       cfg->num_frames < 1 || cfg->random_start < 1 || cfg->action_repeat < 1 || cfg->world_size < 1 ||
-      (cfg->overlap && cfg->net.algo != A3C_ALGO_A3C) ||
+      (cfg->overlap && cfg->net.algo != A3C_ALGO_A3C) || (cfg->overlap && cfg->external_env) ||
       (cfg->net.lstm_units && !cfg->overlap && cfg->n_step < 2)) {   // sync n=1 would read and
                                                                        // write one state buffer
     delete e;
@@ -171,6 +176,8 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   e->E = cfg->num_envs;
   e->n = cfg->n_step;
   e->overlap = cfg->overlap ? 1 : 0;
+  e->ext = cfg->external_env ? 1 : 0;
+  if (e->ext) e->cfg.num_frames = cfg->num_envs;   // the pool is the host frames' staging buffer
   e->fused_screen = 1;
   if (const char* v = getenv("A3C_FUSED_SCREEN")) e->fused_screen = atoi(v) != 0;
   e->nslot = e->overlap ? 2 : 1;
@@ -189,7 +196,8 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   ALLOC(e->mom, L.total * 4);
   ALLOC(e->grads, L.total * 4);
   ALLOC(e->ring, (int64_t)E * e->R * PLANE);
-  ALLOC(e->pool, (int64_t)cfg->num_frames * SCREEN_H * SCREEN_W * 3);
+  ALLOC(e->pool, (int64_t)e->cfg.num_frames * SCREEN_H * SCREEN_W * 3);
+  ALLOC(e->ext_idx, E * 4);
   ALLOC(e->counters, 64);
   ALLOC(e->env.episode, 2 * E * 4);
   ALLOC(e->env.ep_step, 2 * E * 4);
@@ -275,13 +283,19 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     }
   }
   e->envp.k0 = e->k0; e->envp.k1 = e->k1;
-  e->envp.P = cfg->num_frames;
+  e->envp.P = e->cfg.num_frames;
   e->envp.A = L.A;
   e->envp.L0 = cfg->start_lives;
   e->envp.random_start = cfg->random_start;
   e->envp.action_repeat = cfg->action_repeat;
   e->envp.env_id_base = cfg->env_id_base;
   // per-env final epsilon (main.py:68 samples ep_end per worker from {0.1, 0.01, 0.5})
+  std::vector<int32_t> idx(E);
+  for (int64_t i = 0; i < E; ++i) idx[i] = (int32_t)i;
+  if (hipMemcpy(e->ext_idx, idx.data(), E * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    a3c_engine_destroy(e);
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "hipMemcpy");
+  }
   std::vector<float> ee(E);
   static const float choices[3] = {0.1f, 0.01f, 0.5f};
   for (int64_t i = 0; i < E; ++i) {
@@ -359,30 +373,38 @@ static const Slot& prev_slot(const a3c_engine* e, const Slot& sl) {
   return e->nslot == 2 ? e->slot[&sl == &e->slot[0] ? 1 : 0] : sl;
 }
 
-static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
+// rollout start: forward weights of the rollout's parameters (+ q: the epsilon schedule)
+static int enqueue_rollout_begin(a3c_engine* e, const Slot& sl, hipStream_t s) {
+  const a3c_engine_config& c = e->cfg;
+  int rc = a3c_prep_fwd_launch(e->L, sl.P, sl.prep, s);   // params are fixed for the rollout
+  if (rc) return rc;
+  if (e->L.algo == A3C_ALGO_Q) {
+    hipLaunchKernelGGL(k_eps, dim3((e->E + 255) / 256), dim3(256), 0, s, e->eps, e->ep_end, e->E, e->counters,
+                       c.ep_start, c.ep_end_t, c.learn_start);
+    A3C_CHECK(hipGetLastError());
+  }
+  return 0;
+}
+
+// rollout step t: forward of s_{tau+t}, action draw (agent.py:141-151 / network.py:65-72) and,
+// with the device env, act + observe clip + Environment.screen of the new frame into the ring
+// (external envs: the host steps them between a3c_engine_ext_act and a3c_engine_ext_observe).
+static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
   const NetLayout& L = e->L;
   const int E = e->E, n = e->n, zs = L.zs;
   const bool q = L.algo == A3C_ALGO_Q;
-  const Slot& pv = prev_slot(e, sl);
-  const int64_t lastE = (int64_t)(n - 1) * E;
-  int rc = a3c_prep_fwd_launch(L, sl.P, sl.prep, s);   // params are fixed for the rollout
-  if (rc) return rc;
-  if (q) {
-    hipLaunchKernelGGL(k_eps, dim3((E + 255) / 256), dim3(256), 0, s, e->eps, e->ep_end, E, e->counters,
-                       c.ep_start, c.ep_end_t, c.learn_start);
-    A3C_CHECK(hipGetLastError());
-  }
-  for (int t = 0; t < n; ++t) {
-    HeadSelect sel = {};
-    sel.mode = q ? 1 : 0;
-    sel.k0 = e->k0; sel.k1 = e->k1;
-    sel.tau_ptr = e->counters; sel.tau_add = t;
-    sel.env_ids = nullptr; sel.env_id_base = c.env_id_base; sel.E = E;
-    sel.eps = e->eps;
-    const int64_t o = (int64_t)t * E;
-    sel.actions = sl.actions + o;
-    sel.env_on = 1;
+  const bool dev_env = !e->ext;
+  HeadSelect sel = {};
+  sel.mode = q ? 1 : 0;
+  sel.k0 = e->k0; sel.k1 = e->k1;
+  sel.tau_ptr = e->counters; sel.tau_add = t;
+  sel.env_ids = nullptr; sel.env_id_base = c.env_id_base; sel.E = E;
+  sel.eps = e->eps;
+  const int64_t o = (int64_t)t * E;
+  sel.actions = sl.actions + o;
+  sel.env_on = dev_env ? 1 : 0;
+  if (dev_env) {
     sel.par_E = E;
     sel.envp = e->envp;
     sel.envb = e->env;
@@ -394,25 +416,32 @@ static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
       sel.ring = e->ring;
       sel.R = e->R;
     }
-    LstmStep ls = {};
-    if (L.lstm) {   // carry-in: step t-1 of this rollout, or the last step of the previous one
-      const Slot& src = t > 0 ? sl : pv;
-      const int64_t so = t > 0 ? o - E : lastE;
-      ls.h_src = src.lh + so * LSTM_U; ls.c_src = src.lc + so * LSTM_U; ls.prev_terms = src.terms + so;
-      ls.hp = sl.lhp + o * LSTM_U; ls.cp = sl.lcp + o * LSTM_U; ls.gates = sl.lg + o * LSTM_G;
-      ls.h = sl.lh + o * LSTM_U; ls.c = sl.lc + o * LSTM_U;
-    }
-    rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
-                            sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s,
-                            L.lstm ? &ls : nullptr);
-    if (rc) return rc;
-    if (!e->fused_screen) {
-      rc = a3c_env_screen_launch(E, sl.frames + o, e->pool, e->ring, e->R, e->counters, t, s);
-      if (rc) return rc;
-    }
   }
-  if (!q) {
-    // bootstrap V(s_{t+n}) with the same parameters (assets/a3c.png)
+  LstmStep ls = {};
+  if (L.lstm) {   // carry-in: step t-1 of this rollout, or the last step of the previous one
+    const Slot& src = t > 0 ? sl : prev_slot(e, sl);
+    const int64_t so = t > 0 ? o - E : (int64_t)(n - 1) * E;
+    ls.h_src = src.lh + so * LSTM_U; ls.c_src = src.lc + so * LSTM_U; ls.prev_terms = src.terms + so;
+    ls.hp = sl.lhp + o * LSTM_U; ls.cp = sl.lcp + o * LSTM_U; ls.gates = sl.lg + o * LSTM_G;
+    ls.h = sl.lh + o * LSTM_U; ls.c = sl.lc + o * LSTM_U;
+  }
+  int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
+                              sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s,
+                              L.lstm ? &ls : nullptr);
+  if (rc) return rc;
+  if (dev_env && !e->fused_screen) {
+    rc = a3c_env_screen_launch(E, sl.frames + o, e->pool, e->ring, e->R, e->counters, t, s);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// rollout end: bootstrap V(s_{t+n}) with the same parameters (assets/a3c.png)
+static int enqueue_rollout_end(a3c_engine* e, const Slot& sl, hipStream_t s) {
+  const NetLayout& L = e->L;
+  const int E = e->E, n = e->n;
+  if (L.algo != A3C_ALGO_Q) {
+    const int64_t lastE = (int64_t)(n - 1) * E;
     HeadSelect none = {};
     none.mode = -1;
     none.E = E;
@@ -421,8 +450,8 @@ static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
       ls.h_src = sl.lh + lastE * LSTM_U; ls.c_src = sl.lc + lastE * LSTM_U; ls.prev_terms = sl.terms + lastE;
       ls.h = sl.lhb; ls.c = sl.lcb;
     }
-    rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, n, e->counters), E, nullptr, sl.scr_l2, sl.scr_l3,
-                            sl.z + e->nE * zs, none, s, L.lstm ? &ls : nullptr);
+    int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, n, e->counters), E, nullptr, sl.scr_l2,
+                                sl.scr_l3, sl.z + e->nE * L.zs, none, s, L.lstm ? &ls : nullptr);
     if (rc) return rc;
   }
   if (e->overlap) {
@@ -430,6 +459,12 @@ static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
     A3C_CHECK(hipGetLastError());
   }
   return 0;
+}
+
+static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
+  int rc = enqueue_rollout_begin(e, sl, s);
+  for (int t = 0; t < e->n && !rc; ++t) rc = enqueue_step(e, sl, t, s);
+  return rc ? rc : enqueue_rollout_end(e, sl, s);
 }
 
 // returns / TD target, loss + backward over the slot's n*E samples, per-tensor norms (+ the
@@ -544,10 +579,12 @@ extern "C" int a3c_engine_reset(a3c_engine* e, const float* host_params, void* s
   A3C_CHECK(hipMemsetAsync(e->grads, 0, L.total * 4, s));
   A3C_CHECK(hipMemsetAsync(e->loss, 0, 64, s));
   A3C_CHECK(hipMemsetAsync(e->ring, 0, (size_t)e->E * e->R * PLANE, s));
-  rc = a3c_pool_fill_launch(e->pool, e->cfg.num_frames, e->k0, e->k1, s);
-  if (rc) return rc;
-  rc = a3c_env_init_launch(e->envp, e->env, e->E, e->pool, e->ring, e->R, e->counters, s);
-  if (rc) return rc;
+  if (!e->ext) {
+    rc = a3c_pool_fill_launch(e->pool, e->cfg.num_frames, e->k0, e->k1, s);
+    if (rc) return rc;
+    rc = a3c_env_init_launch(e->envp, e->env, e->E, e->pool, e->ring, e->R, e->counters, s);
+    if (rc) return rc;
+  }
   if (e->overlap)
     for (int k = 0; k < 2; ++k)
       A3C_CHECK(hipMemcpyAsync(e->slot[k].P, e->params, L.total * 4, hipMemcpyDeviceToDevice, s));
@@ -560,6 +597,8 @@ extern "C" int a3c_engine_reset(a3c_engine* e, const float* host_params, void* s
   e->iter = 0;
   e->grad_ready = false;
   e->reset_done = true;
+  e->ext_t = 0;
+  e->ext_begun = false;
   return 0;
 }
 
@@ -567,6 +606,16 @@ extern "C" int a3c_engine_rollout_grad(a3c_engine* e, void* stream) {
   if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_rollout_grad", "null");
   if (!e->reset_done) return a3c_set_error(A3C_ERR_STATE, "a3c_engine_rollout_grad", "call a3c_engine_reset first");
   hipStream_t s = (hipStream_t)stream;
+  if (e->ext) {
+    // external envs: the n steps were driven by ext_act / ext_observe; bootstrap + grad here
+    if (e->ext_t != e->n)
+      return a3c_set_error(A3C_ERR_STATE, "a3c_engine_rollout_grad", "external envs: n ext_act/ext_observe first");
+    int rc = enqueue_rollout_end(e, e->slot[0], s);
+    if (!rc) rc = run_graph(e, 3, 2, 0, s);
+    e->grad_ready = rc == 0;
+    e->ext_t = 0;
+    return rc;
+  }
   if (!e->overlap) {
     int rc = run_graph(e, 0, 0, 0, s);
     e->grad_ready = rc == 0;
@@ -611,6 +660,82 @@ extern "C" int a3c_engine_apply(a3c_engine* e, void* stream) {
   // overlap: parameter snapshot for the next rollout (iter), whose slot's previous rollout
   // (iter - 2) has just been back-propagated on this stream
   A3C_CHECK(hipMemcpyAsync(e->slot[e->iter & 1].P, e->params, e->L.total * 4, hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+// ---- external (host) environments (env workers feeding host RGB buffers) ----
+__global__ void k_ext_init(int64_t* counters, int32_t* frame1, int E) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e == 0) { counters[0] = HIST - 1; counters[1] = 0; }
+  if (e < E) frame1[e] = e;      // env state parity (HIST-1)&1 = 1: frame e of the staging buffer
+}
+
+__global__ void k_ext_clip(float* r, int E) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < E) r[e] = fmaxf(-1.0f, fminf(1.0f, r[e]));   // observe clip, agent.py:154
+}
+
+static int ext_check(a3c_engine* e, const char* what) {
+  if (!e) return a3c_set_error(A3C_ERR_INVALID, what, "null");
+  if (!e->ext) return a3c_set_error(A3C_ERR_INVALID, what, "engine was not created with external_env = 1");
+  if (!e->reset_done) return a3c_set_error(A3C_ERR_STATE, what, "call a3c_engine_reset first");
+  return 0;
+}
+
+// first screens of the new (random) games -> every history slot (agent.py:33-38 before_train)
+extern "C" int a3c_engine_ext_begin(a3c_engine* e, const uint8_t* rgb, void* stream) {
+  if (int rc = ext_check(e, "a3c_engine_ext_begin")) return rc;
+  if (!rgb) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_ext_begin", "null frames");
+  hipStream_t s = (hipStream_t)stream;
+  const int E = e->E;
+  A3C_CHECK(hipMemcpyAsync(e->pool, rgb, (size_t)E * SCREEN_H * SCREEN_W * 3, hipMemcpyDefault, s));
+  hipLaunchKernelGGL(k_ext_init, dim3((E + 255) / 256), dim3(256), 0, s, e->counters, e->env.frame + E, E);
+  A3C_CHECK(hipGetLastError());
+  int rc = a3c_env_init_screens_launch(e->env, E, e->pool, e->ring, e->R, s);
+  if (rc) return rc;
+  e->ext_begun = true;
+  e->ext_t = 0;
+  return 0;
+}
+
+// predict of rollout step t for every env (forward + action draw); actions -> `actions`
+// (host, pinned for a true async copy, or device), valid once the stream reaches this point
+extern "C" int a3c_engine_ext_act(a3c_engine* e, int32_t* actions, void* stream) {
+  if (int rc = ext_check(e, "a3c_engine_ext_act")) return rc;
+  if (!e->ext_begun || e->ext_t >= e->n || !actions)
+    return a3c_set_error(A3C_ERR_STATE, "a3c_engine_ext_act", "ext_begin first; at most n steps per rollout");
+  hipStream_t s = (hipStream_t)stream;
+  const Slot& sl = e->slot[0];
+  if (e->ext_t == 0) {
+    int rc = enqueue_rollout_begin(e, sl, s);
+    if (rc) return rc;
+  }
+  int rc = enqueue_step(e, sl, e->ext_t, s);
+  if (rc) return rc;
+  A3C_CHECK(hipMemcpyAsync(actions, sl.actions + (int64_t)e->ext_t * e->E, (size_t)e->E * 4, hipMemcpyDefault, s));
+  return 0;
+}
+
+// observe of rollout step t: the post-act RGB frames [E][210][160][3] u8, rewards [E] f32 and
+// terminals [E] u8 of every env (GymEnvironment.act, environment.py:78-96, done on the host) ->
+// reward clip (agent.py:154), Environment.screen + History.add into the frame ring
+extern "C" int a3c_engine_ext_observe(a3c_engine* e, const uint8_t* rgb, const float* rewards,
+                                      const uint8_t* terminals, void* stream) {
+  if (int rc = ext_check(e, "a3c_engine_ext_observe")) return rc;
+  if (!e->ext_begun || e->ext_t >= e->n || !rgb || !rewards || !terminals)
+    return a3c_set_error(A3C_ERR_STATE, "a3c_engine_ext_observe", "ext_act of this step first");
+  hipStream_t s = (hipStream_t)stream;
+  const Slot& sl = e->slot[0];
+  const int E = e->E, t = e->ext_t;
+  const int64_t o = (int64_t)t * E;
+  A3C_CHECK(hipMemcpyAsync(e->pool, rgb, (size_t)E * SCREEN_H * SCREEN_W * 3, hipMemcpyDefault, s));
+  A3C_CHECK(hipMemcpyAsync(sl.rewards + o, rewards, (size_t)E * 4, hipMemcpyDefault, s));
+  A3C_CHECK(hipMemcpyAsync(sl.terms + o, terminals, (size_t)E, hipMemcpyDefault, s));
+  hipLaunchKernelGGL(k_ext_clip, dim3((E + 255) / 256), dim3(256), 0, s, sl.rewards + o, E);
+  A3C_CHECK(hipGetLastError());
+  int rc = a3c_env_screen_launch(E, e->ext_idx, e->pool, e->ring, e->R, e->counters, t, s);
+  if (rc) return rc;
+  e->ext_t = t + 1;
   return 0;
 }
 

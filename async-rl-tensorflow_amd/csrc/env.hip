@@ -80,6 +80,13 @@ int a3c_env_init_launch(const EnvParams& p, const EnvBufs& b, int E, const uint8
   return 0;
 }
 
+int a3c_env_init_screens_launch(const EnvBufs& b, int E, const uint8_t* pool, uint8_t* ring, int R, hipStream_t s) {
+  PreGeom g = a3c_make_geom(SCREEN_H, SCREEN_W, IMG_OUT, IMG_OUT);
+  hipLaunchKernelGGL(k_env_init_screens, dim3(g.parts, E), dim3(256), a3c_pre_smem_bytes(g), s, b, E, pool, ring, R, g);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
 int a3c_screen_rows();
 
 template <int ROWS>

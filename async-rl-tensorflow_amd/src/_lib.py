@@ -38,7 +38,8 @@ class EngineConfig(ctypes.Structure):
                 ('max_step', c_i64), ('decay', c_float), ('momentum', c_float), ('epsilon', c_float),
                 ('clip_norm', c_float), ('literal_adv', c_int), ('ep_start', c_float),
                 ('ep_end', c_float), ('ep_end_t', c_i64), ('learn_start', c_i64),
-                ('target_q_update_step', c_i64), ('discount', c_double), ('overlap', c_int)]
+                ('target_q_update_step', c_i64), ('discount', c_double), ('overlap', c_int),
+                ('external_env', c_int)]
 
 
 class EngineBuffers(ctypes.Structure):
@@ -109,6 +110,9 @@ SIGNATURES = {
     'a3c_engine_slot_buffers': (c_int, [c_void_p, c_int, ctypes.POINTER(EngineBuffers)]),
     'a3c_engine_grad_ready': (c_int, [c_void_p]),
     'a3c_engine_advance': (c_int, [c_void_p, c_void_p]),
+    'a3c_engine_ext_begin': (c_int, [c_void_p, c_void_p, c_void_p]),
+    'a3c_engine_ext_act': (c_int, [c_void_p, c_void_p, c_void_p]),
+    'a3c_engine_ext_observe': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'a3c_dev_alloc': (c_int, [c_i64, ctypes.POINTER(c_void_p)]),
     'a3c_dev_free': (c_int, [c_void_p]),
     'a3c_ipc_handle': (c_int, [c_void_p, c_void_p]),

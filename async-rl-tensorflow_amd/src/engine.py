@@ -43,7 +43,8 @@ def _view(ptr, shape, dtype):
 
 class Engine:
     def __init__(self, num_envs=256, n_step=5, action_size=6, algo='a3c', start_lives=0, num_frames=1024,
-                 seed=123, env_id_base=0, world_size=1, use_graph=True, overlap=False, lstm=False, **overrides):
+                 seed=123, env_id_base=0, world_size=1, use_graph=True, overlap=False, lstm=False,
+                 external_env=False, **overrides):
         _lib.require_device()
         if lstm and algo != 'a3c':
             raise ValueError('the LSTM head is an a3c head')
@@ -60,7 +61,9 @@ class Engine:
         cfg.world_size = int(world_size)
         cfg.use_graph = 1 if use_graph else 0
         cfg.overlap = 1 if overlap else 0
+        cfg.external_env = 1 if external_env else 0
         self.overlap = bool(overlap)
+        self.external_env = bool(external_env)
         for k, v in overrides.items():
             if not hasattr(cfg, k):
                 raise ValueError(f'unknown engine option {k}')
@@ -157,6 +160,7 @@ class Engine:
             self._hp = hp
             arg = hp.ctypes.data_as(ctypes.c_void_p)
         check(lib().a3c_engine_reset(self._h, arg, _lib.stream_handle()), 'a3c_engine_reset')
+        self._ext_began = False
 
     def rollout_grad(self):
         check(lib().a3c_engine_rollout_grad(self._h, _lib.stream_handle()), 'a3c_engine_rollout_grad')
@@ -197,6 +201,53 @@ class Engine:
         ps.push(self.grads, lr_dev=self.sched_ptr)
         self.advance()
         ps.pull(self.params)
+
+    # ---------------------------------------------------------------- host-stepped envs
+    def ext_begin(self, rgb):
+        """external_env: first frames [E,210,160,3] u8 (pinned host or device) -> every history slot."""
+        self._ext_check(rgb, torch.uint8, (self.E, 210, 160, 3), 'rgb')
+        check(lib().a3c_engine_ext_begin(self._h, _lib.ptr(rgb), _lib.stream_handle()), 'a3c_engine_ext_begin')
+
+    def ext_act(self, actions_out):
+        """external_env: forward + draw of the next rollout step; actions -> actions_out [E] int32
+        (pinned host: valid after the stream synchronises)."""
+        self._ext_check(actions_out, torch.int32, (self.E,), 'actions_out')
+        check(lib().a3c_engine_ext_act(self._h, _lib.ptr(actions_out), _lib.stream_handle()), 'a3c_engine_ext_act')
+
+    def ext_observe(self, rgb, rewards, terminals):
+        """external_env: the step's post-act frames, rewards and terminals of every env."""
+        self._ext_check(rgb, torch.uint8, (self.E, 210, 160, 3), 'rgb')
+        self._ext_check(rewards, torch.float32, (self.E,), 'rewards')
+        self._ext_check(terminals, torch.uint8, (self.E,), 'terminals')
+        check(lib().a3c_engine_ext_observe(self._h, _lib.ptr(rgb), _lib.ptr(rewards), _lib.ptr(terminals),
+                                           _lib.stream_handle()), 'a3c_engine_ext_observe')
+
+    def _ext_check(self, t, dtype, shape, name):
+        if not self.external_env:
+            raise ValueError('engine was not created with external_env=True')
+        if not isinstance(t, torch.Tensor) or t.dtype != dtype or tuple(t.shape) != shape or not t.is_contiguous():
+            raise ValueError(f'{name} must be a contiguous {dtype} tensor of shape {shape}')
+        if not t.is_cuda and not t.is_pinned():
+            raise ValueError(f'{name}: host buffers must be pinned (async copies)')
+
+    def iterate_host(self, pool, exchange=None):
+        """One iteration with host-stepped envs (src/host_env.HostEnvPool): per rollout step the
+        GPU draws the actions, the host steps every env, the post-act frames go back to the GPU
+        for Environment.screen + History.add; then loss, backward, exchange, apply."""
+        if not getattr(self, '_ext_began', False):
+            self.ext_begin(pool.begin())
+            self._ext_began = True
+            self._ext_actions = torch.zeros(self.E, dtype=torch.int32).pin_memory()
+        stream = torch.cuda.current_stream()
+        for _ in range(self.n):
+            self.ext_act(self._ext_actions)
+            stream.synchronize()            # actions on the host; the previous H2D copies are done
+            pool.step(self._ext_actions.numpy())
+            self.ext_observe(pool.rgb, pool.rewards, pool.terminals)
+        self.rollout_grad()
+        if exchange is not None:
+            exchange(self.grads)
+        self.apply()
 
     def time_kernel(self, kernel, iters=20):
         """Average device ms of one engine kernel (HIP events on the current stream)."""

@@ -278,6 +278,10 @@ typedef struct a3c_engine_config {
                         apply of rollout k-1 run on the caller's stream; rollout k uses the
                         parameters after update k-2 (A3C stale-parameter asynchrony, fixed
                         staleness 1).  0: synchronous rollout -> grad -> apply.          */
+  int external_env;   /* 1: the envs are stepped by the host (real ALE / gym workers,
+                        SURVEY §8(f)1): a3c_engine_ext_* below feed their RGB frames,
+                        rewards and terminals each step; no synthetic env, no frame pool
+                        (num_frames ignored).  Synchronous engines only.                 */
 } a3c_engine_config;
 
 void a3c_engine_config_default(a3c_engine_config* cfg);
@@ -298,6 +302,25 @@ int a3c_engine_grad_ready(a3c_engine* eng);
 /* advance tau / global step as a3c_engine_apply does, without touching the parameters
  * (Hogwild: the gradient went to the shared shards instead) */
 int a3c_engine_advance(a3c_engine* eng, void* stream);
+
+/* ----------------------------------------------------------------------------
+ * External (host-stepped) environments, cfg.external_env = 1.  Per rollout:
+ *   for t in 0..n-1:  a3c_engine_ext_act -> sync -> host steps every env with its action
+ *                     (GymEnvironment.act, environment.py:78-96; new_random_game on a
+ *                     terminal, agent.py:66-67) -> a3c_engine_ext_observe
+ *   a3c_engine_rollout_grad (bootstrap + loss + backward) -> [exchange] -> a3c_engine_apply.
+ * Host pointers should be pinned (hipHostMalloc / torch pin_memory) for async copies; device
+ * pointers work too (hipMemcpyDefault).
+ *  ext_begin:   rgb [E][210][160][3] u8 first frames of each env (after new_random_game):
+ *               every history slot <- its screen (agent.py:33-38), tau / step counters reset.
+ *  ext_act:     predict of step t (agent.py:141-151 / network.py:65-72 draw); actions [E] i32.
+ *  ext_observe: post-act frames rgb, rewards [E] f32 (clipped here, agent.py:154), terminals
+ *               [E] u8 -> Environment.screen (environment.py:49-53) + History.add.
+ * -------------------------------------------------------------------------- */
+int a3c_engine_ext_begin(a3c_engine* eng, const uint8_t* rgb, void* stream);
+int a3c_engine_ext_act(a3c_engine* eng, int32_t* actions, void* stream);
+int a3c_engine_ext_observe(a3c_engine* eng, const uint8_t* rgb, const float* rewards, const uint8_t* terminals,
+                           void* stream);
 
 /* device pointers owned by the engine (valid until destroy) */
 typedef struct a3c_engine_buffers {

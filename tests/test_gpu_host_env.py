@@ -1,0 +1,83 @@
+"""Host-stepped envs feeding the engine (a3c_engine_ext_*, src/host_env.py): with
+the synthetic emulator stepped on the HOST (oracle/synthetic_env.py, one object per env, raw RGB
+frames through pinned buffers), the external-env engine must reproduce the device-env engine bit
+for bit: same actions, rewards, terminals, frame ring (Environment.screen of the uploaded frames),
+and the same losses and parameters."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip('torch')
+
+from oracle.synthetic_env import SyntheticAtari, pool_frame  # noqa: E402
+
+
+class HostSynthEnv:
+    """One synthetic env on the host with the interface HostEnvPool steps (raw RGB frames)."""
+
+    def __init__(self, seed, e, P, A, lives):
+        self.seed = seed
+        self.env = SyntheticAtari(seed, 1, P, A, lives, env_id_base=e)
+
+    def _rgb(self):
+        return pool_frame(self.seed, int(self.env.frame[0]))
+
+    def new_random_game(self):
+        self.env.new_random_game()
+        return self._rgb(), 0, 0, bool(self.env.terminal[0])
+
+    def act(self, action, is_training=True):
+        _, r, t = self.env.act(np.array([action]), is_training=is_training)
+        return self._rgb(), float(r[0]), bool(t[0])
+
+
+def _pair(algo, A, E, n, lives, seed, P, lstm=False):
+    from src.engine import Engine
+    from src.initializers import init_params, flatten_host
+    from src.kernels import param_names_shapes
+    kw = dict(num_envs=E, n_step=n, action_size=A, algo=algo, start_lives=lives, seed=seed, lstm=lstm,
+              learning_rate=2e-3)
+    dev = Engine(num_frames=P, **kw)
+    ext = Engine(num_frames=1, external_env=True, **kw)
+    ns = param_names_shapes(A, algo, lstm=lstm)
+    p = flatten_host(ns, dev.offsets, dev.params.numel(), init_params(ns, seed=seed, stddev=0.08))
+    dev.reset(p)
+    ext.reset(p)
+    return dev, ext
+
+
+@pytest.mark.parametrize('algo,A,E,n,lives,lstm', [('a3c', 6, 8, 5, 3, False), ('a3c', 4, 5, 3, 5, True),
+                                                   ('q', 6, 4, 6, 3, False)])
+def test_external_envs_equal_device_envs(algo, A, E, n, lives, lstm):
+    from src.host_env import HostEnvPool
+    seed, P = 900 + E, 40
+    dev, ext = _pair(algo, A, E, n, lives, seed, P, lstm)
+    pool = HostEnvPool([HostSynthEnv(seed, e, P, A, lives) for e in range(E)], threads=2)
+    for it in range(4):
+        dev.iterate()
+        ext.iterate_host(pool)
+        torch.cuda.synchronize()
+        assert torch.equal(dev.actions, ext.actions), it
+        assert torch.equal(dev.rewards, ext.rewards), it
+        assert torch.equal(dev.terminals, ext.terminals), it
+        assert torch.equal(dev.frame_ring, ext.frame_ring), it
+        assert torch.equal(dev.counters, ext.counters), it
+        torch.testing.assert_close(ext.loss, dev.loss, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(ext.params, dev.params, rtol=1e-6, atol=1e-7)
+    pool.close()
+
+
+def test_external_env_call_order_enforced():
+    from src.engine import Engine
+    ext = Engine(num_envs=2, n_step=2, action_size=6, external_env=True, num_frames=1)
+    ext.reset()
+    acts = torch.zeros(2, dtype=torch.int32).pin_memory()
+    with pytest.raises(RuntimeError):
+        ext.ext_act(acts)                       # ext_begin first
+    with pytest.raises(RuntimeError):
+        ext.rollout_grad()                      # n steps first
+    with pytest.raises(ValueError):
+        ext.ext_act(torch.zeros(2, dtype=torch.int32))     # pageable host buffer
+    with pytest.raises(RuntimeError):
+        Engine(num_envs=2, n_step=2, action_size=6, external_env=True, overlap=True)

@@ -1,0 +1,50 @@
+"""Host env adapter (src/host_env.py) against golden traces of the reference's own
+Environment / GymEnvironment code (tests/golden/make_env_goldens.py, environment.py:28-96) on a
+scripted emulator: same frames, rewards, terminals, lives, emulator step and reset counts."""
+import random
+
+import numpy as np
+
+from fake_ale import ScriptedALE
+from src.host_env import AtariEnv, HostEnvPool
+
+
+def _trace(env, emu, actions, is_training):
+    rows = []
+
+    def rec(kind, r, term):
+        rows.append((kind, int(env._screen[0, 0, 0]), float(r), int(bool(term)), emu.lives_, emu.steps, emu.resets))
+
+    _, r, _, term = env.new_random_game()
+    rec(0, r, term)
+    for a in actions:
+        _, r, term = env.act(int(a), is_training=is_training)
+        rec(1, r, term)
+        if term:
+            _, r, _, t2 = env.new_random_game()
+            rec(0, r, t2)
+    return np.array(rows, np.float64)
+
+
+def test_atari_env_matches_reference_traces(golden_dir):
+    g = np.load(f'{golden_dir}/env_act_golden.npz')
+    for i, (seed, lives, rep, rs, training, pyseed) in enumerate(g['cases']):
+        emu = ScriptedALE(int(seed), start_lives=int(lives))
+        env = AtariEnv(emu, action_repeat=int(rep), random_start=int(rs), rng=random.Random(int(pyseed)))
+        got = _trace(env, emu, g[f'actions{i}'], bool(training))
+        assert np.array_equal(got, g[f'trace{i}']), i
+
+
+def test_host_env_pool_steps_and_resets():
+    envs = [AtariEnv(ScriptedALE(s, start_lives=2, max_len=7, frame_shape=(210, 160, 3)), random_start=3, rng=random.Random(s)) for s in range(5)]
+    pool = HostEnvPool(envs, threads=2)
+    rgb = pool.begin()
+    assert tuple(rgb.shape) == (5, 210, 160, 3)
+    seen_term = False
+    for _ in range(20):
+        pool.step(np.arange(5) % 6)
+        t = pool.terminals.numpy()
+        seen_term |= bool(t.any())
+        assert set(np.unique(pool.rewards.numpy())) <= {-2.0, -1.0, 0.0, 1.0}
+    assert seen_term
+    pool.close()
