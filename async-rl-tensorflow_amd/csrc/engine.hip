@@ -3,7 +3,7 @@
 // clip, then (after the host's optional RCCL all-reduce of the clipped gradients) RMSProp apply.
 //
 // Reference loop it replaces (per worker): agent.py:52-67 train -> predict (:141-151) ->
-// env.act (environment.py:78-96) -> observe (:153-167) -> batch_update (:169-207) with the
+// env.act (environment.py:78-96) -> observe (agent.py:153-167) -> batch_update (agent.py:169-207) with the
 // shared RMSProp apply on the parameter server (main.py:60-66).  A3C (network.py + assets/a3c.png)
 // uses n-step returns instead of the TD target; algo Q keeps agent.py's target network.
 //

@@ -1,6 +1,6 @@
 // Synthetic Atari stand-in (device side), bit-identical to oracle/synthetic_env.py, with the
-// reference's interface semantics: new_game environment.py:28-33, new_random_game :81-86,
-// act :124-142 (action repeat, life-loss terminal when training).
+// reference's interface semantics: new_game environment.py:28-33, new_random_game :35-40,
+// act :78-96 (action repeat, life-loss terminal when training).
 #pragma once
 #include "env.h"
 
@@ -27,7 +27,7 @@ __device__ inline void env_store(const EnvBufs& b, int64_t i, const EnvState& s,
 }
 
 // self.env.reset() (environment.py:30)
-__device__ inline void env_reset(EnvState& s, const EnvParams& p, uint32_t id) {
+__host__ __device__ inline void env_reset(EnvState& s, const EnvParams& p, uint32_t id) {
   s.episode += 1u;
   s.ep_step = 0;
   s.lives = p.L0;
@@ -37,13 +37,13 @@ __device__ inline void env_reset(EnvState& s, const EnvParams& p, uint32_t id) {
 }
 
 // frame index of a step whose draw was x.x, for `action`
-__device__ inline int32_t env_frame_of(uint32_t xx, uint32_t action, const EnvParams& p) {
+__host__ __device__ inline int32_t env_frame_of(uint32_t xx, uint32_t action, const EnvParams& p) {
   return (int32_t)((xx + action * GOLDEN_MULT) % (uint32_t)p.P);
 }
 
 // self.env.step(action) (environment.py:42-43) without the frame: nothing here depends on the
 // action, which only picks the frame (env_frame_of(returned x.x, action))
-__device__ inline uint32_t env_step_core(EnvState& s, const EnvParams& p, uint32_t id) {
+__host__ __device__ inline uint32_t env_step_core(EnvState& s, const EnvParams& p, uint32_t id) {
   const uint32_t st = s.ep_step + 1u;
   s.ep_step = st;
   u32x4 x = philox4x32(st, id, s.episode, P_STEP, p.k0, p.k1);
@@ -60,12 +60,12 @@ __device__ inline uint32_t env_step_core(EnvState& s, const EnvParams& p, uint32
 }
 
 // self.env.step(action) (environment.py:42-43)
-__device__ inline void env_step_raw(EnvState& s, const EnvParams& p, uint32_t id, uint32_t action) {
+__host__ __device__ inline void env_step_raw(EnvState& s, const EnvParams& p, uint32_t id, uint32_t action) {
   s.frame = env_frame_of(env_step_core(s, p, id), action, p);
 }
 
-// Environment.new_random_game (environment.py:35-40) via new_game (:74-79)
-__device__ inline void env_new_random_game(EnvState& s, const EnvParams& p, uint32_t id) {
+// Environment.new_random_game (environment.py:35-40) via new_game (:28-33)
+__host__ __device__ inline void env_new_random_game(EnvState& s, const EnvParams& p, uint32_t id) {
   if (s.lives == 0) env_reset(s, p, id);
   env_step_raw(s, p, id, 0u);
   u32x4 x = philox4x32(s.ep_step, id, s.episode, P_NOOP, p.k0, p.k1);
@@ -76,7 +76,7 @@ __device__ inline void env_new_random_game(EnvState& s, const EnvParams& p, uint
 // GymEnvironment.act (environment.py:78-96) up to the frame: the repeats' rewards, lives
 // and terminal do not depend on the action; returns the last executed step's draw, whose
 // frame is env_frame_of(draw, action) (so the act can run before the action is drawn)
-__device__ inline uint32_t env_act_pre(EnvState& s, const EnvParams& p, uint32_t id, bool training) {
+__host__ __device__ inline uint32_t env_act_pre(EnvState& s, const EnvParams& p, uint32_t id, bool training) {
   float cum = 0.f;
   const int32_t start_lives = s.lives;
   uint32_t xx = 0;
@@ -94,7 +94,7 @@ __device__ inline uint32_t env_act_pre(EnvState& s, const EnvParams& p, uint32_t
 }
 
 // GymEnvironment.act (environment.py:78-96)
-__device__ inline void env_act(EnvState& s, const EnvParams& p, uint32_t id, uint32_t action, bool training) {
+__host__ __device__ inline void env_act(EnvState& s, const EnvParams& p, uint32_t id, uint32_t action, bool training) {
   s.frame = env_frame_of(env_act_pre(s, p, id, training), action, p);
 }
 

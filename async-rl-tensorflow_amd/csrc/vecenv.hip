@@ -24,7 +24,7 @@ __global__ void k_venv_zero(EnvBufs b, int E) {
   env_store(b, e, s);
 }
 
-// op 0: new_game (environment.py:28-33), 1: new_random_game (:81-86)
+// op 0: new_game (environment.py:28-33), 1: new_random_game (:35-40)
 __global__ void k_venv_new(EnvParams p, EnvBufs b, int E, const uint8_t* __restrict__ mask, int random) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= E || (mask && !mask[e])) return;
@@ -39,7 +39,7 @@ __global__ void k_venv_new(EnvParams p, EnvBufs b, int E, const uint8_t* __restr
   env_store(b, e, s);
 }
 
-// GymEnvironment.act (environment.py:78-96) / SimpleGymEnvironment.act (:148-152 with simple=1)
+// GymEnvironment.act (environment.py:78-96) / SimpleGymEnvironment.act (:102-106 with simple=1)
 __global__ void k_venv_act(EnvParams p, EnvBufs b, int E, const int32_t* __restrict__ actions, int training,
                            int simple, float* __restrict__ rewards, uint8_t* __restrict__ terms,
                            int32_t* __restrict__ frames) {

@@ -111,6 +111,11 @@ SIGNATURES = {
     'a3c_engine_grad_ready': (c_int, [c_void_p]),
     'a3c_engine_advance': (c_int, [c_void_p, c_void_p]),
     'a3c_engine_ext_begin': (c_int, [c_void_p, c_void_p, c_void_p]),
+    'a3c_hostenv_create': (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_u64, c_int, c_int,
+                                   ctypes.POINTER(c_void_p)]),
+    'a3c_hostenv_destroy': (c_int, [c_void_p]),
+    'a3c_hostenv_begin': (c_int, [c_void_p, c_void_p]),
+    'a3c_hostenv_step': (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     'a3c_engine_ext_act': (c_int, [c_void_p, c_void_p, c_void_p]),
     'a3c_engine_ext_observe': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'a3c_dev_alloc': (c_int, [c_i64, ctypes.POINTER(c_void_p)]),

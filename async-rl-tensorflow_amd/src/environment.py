@@ -4,10 +4,10 @@
 synthetic Atari env of the C-ABI (a3c_env_*; dynamics restated in oracle/synthetic_env.py):
 ALE-like lives, episode ends, rewards in {-1,0,1}, RGB 210x160x3 frames from an HBM frame
 pool.  The reference's interface semantics are kept exactly: ``new_game`` resets only when
-``lives == 0`` then takes one no-op step (:74-79), ``new_random_game`` adds 0..random_start-1
-no-ops (:81-86), ``act`` repeats the action, turns a lost life into reward -1 + terminal when
-training and stops at a terminal (:124-142), ``screen`` is the fp64-luminance + Pillow
-BILINEAR 84x84 image (:95-99, bit-exact).  Screens are u8 [84,84] device tensors.
+``lives == 0`` then takes one no-op step (:28-33), ``new_random_game`` adds 0..random_start-1
+no-ops (:35-40), ``act`` repeats the action, turns a lost life into reward -1 + terminal when
+training and stops at a terminal (:78-96), ``screen`` is the fp64-luminance + Pillow
+BILINEAR 84x84 image (:49-53, bit-exact).  Screens are u8 [84,84] device tensors.
 
 ``BatchedEnvironment`` is the same for E envs at once (the MI355X-native form).
 """

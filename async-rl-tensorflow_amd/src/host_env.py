@@ -138,3 +138,51 @@ class HostEnvPool(object):
     if self._ex is not None:
       self._ex.shutdown()
       self._ex = None
+
+
+class SyntheticHostEnvPool(object):
+  """The synthetic emulator (bit-identical to the device env) stepped on host threads by the
+  C-ABI (a3c_hostenv_*), with HostEnvPool's interface: a stand-in for E real ALE workers when
+  driving or measuring the external-env path (PCIe-inclusive).  Buffers are pinned."""
+
+  def __init__(self, num_envs, action_size, start_lives=0, num_frames=1024, seed=123, env_id_base=0,
+               random_start=30, action_repeat=1, threads=8, is_training=True):
+    import ctypes
+    from . import _lib
+    self._lib = _lib
+    self.E = int(num_envs)
+    h = ctypes.c_void_p()
+    _lib.check(_lib.lib().a3c_hostenv_create(self.E, int(action_size), int(start_lives), int(random_start),
+                                             int(action_repeat), int(num_frames), int(seed), int(env_id_base),
+                                             int(threads), ctypes.byref(h)), 'a3c_hostenv_create')
+    self._h = h
+    pin = torch.cuda.is_available()
+    mk = lambda shape, dt: torch.zeros(shape, dtype=dt).pin_memory() if pin else torch.zeros(shape, dtype=dt)  # noqa: E731
+    self.rgb = mk((self.E,) + SCREEN_SHAPE, torch.uint8)
+    self.rewards = mk((self.E,), torch.float32)
+    self.terminals = mk((self.E,), torch.uint8)
+    self._acts = mk((self.E,), torch.int32)
+    self.is_training = is_training
+
+  def begin(self):
+    self._lib.check(self._lib.lib().a3c_hostenv_begin(self._h, self._lib.ptr(self.rgb)), 'a3c_hostenv_begin')
+    return self.rgb
+
+  def step(self, actions):
+    a = torch.as_tensor(np.asarray(actions, np.int32))
+    self._acts.copy_(a)
+    L, p = self._lib.lib(), self._lib.ptr
+    self._lib.check(L.a3c_hostenv_step(self._h, p(self._acts), 1 if self.is_training else 0, p(self.rgb),
+                                       p(self.rewards), p(self.terminals)), 'a3c_hostenv_step')
+    return self.rgb, self.rewards, self.terminals
+
+  def close(self):
+    if getattr(self, '_h', None):
+      self._lib.lib().a3c_hostenv_destroy(self._h)
+      self._h = None
+
+  def __del__(self):
+    try:
+      self.close()
+    except Exception:
+      pass

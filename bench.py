@@ -45,6 +45,11 @@ def parse():
     ap.add_argument('--n-step', type=int, default=5)
     ap.add_argument('--game', default='Pong-v0', choices=sorted(GAMES))
     ap.add_argument('--algo', default='a3c', choices=['a3c', 'q'])
+    ap.add_argument('--env', default='device', choices=['device', 'host'],
+                    help='device: the synthetic emulator runs on the GPU next to the net (default, HBM-resident '
+                         'inputs); host: it runs on host threads (a3c_hostenv, stand-in for real ALE workers) '
+                         'and every step moves the raw RGB frames over PCIe (PCIe-inclusive rate)')
+    ap.add_argument('--host-threads', type=int, default=16)
     ap.add_argument('--lstm', action='store_true',
                     help='C5 LSTM policy head (BASELINE config 5: SpaceInvaders-v0, 256-cell LSTM after the fc)')
     ap.add_argument('--frames', type=int, default=16384, help='HBM frame pool (16384 = 1.65 GB > L3)')
@@ -116,9 +121,17 @@ def main():
         args.update = 'sync'              # the stale-1 pipeline is an A3C (policy-gradient) mode
     if args.lstm and args.algo != 'a3c':
         raise SystemExit('--lstm is an a3c head')
+    host = args.env == 'host'
+    if host and args.update != 'sync':
+        args.update = 'sync'              # host-stepped envs drive a synchronous engine
     eng = Engine(num_envs=E, n_step=n, action_size=A, algo=args.algo, start_lives=lives, num_frames=args.frames,
                  seed=123, env_id_base=rank * E, world_size=world, use_graph=not args.no_graph,
-                 overlap=args.update == 'overlap', lstm=args.lstm)
+                 overlap=args.update == 'overlap', lstm=args.lstm, external_env=host)
+    hpool = None
+    if host:
+        from src.host_env import SyntheticHostEnvPool
+        hpool = SyntheticHostEnvPool(E, A, lives, num_frames=min(args.frames, 2048), seed=123, env_id_base=rank * E,
+                                     threads=args.host_threads)
     ns = param_names_shapes(A, args.algo, lstm=args.lstm)
     params = flatten_host(ns, eng.offsets, eng.params.numel(), init_params(ns, seed=123))
     eng.reset(params)     # every rank starts from the same parameters
@@ -130,7 +143,9 @@ def main():
         ps = HogwildPS(eng.params)
 
     def step():
-        if ps is not None:
+        if hpool is not None:
+            eng.iterate_host(hpool, exchange)
+        elif ps is not None:
             eng.iterate_hogwild(ps)
         else:
             eng.iterate(exchange)
@@ -162,7 +177,7 @@ def main():
     finite = bool(torch.isfinite(eng.params).all().item())
 
     roofline, kernels = None, {}
-    if rank == 0 and not args.no_kernel_timing:
+    if rank == 0 and not args.no_kernel_timing and not host:
         ms = {
             'k_conv12_fwd': eng.time_kernel(_lib.KER_CONV12_FWD, 20),
             'k_conv_bwd': eng.time_kernel(_lib.KER_CONV_BWD, 10),
@@ -209,12 +224,15 @@ def main():
             'metric': METRIC, 'value': round(steps_total / el, 1), 'unit': 'env-steps/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 4),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
-            'data': f'synthetic: HBM-resident hashed RGB 210x160x3 frame pool ({args.frames} frames) stepped by '
-                    f'the on-device synthetic Atari env; random-init NIPS A3C conv net',
+            'data': (f'synthetic: HBM-resident hashed RGB 210x160x3 frame pool ({args.frames} frames) stepped by '
+                     f'the on-device synthetic Atari env; random-init NIPS A3C conv net' if not host else
+                     f'synthetic: host-stepped emulator ({args.host_threads} threads, a3c_hostenv) writing raw RGB '
+                     f'210x160x3 frames into pinned buffers, PCIe H2D every step (PCIe-inclusive); random-init '
+                     f'NIPS A3C conv net'),
             'config': {'workload': f'{args.game}, {E} envs batched per MI355X, n-step={n}, '
                                    f'{"A3C" if args.algo == "a3c" else "one-step Q"} conv net (nips trunk'
                                    f'{" + 256-cell LSTM head" if args.lstm else ""})',
-                       'game': args.game, 'head': 'lstm' if args.lstm else 'feed-forward', 'envs_per_gpu': E, 'n_step': n, 'action_size': A, 'algo': args.algo,
+                       'game': args.game, 'head': 'lstm' if args.lstm else 'feed-forward', 'env': args.env, 'envs_per_gpu': E, 'n_step': n, 'action_size': A, 'algo': args.algo,
                        'env_steps_per_step': world * E * n,
                        'parallelism': (f'dp{world} hogwild: unlocked RMSProp pushes into {world} IPC-mapped HBM '
                                        f'shards over xGMI, pull at rollout start, no collective'

@@ -226,10 +226,10 @@ int a3c_rmsprop_range(float* w, float* ms, float* mom, const float* grads, int64
 /* ----------------------------------------------------------------------------
  * Batched synthetic Atari env (gym/ALE is absent): the Environment / GymEnvironment interface
  * of environment.py:14-106 for E envs on device (dynamics: oracle/synthetic_env.py).
- *  new_game(random=0): environment.py:28-33; random=1: new_random_game :81-86 (mask nullable)
- *  act: GymEnvironment.act :124-142 (simple=1: SimpleGymEnvironment.act :148-152); outputs
+ *  new_game(random=0): environment.py:28-33; random=1: new_random_game :35-40 (mask nullable)
+ *  act: GymEnvironment.act :78-96 (simple=1: SimpleGymEnvironment.act :102-106); outputs
  *       reward / terminal / frame index per env (each nullable), state updated in place
- *  screen: Environment.screen :95-99 of every env's current frame -> out + e*out_stride
+ *  screen: Environment.screen :49-53 of every env's current frame -> out + e*out_stride
  * -------------------------------------------------------------------------- */
 typedef struct a3c_env a3c_env;
 int a3c_env_create(int num_envs, int action_size, int start_lives, int random_start, int action_repeat,
@@ -321,6 +321,21 @@ int a3c_engine_ext_begin(a3c_engine* eng, const uint8_t* rgb, void* stream);
 int a3c_engine_ext_act(a3c_engine* eng, int32_t* actions, void* stream);
 int a3c_engine_ext_observe(a3c_engine* eng, const uint8_t* rgb, const float* rewards, const uint8_t* terminals,
                            void* stream);
+
+/* Host-side batched synthetic env (the device env's emulator, bit-identical dynamics, stepped by
+ * `threads` CPU threads): raw RGB frames into caller host buffers -- a stand-in for real ALE
+ * worker processes when driving / measuring the external-env path.  No GPU work.
+ *  begin: new_random_game of every env; first frames -> rgb [E][210][160][3] u8
+ *  step:  GymEnvironment.act (environment.py:78-96) of every env, post-act frames -> rgb,
+ *         rewards [E] f32 (unclipped), terminals [E] u8; new_random_game where terminal
+ *         (agent.py:66-67). */
+typedef struct a3c_hostenv a3c_hostenv;
+int a3c_hostenv_create(int num_envs, int action_size, int start_lives, int random_start, int action_repeat,
+                       int num_frames, uint64_t seed, int env_id_base, int threads, a3c_hostenv** out);
+int a3c_hostenv_destroy(a3c_hostenv* env);
+int a3c_hostenv_begin(a3c_hostenv* env, uint8_t* rgb);
+int a3c_hostenv_step(a3c_hostenv* env, const int32_t* actions, int is_training, uint8_t* rgb, float* rewards,
+                     uint8_t* terminals);
 
 /* device pointers owned by the engine (valid until destroy) */
 typedef struct a3c_engine_buffers {

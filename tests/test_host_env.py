@@ -48,3 +48,30 @@ def test_host_env_pool_steps_and_resets():
         assert set(np.unique(pool.rewards.numpy())) <= {-2.0, -1.0, 0.0, 1.0}
     assert seen_term
     pool.close()
+
+
+def test_cpp_host_env_matches_oracle():
+    """a3c_hostenv_* (C++ threads, no GPU) == oracle/synthetic_env.py: frames, rewards, terminals,
+    resets after terminals (agent.py:66-67)."""
+    from oracle.synthetic_env import SyntheticAtari, pool_frame
+    from src.host_env import SyntheticHostEnvPool
+    E, P, A, L = 5, 40, 6, 3
+    pool = SyntheticHostEnvPool(E, A, L, num_frames=P, seed=77, threads=3)
+    ref = SyntheticAtari(77, E, P, A, L)
+    rgb = pool.begin().numpy()
+    ref.new_random_game()
+    assert all(np.array_equal(rgb[e], pool_frame(77, int(ref.frame[e]))) for e in range(E))
+    rng = np.random.default_rng(0)
+    terms = 0
+    for it in range(250):
+        a = rng.integers(0, A, E).astype(np.int32)
+        pool.step(a)
+        f, r, t = ref.act(a, True)
+        assert np.array_equal(pool.rewards.numpy(), r), it
+        assert np.array_equal(pool.terminals.numpy(), t.astype(np.uint8)), it
+        assert all(np.array_equal(pool.rgb.numpy()[e], pool_frame(77, int(f[e]))) for e in range(E)), it
+        terms += int(t.sum())
+        if t.any():
+            ref.new_random_game(t.astype(bool))
+    assert terms > 0
+    pool.close()
