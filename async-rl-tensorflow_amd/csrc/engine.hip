@@ -43,6 +43,7 @@ struct Slot {
   // C5 LSTM head: per step h_t, c_t, masked inputs hp, cp [n][E][U], gates [n][E][4U];
   // bootstrap-step h, c [E][U]
   float *lh, *lc, *lhp, *lcp, *lg, *lhb, *lcb;
+  float* lwt;              // LSTM gate matrix of P, transposed for the forward (rollout start)
 };
 
 struct a3c_engine {
@@ -238,6 +239,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
       ALLOC(sl.lg, nE * LSTM_G * 4);
       ALLOC(sl.lhb, E * LSTM_U * 4);
       ALLOC(sl.lcb, E * LSTM_U * 4);
+      ALLOC(sl.lwt, (int64_t)LSTM_K * LSTM_G * 4);
     }
   }
   if (L.lstm) {
@@ -378,6 +380,10 @@ static int enqueue_rollout_begin(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
   int rc = a3c_prep_fwd_launch(e->L, sl.P, sl.prep, s);   // params are fixed for the rollout
   if (rc) return rc;
+  if (e->L.lstm) {
+    rc = a3c_lstm_transpose_launch(sl.P + e->L.off[T_LW], sl.lwt, s);
+    if (rc) return rc;
+  }
   if (e->L.algo == A3C_ALGO_Q) {
     hipLaunchKernelGGL(k_eps, dim3((e->E + 255) / 256), dim3(256), 0, s, e->eps, e->ep_end, e->E, e->counters,
                        c.ep_start, c.ep_end_t, c.learn_start);
@@ -421,6 +427,7 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
   if (L.lstm) {   // carry-in: step t-1 of this rollout, or the last step of the previous one
     const Slot& src = t > 0 ? sl : prev_slot(e, sl);
     const int64_t so = t > 0 ? o - E : (int64_t)(n - 1) * E;
+    ls.wt = sl.lwt;
     ls.h_src = src.lh + so * LSTM_U; ls.c_src = src.lc + so * LSTM_U; ls.prev_terms = src.terms + so;
     ls.hp = sl.lhp + o * LSTM_U; ls.cp = sl.lcp + o * LSTM_U; ls.gates = sl.lg + o * LSTM_G;
     ls.h = sl.lh + o * LSTM_U; ls.c = sl.lc + o * LSTM_U;
@@ -447,6 +454,7 @@ static int enqueue_rollout_end(a3c_engine* e, const Slot& sl, hipStream_t s) {
     none.E = E;
     LstmStep ls = {};
     if (L.lstm) {
+      ls.wt = sl.lwt;
       ls.h_src = sl.lh + lastE * LSTM_U; ls.c_src = sl.lc + lastE * LSTM_U; ls.prev_terms = sl.terms + lastE;
       ls.h = sl.lhb; ls.c = sl.lcb;
     }

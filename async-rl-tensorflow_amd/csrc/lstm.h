@@ -7,14 +7,16 @@
 // one step of the cell for B envs.  h_src / c_src: the previous step's raw outputs, zeroed
 // where prev_terms[e] (the previous transition was terminal).  hp / cp / gates nullable.
 struct LstmStep {
+  const float* wt;          // gate matrix transposed, [1024][512] (a3c_lstm_transpose_launch)
   const float* h_src;
   const float* c_src;
   const uint8_t* prev_terms;
   float *hp, *cp, *gates, *h, *c;
 };
 
-int a3c_lstm_fwd_launch(const float* W, const float* bias, const float* x, const LstmStep& st, int64_t B,
-                        hipStream_t s);
+int a3c_lstm_fwd_launch(const float* bias, const float* x, const LstmStep& st, int64_t B, hipStream_t s);
+// Wt[1024][512] = W[512][1024]^T (once per parameter version: the rollout's forward operand)
+int a3c_lstm_transpose_launch(const float* W, float* Wt, hipStream_t s);
 
 // truncated BPTT over n steps of E envs (see include/a3c_hip.h a3c_lstm_bptt)
 struct LstmSeq {

@@ -501,7 +501,7 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
   if (rc) return rc;
   const float* head_in = act_l3;
   if (ls) {   // C5: LSTM cell on the fc output, heads on its h
-    rc = a3c_lstm_fwd_launch(P + L.off[T_LW], P + L.off[T_LB], act_l3, *ls, B, s);
+    rc = a3c_lstm_fwd_launch(P + L.off[T_LB], act_l3, *ls, B, s);
     if (rc) return rc;
     head_in = ls->h;
   }

@@ -91,6 +91,7 @@ SIGNATURES = {
     'a3c_matmul': (c_int, [c_void_p, c_i64, c_i64, c_void_p, c_i64, c_i64, c_void_p, c_i64, c_int, c_int, c_int,
                            c_void_p, c_int, c_int, c_void_p]),
     'a3c_copy_params': (c_int, [c_void_p, c_void_p, c_i64, c_void_p]),
+    'a3c_lstm_transpose': (c_int, [c_void_p, c_void_p, c_void_p]),
     'a3c_lstm_step': (c_int, [c_void_p] * 6 + [c_i64] + [c_void_p] * 6),
     'a3c_lstm_workspace_bytes': (c_int, [c_int, c_i64, ctypes.POINTER(c_i64)]),
     'a3c_lstm_bptt': (c_int, [c_void_p, c_int, c_i64] + [c_void_p] * 12),

@@ -109,7 +109,9 @@ def lstm_step(w, b, x, h_src, c_src, prev_terms=None, save=True):
     out = dict(h=new(B, U), c=new(B, U))
     if save:
         out.update(hp=new(B, U), cp=new(B, U), gates=new(B, 4 * U))
-    check(lib().a3c_lstm_step(ptr(w), ptr(b), ptr(x), ptr(h_src), ptr(c_src), ptr(prev_terms), B,
+    w_t = torch.empty((w.shape[1], w.shape[0]), dtype=torch.float32, device=x.device)
+    check(lib().a3c_lstm_transpose(ptr(w), ptr(w_t), stream_handle()), 'a3c_lstm_transpose')
+    check(lib().a3c_lstm_step(ptr(w_t), ptr(b), ptr(x), ptr(h_src), ptr(c_src), ptr(prev_terms), B,
                               ptr(out.get('hp')), ptr(out.get('cp')), ptr(out.get('gates')), ptr(out['h']),
                               ptr(out['c']), stream_handle()), 'a3c_lstm_step')
     return out

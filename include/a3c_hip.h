@@ -183,7 +183,9 @@ int a3c_matmul(const float* A, int64_t sam, int64_t sak, const float* B, int64_t
 /* ----------------------------------------------------------------------------
  * C5  LSTM head (BASELINE config 5; no reference code -- build-defined after TF1
  *     BasicLSTMCell, forget_bias 1.0, and the A3C-LSTM of assets/a3c.png's paper).
- *  a3c_lstm_step: one cell step for B envs.  x [B][256] (fc ReLU output), h_src/c_src [B][U]
+ *  a3c_lstm_transpose: w_t [4U][256+U] = w^T, the forward's operand layout (once per
+ *    parameter version).
+ *  a3c_lstm_step: one cell step for B envs on w_t.  x [B][256] (fc ReLU output), h_src/c_src [B][U]
  *    the previous step's outputs; prev_terms [B] (nullable): state zeroed where the previous
  *    transition was terminal.  Writes h/c [B][U]; hp/cp (the masked inputs it used) and gates
  *    ([B][4U], activated i, j, f, o) are nullable (only the backward needs them).
@@ -192,7 +194,8 @@ int a3c_matmul(const float* A, int64_t sam, int64_t sak, const float* B, int64_t
  *    the fc backward); dw [256+U][4U], db [4U] OVERWRITTEN.  terms [n][E] (transition t
  *    terminal -> no gradient flows from step t+1 into step t's state).
  * -------------------------------------------------------------------------- */
-int a3c_lstm_step(const float* w, const float* b, const float* x, const float* h_src, const float* c_src,
+int a3c_lstm_transpose(const float* w, float* w_t, void* stream);
+int a3c_lstm_step(const float* w_t, const float* b, const float* x, const float* h_src, const float* c_src,
                   const uint8_t* prev_terms, int64_t B, float* hp, float* cp, float* gates, float* h,
                   float* c, void* stream);
 int a3c_lstm_workspace_bytes(int n, int64_t E, int64_t* bytes);
