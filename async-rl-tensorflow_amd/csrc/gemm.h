@@ -24,16 +24,6 @@ struct GemmArgs {
 };
 
 int a3c_gemm(bool a_kcontig, bool b_ncontig, GemmArgs g, hipStream_t s);
-
-// k-permuted fp32 MFMA step: in 16x16x4 step s of a 16-wide k block kb, lane (i16, j4) supplies
-// A[row i16][kb + 4 j4 + s] and B[kb + 4 j4 + s][col i16] -- every k of the block exactly once,
-// and each lane's four k are contiguous in memory for k-contiguous A rows and B^T rows, so both
-// operands arrive as one 16-byte load per lane per four MFMAs (no LDS staging).
-__device__ inline f32x4 mfma_k16(const f32x4 a, const f32x4 b, f32x4 c) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], c, 0, 0, 0);
-  return c;
-}
 int a3c_gemm_plan_split(int M, int N, int K, int target_blocks);
 
 inline int a3c_gemm_effective_split(int K, int nsplit) {

@@ -6,7 +6,6 @@
 // Tile 64x64x16, 256 threads = 2x2 waves of 32x32, LDS-staged operands with a register
 // prefetch of the next K-tile, optional split-K into fp32 slabs (reduced by k_reduce_slabs
 // with the epilogue) and an optional fused column sum of the B operand (bias gradients).
-#include <cstdlib>
 #include "gemm.h"
 
 #define BM 64
@@ -110,142 +109,6 @@ __global__ void __launch_bounds__(256) k_gemm_f32(GemmArgs g) {
   if (do_colsum && tid < BN && n0 + tid < g.N) g.colsum[(int64_t)ks * g.N + n0 + tid] = csum;
 }
 
-// C[M][N] = epi(A B^T) with both operands k-contiguous ("NT": A[m*lda + k], B[n*ldb + k]), K % 16 == 0:
-// the backward's dl2 = (dl3 W^T) * (l2 > 0).  256 threads = 2x2 waves of 32x32 (2x2 16x16 tiles),
-// operands straight from global/L1 as 16-byte k-permuted loads (mfma_k16), two k blocks in flight,
-// four independent accumulator chains.
-__global__ void __launch_bounds__(256) k_gemm_nt(GemmArgs g) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int i16 = lane & 15, j4 = lane >> 4;
-  const int m0 = blockIdx.y * 64 + (w >> 1) * 32, n0 = blockIdx.x * 64 + (w & 1) * 32;
-  const float* pa[2];
-  const float* pb[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    pa[t] = g.A + (int64_t)min(m0 + 16 * t + i16, g.M - 1) * g.lda + 4 * j4;
-    pb[t] = g.B + (int64_t)min(n0 + 16 * t + i16, g.N - 1) * g.ldb + 4 * j4;
-  }
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int nb = g.K / 16;
-  f32x4 a0[2], b0[2], a1[2], b1[2];
-  auto load = [&](int kb, f32x4 (&a)[2], f32x4 (&b)[2]) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      a[t] = *(const f32x4*)(pa[t] + 16 * kb);
-      b[t] = *(const f32x4*)(pb[t] + 16 * kb);
-    }
-  };
-  auto mma = [&](const f32x4 (&a)[2], const f32x4 (&b)[2]) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mfma_k16(a[i], b[j], acc[i][j]);
-  };
-  load(0, a0, b0);
-  for (int kb = 0; kb < nb; kb += 2) {
-    if (kb + 1 < nb) load(kb + 1, a1, b1);
-    mma(a0, b0);
-    if (kb + 2 < nb) load(kb + 2, a0, b0);
-    if (kb + 1 < nb) mma(a1, b1);
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = n0 + 16 * j + i16;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + 16 * i + 4 * j4 + r;
-        if (row < g.M && col < g.N) {
-          float v = acc[i][j][r];
-          if (g.epi == EPI_BIAS_RELU) v = fmaxf(v + g.bias[col], 0.f);
-          else if (g.epi == EPI_BIAS) v = v + g.bias[col];
-          else if (g.epi == EPI_MASK) v = g.mask[(int64_t)row * g.ldm + col] > 0.f ? v : 0.f;
-          g.C[(int64_t)row * g.ldc + col] = v;
-        }
-      }
-    }
-}
-
-// C[M][N] = sum_k A[k*lda + m] B[k*ldb + n] -- the weight gradients X^T Y over the batch ("TN"),
-// M % 4 == N % 4 == 0.  One wave per 64x64 tile: lane (i16, j4) loads the 16-byte A[k][m0 + 4 i16 ..]
-// and B[k][n0 + 4 i16 ..] at k = k0 + j4, which feed the 4x4 16x16 tiles whose rows are
-// m0 + 4 r + sa and columns n0 + 4 c + sb (a row / column permutation the stores undo): 16 MFMAs per
-// two 16-byte loads, no LDS.  Split-K over blockIdx.z into slabs (k_reduce_slabs); optional column
-// sums of B (bias gradients) from the m-tile-0 waves.
-__global__ void __launch_bounds__(64) k_gemm_tn(GemmArgs g) {
-  const int lane = threadIdx.x, i16 = lane & 15, j4 = lane >> 4;
-  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
-  const int ks = blockIdx.z;
-  const int kbeg = ks * g.kchunk, kend = min(g.K, kbeg + g.kchunk);
-  const bool mv = m0 + 4 * i16 < g.M, nv = n0 + 4 * i16 < g.N;
-  const float* pa = g.A + m0 + 4 * i16;
-  const float* pb = g.B + n0 + 4 * i16;
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  f32x4 cs = {0.f, 0.f, 0.f, 0.f};
-  const bool do_colsum = g.colsum != nullptr && blockIdx.y == 0;
-  // one iteration = 16 k (4 MFMA k-steps); two iterations' operands in flight
-  f32x4 a0[4], b0[4], a1[4], b1[4];
-  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  auto load = [&](int k0, f32x4 (&a)[4], f32x4 (&b)[4]) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int k = k0 + 4 * q + j4;
-      const bool kv = k < kend;
-      a[q] = kv && mv ? *(const f32x4*)(pa + (int64_t)k * g.lda) : z4;
-      b[q] = kv && nv ? *(const f32x4*)(pb + (int64_t)k * g.ldb) : z4;
-    }
-  };
-  auto mma = [&](const f32x4 (&a)[4], const f32x4 (&b)[4]) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int sa = 0; sa < 4; ++sa)
-#pragma unroll
-        for (int sb = 0; sb < 4; ++sb)
-          acc[sa][sb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q][sa], b[q][sb], acc[sa][sb], 0, 0, 0);
-      if (do_colsum) cs += b[q];
-    }
-  };
-  if (kbeg < kend) load(kbeg, a0, b0);
-  for (int k0 = kbeg; k0 < kend; k0 += 32) {
-    const bool has1 = k0 + 16 < kend;
-    if (has1) load(k0 + 16, a1, b1);
-    mma(a0, b0);
-    if (k0 + 32 < kend) load(k0 + 32, a0, b0);
-    if (has1) mma(a1, b1);
-  }
-  float* out = g.nsplit > 1 ? g.slab + (int64_t)ks * g.M * g.N : g.C;
-  const int64_t ld = g.nsplit > 1 ? g.N : g.ldc;
-  if (nv) {
-#pragma unroll
-    for (int sa = 0; sa < 4; ++sa)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = m0 + 16 * j4 + 4 * q + sa;    // tile row r = 4 j4 + q -> m0 + 4 r + sa
-        if (m < g.M)
-          *(f32x4*)(out + (int64_t)m * ld + n0 + 4 * i16) =
-              (f32x4){acc[sa][0][q], acc[sa][1][q], acc[sa][2][q], acc[sa][3][q]};
-      }
-  }
-  if (do_colsum) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      cs[s] += __shfl_xor(cs[s], 16, 64);
-      cs[s] += __shfl_xor(cs[s], 32, 64);
-    }
-    if (j4 == 0 && nv) *(f32x4*)(g.colsum + (int64_t)ks * g.N + n0 + 4 * i16) = cs;
-  }
-}
-
 // dst[row*ldc + col] = epi(scale * sum_s slab[s][row][col])
 __global__ void k_reduce_slabs(const float* __restrict__ slab, int nsplit, int M, int N,
                                float* __restrict__ C, int64_t ldc, int epi,
@@ -279,32 +142,11 @@ int a3c_gemm(bool a_kc, bool b_nc, GemmArgs g, hipStream_t s) {
       (((uintptr_t)g.A | (uintptr_t)g.B) & 15) || (a_kc ? 0 : (g.M & 3)) || (b_nc ? (g.N & 3) : 0))
     return a3c_set_error(A3C_ERR_INVALID, "a3c_gemm", "unaligned operands (need 16-B alignment, dims %4)");
   if (g.nsplit < 1) g.nsplit = 1;
-  static const bool nt_off = getenv("A3C_GEMM_NT") && atoi(getenv("A3C_GEMM_NT")) == 0;
-  if (a_kc && !b_nc && g.nsplit == 1 && g.K % 16 == 0 && g.K > 0 && !nt_off) {
-    hipLaunchKernelGGL(k_gemm_nt, dim3((g.N + 63) / 64, (g.M + 63) / 64), dim3(256), 0, s, g);
-    A3C_CHECK(hipGetLastError());
-    return 0;
-  }
   int ktiles = (g.K + BK - 1) / BK;
   int per = (ktiles + g.nsplit - 1) / g.nsplit;
   g.kchunk = per * BK;
   g.nsplit = (ktiles + per - 1) / per;
   if (g.nsplit > 1 && !g.slab) return a3c_set_error(A3C_ERR_INVALID, "a3c_gemm", "split-K needs a slab");
-  static const bool tn_off = getenv("A3C_GEMM_TN") && atoi(getenv("A3C_GEMM_TN")) == 0;
-  if (!a_kc && b_nc && g.epi == EPI_STORE && (g.M & 3) == 0 && (g.N & 3) == 0 && (g.ldc & 3) == 0 &&
-      (((uintptr_t)g.C | (uintptr_t)(g.slab ? g.slab : g.C) | (uintptr_t)(g.colsum ? g.colsum : g.C)) & 15) == 0 &&
-      !tn_off) {
-    dim3 grid((g.N + 63) / 64, (g.M + 63) / 64, g.nsplit);
-    hipLaunchKernelGGL(k_gemm_tn, grid, dim3(64), 0, s, g);
-    A3C_CHECK(hipGetLastError());
-    if (g.nsplit > 1) {
-      int64_t total = (int64_t)g.M * g.N;
-      hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                         g.slab, g.nsplit, g.M, g.N, g.C, g.ldc, g.epi, g.bias, g.mask, g.ldm);
-      A3C_CHECK(hipGetLastError());
-    }
-    return 0;
-  }
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, g.nsplit);
   if (a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32<true, true>), grid, dim3(256), 0, s, g);
   else if (a_kc && !b_nc) hipLaunchKernelGGL((k_gemm_f32<true, false>), grid, dim3(256), 0, s, g);

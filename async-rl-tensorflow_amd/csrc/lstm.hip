@@ -35,6 +35,16 @@ int a3c_lstm_transpose_launch(const float* W, float* Wt, hipStream_t s) {
   return 0;
 }
 
+// k-permuted fp32 MFMA step: in 16x16x4 step s of a 16-wide k block kb, lane (i16, j4) supplies
+// A[row i16][kb + 4 j4 + s] and B[kb + 4 j4 + s][col i16] -- every k of the block exactly once,
+// and each lane's four k are contiguous in memory for row-major A and for B given as B^T rows,
+// so both operands arrive as one 16-byte load per lane per four MFMAs.
+__device__ inline f32x4 mfma_k16(const f32x4 a, const f32x4 b, f32x4 c) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], c, 0, 0, 0);
+  return c;
+}
+
 // cell step: workgroup = 16 envs x 16 units x 4 gates, 8 waves = (gate g, K half kh): kh 0 runs
 // x @ W[0:256], kh 1 runs h_prev @ W[256:512] (rows of terminal-masked envs zeroed afterwards:
 // (keep h) W = keep (h W)).  All 16 k-blocks of both operands are loaded up front.
@@ -212,7 +222,7 @@ struct LstmWs {
 static LstmWs lstm_ws(int n, int64_t E) {
   LstmWs w;
   const int64_t nE = (int64_t)n * E;
-  w.split_dw = a3c_gemm_effective_split((int)nE, a3c_gemm_plan_split(FC, LSTM_G, (int)nE, 1024));
+  w.split_dw = a3c_gemm_effective_split((int)nE, a3c_gemm_plan_split(FC, LSTM_G, (int)nE, 256));
   int64_t o = 0;
   auto take = [&](int64_t floats) { int64_t r = o; o += (floats + 63) & ~(int64_t)63; return r; };
   w.da = take(nE * LSTM_G);

@@ -542,9 +542,8 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   if (p.nwg < 1) p.nwg = 1;
   p.per_wg = (int)((B + p.nwg - 1) / p.nwg);
   p.nwg = (int)((B + p.per_wg - 1) / p.per_wg);
-  // weight-gradient GEMMs run one wave per 64x64 tile (k_gemm_tn): split K for ~2 waves per SIMD
   p.head_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FC, L.zs, (int)B, 128));
-  p.fc_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FLAT, FC, (int)B, 2048));
+  p.fc_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FLAT, FC, (int)B, 512));
   p.dz = take(B * L.zs);
   p.dh3 = take(B * FC);
   p.dl2 = take(B * FLAT);
