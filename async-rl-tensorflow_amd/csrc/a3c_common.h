@@ -89,3 +89,22 @@ __device__ inline const uint8_t* state_plane(const StateAddr& a, int64_t b, int 
   if (slot < 0) slot += a.R;
   return a.base + e * a.env_stride + slot * a.plane_bytes;
 }
+
+// Debug builds only (-DA3C_WG_TIMES, tools/wg_times.py): every workgroup writes its start and
+// end s_memrealtime stamps (100 MHz, one clock for the whole chip) as two u64 at `dst`, a
+// location of the kernel's own output that the caller then reads back -- the dispatch skew and
+// the per-workgroup duration of one launch.
+#ifdef A3C_WG_TIMES
+#define WG_T0() const uint64_t wg_t0_ = __builtin_amdgcn_s_memrealtime()
+#define WG_T1(dst)                                                    \
+  do {                                                                \
+    __syncthreads();                                                  \
+    if (threadIdx.x == 0) {                                           \
+      ((uint64_t*)(dst))[0] = wg_t0_;                                 \
+      ((uint64_t*)(dst))[1] = __builtin_amdgcn_s_memrealtime();       \
+    }                                                                 \
+  } while (0)
+#else
+#define WG_T0() ((void)0)
+#define WG_T1(dst) ((void)0)
+#endif

@@ -805,7 +805,11 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
     int rc0 = a3c_prep_fwd_launch(L, e->params, sl.prep, s);
     if (rc0) return rc0;
   }
+  // head_screen: each launch shifts the frame indices (frame_salt) so it streams frames that are
+  // not cache-resident, like the live rollout (re-reading one frame set would time MALL hits)
+  uint32_t salt = 0;
   auto launch = [&]() -> int {
+    salt += 4099u;
     switch (kernel) {
       case A3C_KER_CONV12_FWD:
         return a3c_conv12_launch(L, e->params, sl.prep, ring_addr(e, 0, e->counters), E, sl.act_l1, sl.act_l2, s);
@@ -829,6 +833,7 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
         sel.rewards = sl.rewards; sel.terms = sl.terms;
         sel.frames_out = sl.frames;
         sel.pool = e->pool; sel.ring = e->ring; sel.R = e->R;
+        sel.frame_salt = salt;
         return a3c_head_screen_launch(L, e->params, L.lstm ? sl.lh : sl.act_l3, E, sl.z, sel, s);
       }
       case A3C_KER_CONV_BWD: {

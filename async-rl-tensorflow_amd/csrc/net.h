@@ -113,6 +113,10 @@ struct HeadSelect {
   const uint8_t* pool;
   uint8_t* ring;
   int R;
+  // measurement only (a3c_engine_time_kernel): offsets the post-act frame index so that every
+  // timed launch streams a different set of frames from HBM, as the live rollout does; 0 in
+  // every product launch
+  uint32_t frame_salt;
 };
 
 // forward of B states; returns 0 or error

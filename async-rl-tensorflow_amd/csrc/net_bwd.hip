@@ -1,3 +1,4 @@
+#include <algorithm>
 #include <cstdlib>
 // Loss + backward of the NIPS trunk on gfx950.
 //
@@ -198,6 +199,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
   const int64_t tau0 = sa.tau_ptr ? *sa.tau_ptr : 0;
   const int64_t b0 = (int64_t)blockIdx.x * per_wg;
   const int64_t b1 = min(B, b0 + per_wg);
+  WG_T0();
 
   // parity class of this wave for dl1: (py, px); with 8 waves two waves share a class and
   // split its 7 M-tiles (0-3 / 4-6)
@@ -472,6 +474,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     out[CB_OFF_B1 + tid] = v;
   }
   if (tid < C2_N) out[CB_OFF_B2 + tid] = db2acc;
+  WG_T1(act_l1 + b0 * C1_P * C1_N);   // debug: over this workgroup's own (consumed) l1 rows
 }
 
 // ---------------------------------------------------------------------------------------
@@ -532,16 +535,23 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   BwdPlan p;
   int64_t o = 0;
   auto take = [&](int64_t floats) { int64_t r = o; o += (floats + 63) & ~(int64_t)63; return r; };
-  // conv-backward workgroups: one per CU when the backward owns the GPU; in overlap mode ~7/8 of
-  // the CUs (224 -> 6 samples per workgroup at B = 1280) so the concurrent rollout keeps some
-  // CUs to itself (measured: 3.22M vs 3.15M env-steps/s at 256).  The workspace is sized for
-  // the larger count (a3c_bwd_plan with shared = false).
+  // conv-backward workgroups: one per CU when the backward owns the GPU (the 144 KB LDS-DMA
+  // kernel fits once per CU); in overlap mode 448 compact (74 KB) workgroups, two per CU on 224
+  // CUs, so each CU interleaves two workgroups' barrier and load waits while ~1/8 of the CUs stay
+  // free for the concurrent rollout (measured on MI355X: conv_bwd 132.5 -> 92.3 us isolated at
+  // B = 1280, the same env-steps/s live).  The slab workspace is sized for the larger count, so
+  // the plan's offsets do not depend on the mode.
   static const int env_nwg = getenv("A3C_CB_NWG") ? atoi(getenv("A3C_CB_NWG")) : 0;
-  const int nwg_max = env_nwg ? env_nwg : (a3c_shared_gpu() ? 224 : 256);
-  p.nwg = (int)(B < nwg_max ? B : nwg_max);
-  if (p.nwg < 1) p.nwg = 1;
-  p.per_wg = (int)((B + p.nwg - 1) / p.nwg);
-  p.nwg = (int)((B + p.per_wg - 1) / p.per_wg);
+  const int nwg_shared = env_nwg ? env_nwg : 448, nwg_own = env_nwg ? env_nwg : 256;
+  auto count = [&](int nwg_max, int& per) {
+    int nwg = (int)(B < nwg_max ? B : nwg_max);
+    if (nwg < 1) nwg = 1;
+    per = (int)((B + nwg - 1) / nwg);
+    return (int)((B + per - 1) / per);
+  };
+  int per_alloc = 0;
+  const int nwg_alloc = std::max(count(nwg_shared, per_alloc), count(nwg_own, per_alloc));
+  p.nwg = count(a3c_shared_gpu() ? nwg_shared : nwg_own, p.per_wg);
   p.head_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FC, L.zs, (int)B, 128));
   p.fc_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FLAT, FC, (int)B, 512));
   p.dz = take(B * L.zs);
@@ -553,9 +563,9 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   p.hslab = take(p.head_split > 1 ? (int64_t)p.head_split * FC * L.zs : 0);
   p.fccol = take((int64_t)p.fc_split * FC);
   p.fcslab = take(p.fc_split > 1 ? (int64_t)p.fc_split * FLAT * FC : 0);
-  p.cslab = take((int64_t)p.nwg * CB_SLAB);
+  p.cslab = take((int64_t)nwg_alloc * CB_SLAB);
   p.groups = p.nwg < 16 ? p.nwg : 16;
-  p.cgroup = take((int64_t)p.groups * CB_SLAB);
+  p.cgroup = take((int64_t)16 * CB_SLAB);    // groups <= 16 in either mode
   p.total = o;
   return p;
 }

@@ -90,6 +90,7 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i16 = lane & 15, j4 = lane >> 4;
   const int64_t tau0 = sa.tau_ptr ? *sa.tau_ptr : 0;
+  WG_T0();
 
   // stage: u8 planes -> bf16 planes (integers 0..255 are exact in bf16).  EW: all of a thread's
   // loads issued before the first conversion; otherwise a load-convert loop (fewer live VGPRs)
@@ -221,6 +222,7 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
       if (q < C2_Q) act_l2[b * FLAT + q * C2_N + 16 * nt + i16] = fmaxf(acc2[mi][r] + bias2, 0.f);
     }
   }
+  WG_T1(act_l2 + b * FLAT);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -415,6 +417,7 @@ __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restr
   const int64_t tau = *sel.tau_ptr + sel.tau_add;
   const int e = (int)b;
   const int64_t nxt = ((tau + 1) & 1) * (int64_t)sel.par_E + e;
+  WG_T0();
 #ifdef HS_TIMES
   uint64_t* dbg = blockIdx.x == HS_TIMES ? (uint64_t*)z : nullptr;
   if (dbg && threadIdx.x == 0) dbg[0] = __builtin_readcyclecounter();
@@ -456,7 +459,7 @@ __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restr
   __syncthreads();
   int32_t frame;
   if (sel.env_on) {
-    frame = env_frame_of(s_draw, (uint32_t)s_act, sel.envp);
+    frame = env_frame_of(s_draw + sel.frame_salt, (uint32_t)s_act, sel.envp);
     if (threadIdx.x == 0) {
       sel.frames_out[e] = frame;
       if (!s_term) sel.envb.frame[nxt] = frame;
@@ -472,6 +475,7 @@ __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restr
 #endif
   atari::screen_frame<HS_THREADS>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3),
                                   sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE, smem);
+  WG_T1(z + b * zs);
 }
 
 __global__ void __launch_bounds__(256) k_select(const float* __restrict__ z, int64_t B, int zs, int A,
@@ -593,9 +597,13 @@ __global__ void __launch_bounds__(64 * NW) k_fc_fwd(const float* __restrict__ A,
   const int ct = blockIdx.x;
   const int m0 = blockIdx.y * 16, n0 = ct * 16;
   const int m = min(m0 + i16, M - 1);
+  WG_T0();
   // chunks [c0, c1) of this wave: the 162 chunks split as evenly as possible
   const int c0 = (wid * FC_CH) / NW, c1 = ((wid + 1) * FC_CH) / NW;
-  constexpr int D = 8;
+#ifndef FC_D
+#define FC_D 8
+#endif
+  constexpr int D = FC_D;
   const float* a = A + (int64_t)m * FLAT + 4 * j4;
   const f32x4* b = (const f32x4*)Wp + (int64_t)ct * FC_CH * 64 + lane;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -636,6 +644,7 @@ __global__ void __launch_bounds__(64 * NW) k_fc_fwd(const float* __restrict__ A,
       if (row < M) C[(int64_t)row * FC + n] = fmaxf(acc[r] + bb, 0.f);
     }
   }
+  WG_T1(C + (int64_t)m0 * FC + n0);   // debug: the tile's first 4 outputs
 }
 
 // row-major-weight variant (4 scalar B loads per chunk), kept for A/B measurement
