@@ -46,6 +46,10 @@ struct Slot {
   float* lwt;              // LSTM gate matrix of P, transposed for the forward (rollout start)
 };
 
+// graphs: 0 sync rollout+grad; 1, 2 rollout of slot 0, 1; 3, 4 grad of slot 0, 1; and with the
+// apply fused (a3c_engine_iterate, world_size 1): 5 sync rollout+grad+apply; 6, 7 grad+apply
+// (+ the parameter snapshot) of slot 0, 1
+#define NGRAPH 8
 struct a3c_engine {
   a3c_engine_config cfg;
   NetLayout L;
@@ -74,9 +78,9 @@ struct a3c_engine {
   float* sched;            // [0] lr, [1] target-sync flag (device)
   TensorTab tt;
   // sync: one graph (rollout + grad); overlap: rollout and grad graphs per slot
-  hipGraph_t graph[5];
-  hipGraphExec_t gexec[5];
-  bool captured[5];
+  hipGraph_t graph[NGRAPH];
+  hipGraphExec_t gexec[NGRAPH];
+  bool captured[NGRAPH];
   // overlap pipeline
   hipStream_t rs;          // rollout stream
   hipStream_t gs;          // backward side stream (weight-gradient GEMMs beside the conv backward)
@@ -89,6 +93,7 @@ struct a3c_engine {
   int32_t* ext_idx;        // [E] identity frame index into the staging buffer (pool)
   int64_t iter;            // rollouts issued since reset
   bool grad_ready;         // the last rollout_grad call computed a gradient
+  bool grad_applied;       // ... and a3c_engine_iterate already applied it (apply is then a no-op)
   bool reset_done;
 };
 
@@ -140,7 +145,7 @@ extern "C" void a3c_engine_config_default(a3c_engine_config* c) {
 extern "C" int a3c_engine_destroy(a3c_engine* e) {
   if (!e) return 0;
   if (e->rs) (void)hipStreamSynchronize(e->rs);
-  for (int i = 0; i < 5; ++i)
+  for (int i = 0; i < NGRAPH; ++i)
     if (e->captured[i]) {
       (void)hipGraphExecDestroy(e->gexec[i]);
       (void)hipGraphDestroy(e->graph[i]);
@@ -540,14 +545,36 @@ static int enqueue_rollout_grad(a3c_engine* e, hipStream_t s) {
   return rc ? rc : enqueue_grad(e, e->slot[0], s);
 }
 
-// Graph gi (0: sync rollout+grad; 1, 2: rollout of slot 0, 1; 3, 4: grad of slot 0, 1) is
-// captured on first use (what: 0 rollout+grad, 1 rollout, 2 grad) and launched on s.
+// RMSProp apply (lr from the schedule computed on device), target sync (q) and the counter
+// advance in one launch; world_size == 1: the per-tensor clip as well.  Overlap: then the
+// parameter snapshot of the rollout that will use slot `snap` (the slot just back-propagated).
+static int enqueue_apply(a3c_engine* e, int snap, hipStream_t s) {
+  OptParams op = opt_params(e);
+  op.mode = e->cfg.world_size > 1 ? OPT_APPLY : (OPT_CLIP | OPT_APPLY);
+  int rc = a3c_apply_launch(e->params, e->ms, e->mom, e->grads, e->tt, op, e->opt_part,
+                            e->cfg.world_size > 1 ? nullptr : e->sumsq, s);
+  if (rc || !e->overlap) return rc;
+  A3C_CHECK(hipMemcpyAsync(e->slot[snap].P, e->params, e->L.total * 4, hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+// Graph gi (see NGRAPH) is captured on first use (what: 0 rollout+grad, 1 rollout, 2 grad,
+// 3 grad+apply, 4 rollout+grad+apply) and launched on s.
 static int run_graph(a3c_engine* e, int gi, int what, int slot, hipStream_t s) {
-  if (gi < 0 || gi >= 5) return a3c_set_error(A3C_ERR_INVALID, "run_graph", "graph index");
+  if (gi < 0 || gi >= NGRAPH) return a3c_set_error(A3C_ERR_INVALID, "run_graph", "graph index");
   auto enqueue = [&](hipStream_t cs) -> int {
-    if (what == 0) return enqueue_rollout_grad(e, cs);
-    if (what == 1) return enqueue_rollout(e, e->slot[slot], cs);
-    return enqueue_grad(e, e->slot[slot], cs);
+    int rc;
+    switch (what) {
+      case 0: return enqueue_rollout_grad(e, cs);
+      case 1: return enqueue_rollout(e, e->slot[slot], cs);
+      case 2: return enqueue_grad(e, e->slot[slot], cs);
+      case 3:
+        rc = enqueue_grad(e, e->slot[slot], cs);
+        return rc ? rc : enqueue_apply(e, slot, cs);
+      default:
+        rc = enqueue_rollout_grad(e, cs);
+        return rc ? rc : enqueue_apply(e, 0, cs);
+    }
   };
   if (!e->cfg.use_graph) return enqueue(s);
   if (!e->captured[gi]) {
@@ -604,16 +631,16 @@ extern "C" int a3c_engine_reset(a3c_engine* e, const float* host_params, void* s
     }
   e->iter = 0;
   e->grad_ready = false;
+  e->grad_applied = false;
   e->reset_done = true;
   e->ext_t = 0;
   e->ext_begun = false;
   return 0;
 }
 
-extern "C" int a3c_engine_rollout_grad(a3c_engine* e, void* stream) {
-  if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_rollout_grad", "null");
-  if (!e->reset_done) return a3c_set_error(A3C_ERR_STATE, "a3c_engine_rollout_grad", "call a3c_engine_reset first");
-  hipStream_t s = (hipStream_t)stream;
+// rollout + gradient (fused = 0), or rollout + gradient + apply (fused = 1: world_size 1, the
+// apply captured in the same graphs -- a3c_engine_iterate)
+static int rollout_grad(a3c_engine* e, hipStream_t s, bool fused) {
   if (e->ext) {
     // external envs: the n steps were driven by ext_act / ext_observe; bootstrap + grad here
     if (e->ext_t != e->n)
@@ -621,17 +648,19 @@ extern "C" int a3c_engine_rollout_grad(a3c_engine* e, void* stream) {
     int rc = enqueue_rollout_end(e, e->slot[0], s);
     if (!rc) rc = run_graph(e, 3, 2, 0, s);
     e->grad_ready = rc == 0;
+    e->grad_applied = false;
     e->ext_t = 0;
     return rc;
   }
   if (!e->overlap) {
-    int rc = run_graph(e, 0, 0, 0, s);
+    int rc = fused ? run_graph(e, 5, 4, 0, s) : run_graph(e, 0, 0, 0, s);
     e->grad_ready = rc == 0;
+    e->grad_applied = fused;
     return rc;
   }
   // overlap: rollout k (slot p) on the engine's rollout stream, after everything the caller
   // enqueued so far -- in steady state the apply of rollout k-2, which also left the parameter
-  // snapshot of rollout k in slot p (a3c_engine_apply); the backward of rollout k-1 (slot p^1) on
+  // snapshot of rollout k in slot p (enqueue_apply); the backward of rollout k-1 (slot p^1) on
   // the caller's stream once that rollout is complete.
   const int p = (int)(e->iter & 1);
   const Slot& sl = e->slot[p];
@@ -644,12 +673,31 @@ extern "C" int a3c_engine_rollout_grad(a3c_engine* e, void* stream) {
   e->grad_ready = false;
   if (e->iter >= 1) {
     A3C_CHECK(hipStreamWaitEvent(s, e->ev_roll[p ^ 1], 0));
-    rc = run_graph(e, 3 + (p ^ 1), 2, p ^ 1, s);
+    rc = fused ? run_graph(e, 6 + (p ^ 1), 3, p ^ 1, s) : run_graph(e, 3 + (p ^ 1), 2, p ^ 1, s);
     if (rc) return rc;
     e->grad_ready = true;
+    e->grad_applied = fused;
   }
   e->iter += 1;
   return 0;
+}
+
+extern "C" int a3c_engine_rollout_grad(a3c_engine* e, void* stream) {
+  if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_rollout_grad", "null");
+  if (!e->reset_done) return a3c_set_error(A3C_ERR_STATE, "a3c_engine_rollout_grad", "call a3c_engine_reset first");
+  return rollout_grad(e, (hipStream_t)stream, false);
+}
+
+// One whole iteration (rollout_grad + apply) for a single-GPU engine, the apply captured into the
+// same hipGraphs (no host-launched kernel between the graph and the apply).  Bit-identical to
+// a3c_engine_rollout_grad followed by a3c_engine_apply.
+extern "C" int a3c_engine_iterate(a3c_engine* e, void* stream) {
+  if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_iterate", "null");
+  if (!e->reset_done) return a3c_set_error(A3C_ERR_STATE, "a3c_engine_iterate", "call a3c_engine_reset first");
+  if (e->ext || e->cfg.world_size != 1)
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_iterate",
+                         "single-GPU device-env engines only (else rollout_grad, exchange, apply)");
+  return rollout_grad(e, (hipStream_t)stream, true);
 }
 
 extern "C" int a3c_engine_grad_ready(a3c_engine* e) { return e && e->grad_ready ? 1 : 0; }
@@ -658,17 +706,11 @@ extern "C" int a3c_engine_grad_ready(a3c_engine* e) { return e && e->grad_ready 
 // advance, all in one launch.  world_size == 1: the per-tensor clip is applied here as well.
 extern "C" int a3c_engine_apply(a3c_engine* e, void* stream) {
   if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_apply", "null");
-  hipStream_t s = (hipStream_t)stream;
-  if (!e->grad_ready) return 0;          // overlap pipeline still filling: nothing to apply
-  OptParams op = opt_params(e);
-  op.mode = e->cfg.world_size > 1 ? OPT_APPLY : (OPT_CLIP | OPT_APPLY);
-  int rc = a3c_apply_launch(e->params, e->ms, e->mom, e->grads, e->tt, op, e->opt_part,
-                            e->cfg.world_size > 1 ? nullptr : e->sumsq, s);
-  if (rc || !e->overlap) return rc;
-  // overlap: parameter snapshot for the next rollout (iter), whose slot's previous rollout
-  // (iter - 2) has just been back-propagated on this stream
-  A3C_CHECK(hipMemcpyAsync(e->slot[e->iter & 1].P, e->params, e->L.total * 4, hipMemcpyDeviceToDevice, s));
-  return 0;
+  // overlap pipeline still filling (no gradient yet), or a3c_engine_iterate applied it already
+  if (!e->grad_ready || e->grad_applied) return 0;
+  // overlap: the snapshot is for the next rollout (iter), whose slot's previous rollout (iter - 2)
+  // has just been back-propagated on this stream
+  return enqueue_apply(e, (int)(e->iter & 1), (hipStream_t)stream);
 }
 
 // ---- external (host) environments (env workers feeding host RGB buffers) ----

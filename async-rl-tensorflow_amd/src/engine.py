@@ -173,6 +173,12 @@ class Engine:
         return bool(lib().a3c_engine_grad_ready(self._h))
 
     def iterate(self, exchange=None):
+        """One iteration: rollout + gradient, [exchange(grads)], apply.  Single-GPU device-env
+        engines without an exchange take the fused path (a3c_engine_iterate: the apply captured
+        into the same hipGraphs, bit-identical to rollout_grad() + apply())."""
+        if exchange is None and self.cfg.world_size == 1 and not self.external_env:
+            check(lib().a3c_engine_iterate(self._h, _lib.stream_handle()), 'a3c_engine_iterate')
+            return
         self.rollout_grad()
         if not self.grad_ready:          # overlap pipeline filling: no gradient yet
             return

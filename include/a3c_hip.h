@@ -299,6 +299,11 @@ int a3c_engine_rollout_grad(a3c_engine* eng, void* stream);
 /* RMSProp apply of grads (lr from the device global step) and advance counters.
  * overlap: a no-op until the pipeline holds a gradient (first call after reset). */
 int a3c_engine_apply(a3c_engine* eng, void* stream);
+/* a3c_engine_rollout_grad + a3c_engine_apply as one enqueue (single GPU, device envs only: no
+ * gradient exchange between them), the apply captured into the same hipGraphs.  Same results
+ * bit for bit; a3c_engine_grad_ready reports as after a3c_engine_rollout_grad, and a following
+ * a3c_engine_apply is a no-op (the gradient is applied already). */
+int a3c_engine_iterate(a3c_engine* eng, void* stream);
 /* 1 if the last a3c_engine_rollout_grad produced a gradient (always, unless overlap and it
  * was the first call after reset) -- exchange / apply only then. */
 int a3c_engine_grad_ready(a3c_engine* eng);

@@ -31,7 +31,7 @@ def test_header_declares_the_boundary():
     fns = declared_functions()
     for f in ('a3c_preprocess_u8', 'a3c_history_push', 'a3c_forward', 'a3c_select_action', 'a3c_returns',
               'a3c_td_target', 'a3c_loss_backward', 'a3c_clip_rmsprop_apply', 'a3c_copy_params',
-              'a3c_engine_create', 'a3c_engine_rollout_grad', 'a3c_engine_apply'):
+              'a3c_engine_create', 'a3c_engine_rollout_grad', 'a3c_engine_apply', 'a3c_engine_iterate'):
         assert f in fns, f
 
 

@@ -142,6 +142,24 @@ def test_engine_deterministic_and_graph_equals_eager():
     assert torch.equal(a.loss, b.loss)
 
 
+@pytest.mark.parametrize('overlap', [False, True])
+def test_fused_iterate_equals_rollout_grad_then_apply(overlap):
+    """a3c_engine_iterate (apply captured into the graphs) == a3c_engine_rollout_grad +
+    a3c_engine_apply, bit for bit (params, RMSProp slots, frames, losses, counters)."""
+    a, _, _ = build('a3c', 6, 16, 5, 0, seed=11, overlap=overlap)
+    b, _, _ = build('a3c', 6, 16, 5, 0, seed=11, overlap=overlap)
+    for _ in range(5):
+        a.iterate()                       # fused path
+        b.rollout_grad()                  # split path
+        assert a.grad_ready == b.grad_ready
+        if b.grad_ready:
+            b.apply()
+        a.apply()                         # no-op: the fused iterate applied already
+    torch.cuda.synchronize()
+    for name in ('params', 'ms', 'mom', 'frame_ring', 'loss', 'counters'):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+
+
 def test_engine_bench_shape_runs():
     """The bench configuration (Pong, 256 envs, n=5) runs and stays finite."""
     eng, _, ns = build('a3c', 6, 256, 5, 0, seed=123, frames=256, scale=1.0)
