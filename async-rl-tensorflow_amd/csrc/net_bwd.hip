@@ -536,13 +536,14 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   int64_t o = 0;
   auto take = [&](int64_t floats) { int64_t r = o; o += (floats + 63) & ~(int64_t)63; return r; };
   // conv-backward workgroups: one per CU when the backward owns the GPU (the 144 KB LDS-DMA
-  // kernel fits once per CU); in overlap mode 448 compact (74 KB) workgroups, two per CU on 224
-  // CUs, so each CU interleaves two workgroups' barrier and load waits while ~1/8 of the CUs stay
-  // free for the concurrent rollout (measured on MI355X: conv_bwd 132.5 -> 92.3 us isolated at
-  // B = 1280, the same env-steps/s live).  The slab workspace is sized for the larger count, so
-  // the plan's offsets do not depend on the mode.
+  // kernel fits once per CU); in overlap mode 224 compact (74 KB) workgroups, one per CU on 7/8
+  // of the CUs, so that each CU keeps LDS for a concurrent rollout workgroup (conv12's 60 KB u8
+  // variant, head_screen's 54 KB).  Measured on MI355X (Pong, 256 envs): 3.70M env-steps/s vs
+  // 3.45M with 448 two-per-CU workgroups (those alone are faster, 92 vs 132 us, but leave no LDS
+  // for the rollout).  The slab workspace is sized for the larger count, so the plan's offsets
+  // do not depend on the mode.
   static const int env_nwg = getenv("A3C_CB_NWG") ? atoi(getenv("A3C_CB_NWG")) : 0;
-  const int nwg_shared = env_nwg ? env_nwg : 448, nwg_own = env_nwg ? env_nwg : 256;
+  const int nwg_shared = env_nwg ? env_nwg : 224, nwg_own = env_nwg ? env_nwg : 256;
   auto count = [&](int nwg_max, int& per) {
     int nwg = (int)(B < nwg_max ? B : nwg_max);
     if (nwg < 1) nwg = 1;

@@ -22,6 +22,7 @@
 #define XB_BYTES (HIST * PLANE * 2)                  // 56448: state planes as bf16
 #define L1S_BYTES (C1_P * L1S_LD * 4)                // 32000
 #define CONV12_SMEM (XB_BYTES + L1S_BYTES)           // 88448
+#define CONV12_SMEM_U8 (HIST * PLANE + L1S_BYTES)    // 60224: u8 planes, converted per operand
 
 // ---------------------------------------------------------------------------------------
 // conv1 weights as three bf16 terms.  A u8 pixel is exact in bf16, so conv1 runs on the bf16
@@ -75,7 +76,25 @@ int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipSt
 // of 16 positions x K = 256 (8 steps of (kh; cin x kw 0..7)) on v_mfma_f32_16x16x32_bf16 with the
 // three weight terms; conv1 + relu to LDS (and HBM when the backward needs it); conv2 (4x4/2,
 // 16->32, K = 256) in fp32 MFMA from LDS, 12 (M-tile, N-tile) pairs over the 8 waves.
-template <bool SAVE_L1, bool EW>
+// 8 u8 pixels (two dwords, little-endian) -> 8 bf16 (integers 0..255 are exact in bf16: the
+// upper half of the f32)
+__device__ inline bf16x8 u8x8_to_bf16(uint32_t d0, uint32_t d1) {
+  uint32_t o[4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t d = h ? d1 : d0;
+    const float f0 = (float)(d & 255u), f1 = (float)((d >> 8) & 255u);
+    const float f2 = (float)((d >> 16) & 255u), f3 = (float)(d >> 24);
+    o[2 * h] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
+    o[2 * h + 1] = __builtin_amdgcn_perm(__float_as_uint(f3), __float_as_uint(f2), 0x07060302u);
+  }
+  return __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
+}
+
+// U8: the planes stay u8 in LDS (28 KB instead of 56 KB) and each conv1 A operand is converted
+// to bf16 in registers (8 pixels: 2 ds_read_b32 + 8 v_cvt_f32_ubyte + 4 v_perm) -- a 60 KB
+// footprint, so a workgroup co-resides on a CU with the concurrent backward's (overlap mode).
+template <bool SAVE_L1, bool EW, bool U8>
 __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
                                                     const uint16_t* __restrict__ w1s,
                                                     const float* __restrict__ b1,
@@ -85,7 +104,8 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
                                                     float* __restrict__ act_l2) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint16_t* xb = (uint16_t*)smem;
-  float* l1s = (float*)(smem + XB_BYTES);
+  uint8_t* x8 = smem;
+  float* l1s = (float*)(smem + (U8 ? HIST * PLANE : XB_BYTES));
   const int64_t b = blockIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i16 = lane & 15, j4 = lane >> 4;
@@ -97,6 +117,10 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
   constexpr int NCH = HIST * (PLANE / 16);             // 1764 chunks of 16 pixels
   constexpr int PER = (NCH + 511) / 512;               // 4
   auto stage_chunk = [&](int i, const uint4 v) {
+    if constexpr (U8) {                                // planes are contiguous: chunk i at 16 i
+      ((uint4*)x8)[i] = v;
+      return;
+    }
     const int c = i / (PLANE / 16), j = i - c * (PLANE / 16);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint32_t o[8];
@@ -156,12 +180,19 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
     const int p = 16 * m + i16;
     const int oy = p / C1_O, ox = p - oy * C1_O;
     const uint16_t* row = xb + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;    // cin = j4
+    const uint8_t* row8 = x8 + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accb = {0.f, 0.f, 0.f, 0.f};   // two chains by kh parity
 #pragma unroll
     for (int kh = 0; kh < C1_K; ++kh) {
-      const uint2* q = (const uint2*)(row + kh * IMG);                        // 8-byte aligned
-      const uint2 lo = q[0], hi = q[1];
-      const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      bf16x8 a;
+      if constexpr (U8) {
+        const uint32_t* q = (const uint32_t*)(row8 + kh * IMG);              // 4-byte aligned
+        a = u8x8_to_bf16(q[0], q[1]);
+      } else {
+        const uint2* q = (const uint2*)(row + kh * IMG);                      // 8-byte aligned
+        const uint2 lo = q[0], hi = q[1];
+        a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
       f32x4& c = (kh & 1) ? accb : acc;
       c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][0], c, 0, 0, 0);
       c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][1], c, 0, 0, 0);
@@ -543,15 +574,24 @@ int a3c_conv12_launch(const NetLayout& L, const float* P, const uint8_t* prep, c
   if (!prep) return a3c_set_error(A3C_ERR_INVALID, "a3c_conv12_launch", "prepared forward weights missing");
   const uint16_t* w1s = (const uint16_t*)prep;
   const bool ew = !a3c_shared_gpu();
+  // overlap mode: the 60 KB u8-plane variant (co-resides with the backward's workgroups)
+  static const int env_u8 = getenv("A3C_C12_U8") ? atoi(getenv("A3C_C12_U8")) : -1;
+  const bool u8 = env_u8 >= 0 ? env_u8 != 0 : !ew;
 #define CONV12_ARGS sa, B, w1s, P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2
-  if (act_l1 && ew)
-    hipLaunchKernelGGL((k_conv12_fwd<true, true>), dim3((unsigned)B), dim3(512), CONV12_SMEM, s, CONV12_ARGS);
-  else if (act_l1)
-    hipLaunchKernelGGL((k_conv12_fwd<true, false>), dim3((unsigned)B), dim3(512), CONV12_SMEM, s, CONV12_ARGS);
-  else if (ew)
-    hipLaunchKernelGGL((k_conv12_fwd<false, true>), dim3((unsigned)B), dim3(512), CONV12_SMEM, s, CONV12_ARGS);
-  else
-    hipLaunchKernelGGL((k_conv12_fwd<false, false>), dim3((unsigned)B), dim3(512), CONV12_SMEM, s, CONV12_ARGS);
+#define CONV12_GO(S, E, U) \
+  hipLaunchKernelGGL((k_conv12_fwd<S, E, U>), dim3((unsigned)B), dim3(512), U ? CONV12_SMEM_U8 : CONV12_SMEM, s, CONV12_ARGS)
+  if (u8) {
+    if (act_l1 && ew) CONV12_GO(true, true, true);
+    else if (act_l1) CONV12_GO(true, false, true);
+    else if (ew) CONV12_GO(false, true, true);
+    else CONV12_GO(false, false, true);
+  } else {
+    if (act_l1 && ew) CONV12_GO(true, true, false);
+    else if (act_l1) CONV12_GO(true, false, false);
+    else if (ew) CONV12_GO(false, true, false);
+    else CONV12_GO(false, false, false);
+  }
+#undef CONV12_GO
 #undef CONV12_ARGS
   A3C_CHECK(hipGetLastError());
   return 0;
@@ -565,14 +605,12 @@ int a3c_select_launch(const float* z, int64_t B, int zs, int A, const HeadSelect
 }
 
 void a3c_conv12_set_smem() {
-  (void)hipFuncSetAttribute((const void*)k_conv12_fwd<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            CONV12_SMEM);
-  (void)hipFuncSetAttribute((const void*)k_conv12_fwd<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            CONV12_SMEM);
-  (void)hipFuncSetAttribute((const void*)k_conv12_fwd<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            CONV12_SMEM);
-  (void)hipFuncSetAttribute((const void*)k_conv12_fwd<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            CONV12_SMEM);
+#define C12_SMEM(S, E, U)                                                                        \
+  (void)hipFuncSetAttribute((const void*)k_conv12_fwd<S, E, U>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                            U ? CONV12_SMEM_U8 : CONV12_SMEM)
+  C12_SMEM(true, true, false); C12_SMEM(true, false, false); C12_SMEM(false, true, false); C12_SMEM(false, false, false);
+  C12_SMEM(true, true, true); C12_SMEM(true, false, true); C12_SMEM(false, true, true); C12_SMEM(false, false, true);
+#undef C12_SMEM
   (void)hipFuncSetAttribute((const void*)k_head_screen<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             SCREEN_FRAME_SMEM);
   (void)hipFuncSetAttribute((const void*)k_head_screen<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
