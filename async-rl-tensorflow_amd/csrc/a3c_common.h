@@ -108,3 +108,15 @@ __device__ inline const uint8_t* state_plane(const StateAddr& a, int64_t b, int 
 #define WG_T0() ((void)0)
 #define WG_T1(dst) ((void)0)
 #endif
+
+// Stores of activations that the next kernel reads on other XCDs (l1, l2, l3, the frame ring):
+// non-temporal with A3C_NT_STORE (bypass the writing XCD's L2, so the end-of-kernel release has
+// fewer dirty lines to write back) -- an A/B switch.
+template <typename T>
+__device__ inline void st_act(T* p, T v) {
+#ifdef A3C_NT_STORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}

@@ -64,6 +64,7 @@ struct a3c_engine {
   EnvParams envp;
   int overlap, nslot;
   int fused_screen;        // 1: screen kernel fused into the head (k_head_screen)
+  int fuse_conv;           // 1: step t+1's conv1 + conv2 fused into step t's head + screen
   Slot slot[2];
   float* loss;
   float* sumsq;
@@ -186,6 +187,11 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   if (e->ext) e->cfg.num_frames = cfg->num_envs;   // the pool is the host frames' staging buffer
   e->fused_screen = 1;
   if (const char* v = getenv("A3C_FUSED_SCREEN")) e->fused_screen = atoi(v) != 0;
+  // overlap mode only: measured on MI355X (Pong, 256 envs) 3.65M -> 3.84M env-steps/s overlapped,
+  // but 3.25M -> 3.08M in sync mode, where the unfused kernels run their bigger variants
+  // (1024-thread screen, early-W2 conv12) with the GPU to themselves
+  e->fuse_conv = e->overlap;
+  if (const char* v = getenv("A3C_FUSE_CONV")) e->fuse_conv = atoi(v) != 0;
   e->nslot = e->overlap ? 2 : 1;
   // ring: the states of one rollout (frames tau-3 .. tau+n); overlap keeps two rollouts' frames
   e->R = (e->overlap ? 2 * e->n : e->n) + HIST + (cfg->net.algo == A3C_ALGO_Q ? 1 : 0);
@@ -344,6 +350,9 @@ static StateAddr ring_addr(const a3c_engine* e, int tau_offset, const int64_t* t
   return sa;
 }
 
+// conv fusion (k_head_screen_conv12) runs with the device envs and the fused screen
+static bool conv_fused(const a3c_engine* e) { return e->fuse_conv && !e->ext && e->fused_screen; }
+
 __global__ void k_advance_tau(int64_t* counters, int n) { counters[0] += n; }
 
 static OptParams opt_params(const a3c_engine* e) {
@@ -437,9 +446,23 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
     ls.hp = sl.lhp + o * LSTM_U; ls.cp = sl.lcp + o * LSTM_U; ls.gates = sl.lg + o * LSTM_G;
     ls.h = sl.lh + o * LSTM_U; ls.c = sl.lc + o * LSTM_U;
   }
+  // conv fusion: step t > 0's conv1 + conv2 ran inside step t-1's head + screen kernel, and this
+  // step's head + screen runs step t+1's (the bootstrap state's after the last step, a3c)
+  const bool fuse = conv_fused(e);
+  Conv12Next nx = {};
+  const bool has_next = fuse && (t + 1 < n || !q);
+  if (has_next) {
+    nx.sa = ring_addr(e, t + 1, e->counters);
+    nx.w1s = (const uint16_t*)sl.prep;
+    nx.b1 = sl.P + L.off[T_L1B];
+    nx.W2 = sl.P + L.off[T_L2W];
+    nx.b2 = sl.P + L.off[T_L2B];
+    nx.act_l1 = t + 1 < n ? sl.act_l1 + (o + E) * C1_P * C1_N : nullptr;
+    nx.act_l2 = t + 1 < n ? sl.act_l2 + (o + E) * FLAT : sl.scr_l2;
+  }
   int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
                               sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s,
-                              L.lstm ? &ls : nullptr);
+                              L.lstm ? &ls : nullptr, fuse && t > 0, has_next ? &nx : nullptr);
   if (rc) return rc;
   if (dev_env && !e->fused_screen) {
     rc = a3c_env_screen_launch(E, sl.frames + o, e->pool, e->ring, e->R, e->counters, t, s);
@@ -464,7 +487,8 @@ static int enqueue_rollout_end(a3c_engine* e, const Slot& sl, hipStream_t s) {
       ls.h = sl.lhb; ls.c = sl.lcb;
     }
     int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, n, e->counters), E, nullptr, sl.scr_l2,
-                                sl.scr_l3, sl.z + e->nE * L.zs, none, s, L.lstm ? &ls : nullptr);
+                                sl.scr_l3, sl.z + e->nE * L.zs, none, s, L.lstm ? &ls : nullptr,
+                                conv_fused(e));   // s_n's convs ran in the last step's kernel
     if (rc) return rc;
   }
   if (e->overlap) {

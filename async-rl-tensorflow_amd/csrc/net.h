@@ -127,10 +127,22 @@ struct HeadSelect {
 #define FC_CH (FLAT / 16)               // 162 K-chunks of 16
 #define PREP_BYTES (PREP_W1S_BYTES + FLAT * FC * 4)
 struct LstmStep;
+// the next state's conv1 + conv2, fused into rollout step t's head + screen kernel
+// (k_head_screen_conv12): s_{t+1} addressing, conv weights (prep'd W1 terms) and outputs
+struct Conv12Next {
+  StateAddr sa;
+  const uint16_t* w1s;
+  const float* b1;
+  const float* W2;
+  const float* b2;
+  float* act_l1;            // nullable: the bootstrap state keeps no l1
+  float* act_l2;
+};
 // ls (LSTM head, C5): the cell step runs on act_l3 and the heads read ls->h
 int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* prep, const StateAddr& sa,
                        int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
-                       hipStream_t s, const LstmStep* ls = nullptr);
+                       hipStream_t s, const LstmStep* ls = nullptr, bool skip_conv12 = false,
+                       const Conv12Next* next = nullptr);
 int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s);
 // true while enqueuing work that runs concurrently with another stream (engine overlap mode)
 bool a3c_shared_gpu();

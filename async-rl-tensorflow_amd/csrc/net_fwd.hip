@@ -91,6 +91,105 @@ __device__ inline bf16x8 u8x8_to_bf16(uint32_t d0, uint32_t d1) {
   return __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
 }
 
+// conv1 (bf16x3 MFMA) + relu -> l1s (and act_l1), conv2 (fp32 MFMA) + relu -> act_l2 for state b,
+// whose HIST planes are staged in LDS (x8 u8 when U8, else xb bf16).  EW: w2r already loaded.
+template <bool SAVE_L1, bool EW, bool U8>
+__device__ inline void conv12_core(const uint8_t* x8, const uint16_t* xb, float* l1s, int64_t b,
+                                   const uint16_t* __restrict__ w1s, const float* __restrict__ b1,
+                                   const float* __restrict__ W2, float* __restrict__ act_l1,
+                                   float* __restrict__ act_l2, float (&w2r)[64], float bias2) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i16 = lane & 15, j4 = lane >> 4;
+  const int nt = wid & 1, grp = wid >> 1;          // conv2: M-tiles grp and grp + 4 (when < 6)
+  // conv1 weight fragments (3 bf16 terms per K step)
+  bf16x8 wf[C1_K][3];
+#pragma unroll
+  for (int kh = 0; kh < C1_K; ++kh)
+#pragma unroll
+    for (int t = 0; t < 3; ++t) wf[kh][t] = __builtin_bit_cast(bf16x8, ((const uint4*)w1s)[(kh * 3 + t) * 64 + lane]);
+  const float bias1 = b1[i16];
+  __syncthreads();
+
+  // ---- conv1 ----
+  for (int m = wid; m < C1_P / 16; m += 8) {
+    const int p = 16 * m + i16;
+    const int oy = p / C1_O, ox = p - oy * C1_O;
+    const uint16_t* row = xb + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;    // cin = j4
+    const uint8_t* row8 = x8 + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accb = {0.f, 0.f, 0.f, 0.f};   // two chains by kh parity
+#pragma unroll
+    for (int kh = 0; kh < C1_K; ++kh) {
+      bf16x8 a;
+      if constexpr (U8) {
+        const uint32_t* q = (const uint32_t*)(row8 + kh * IMG);              // 4-byte aligned
+        a = u8x8_to_bf16(q[0], q[1]);
+      } else {
+        const uint2* q = (const uint2*)(row + kh * IMG);                      // 8-byte aligned
+        const uint2 lo = q[0], hi = q[1];
+        a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+      f32x4& c = (kh & 1) ? accb : acc;
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][2], c, 0, 0, 0);
+    }
+    acc += accb;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int pos = 16 * m + 4 * j4 + r;
+      float v = fmaxf(acc[r] * (1.0f / 255.0f) + bias1, 0.f);
+      l1s[pos * L1S_LD + i16] = v;
+      if (SAVE_L1) st_act(act_l1 + (b * C1_P + pos) * C1_N + i16, v);
+    }
+  }
+
+  if (!EW) {
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) w2r[kk * 4 + c4] = W2[(kk * C1_N + 4 * j4 + c4) * C2_N + 16 * nt + i16];
+  }
+  __syncthreads();
+
+  // ---- conv2: 6 M-tiles (81 rows padded to 96) x 2 N-tiles, K = 16 (kh,kw) x 16 cin ----
+  const int nm = grp + 4 < 6 ? 2 : 1;
+  int pos0[2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    int q = 16 * (grp + 4 * mi) + i16;
+    q = q < C2_Q ? q : C2_Q - 1;
+    int oy = q / C2_O, ox = q - oy * C2_O;
+    pos0[mi] = (C2_S * oy) * C1_O + C2_S * ox;
+  }
+  f32x4 acc2[2], acc2b[2];                         // two chains per tile (kw parity)
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) acc2[mi] = acc2b[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kh = 0; kh < C2_K; ++kh)
+#pragma unroll
+    for (int kw = 0; kw < C2_K; ++kw)
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        if (mi >= nm) break;
+        f32x4 a = *(const f32x4*)(l1s + (pos0[mi] + kh * C1_O + kw) * L1S_LD + 4 * j4);
+        f32x4& c = (kw & 1) ? acc2b[mi] : acc2[mi];
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4)
+          c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c4], w2r[(kh * 4 + kw) * 4 + c4], c, 0, 0, 0);
+      }
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) acc2[mi] += acc2b[mi];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    if (mi >= nm) break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = 16 * (grp + 4 * mi) + 4 * j4 + r;
+      if (q < C2_Q) st_act(act_l2 + b * FLAT + q * C2_N + 16 * nt + i16, fmaxf(acc2[mi][r] + bias2, 0.f));
+    }
+  }
+}
+
 // U8: the planes stay u8 in LDS (28 KB instead of 56 KB) and each conv1 A operand is converted
 // to bf16 in registers (8 pixels: 2 ds_read_b32 + 8 v_cvt_f32_ubyte + 4 v_perm) -- a 60 KB
 // footprint, so a workgroup co-resides on a CU with the concurrent backward's (overlap mode).
@@ -166,93 +265,7 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
     }
   }
 
-  // conv1 weight fragments (3 bf16 terms per K step)
-  bf16x8 wf[C1_K][3];
-#pragma unroll
-  for (int kh = 0; kh < C1_K; ++kh)
-#pragma unroll
-    for (int t = 0; t < 3; ++t) wf[kh][t] = __builtin_bit_cast(bf16x8, ((const uint4*)w1s)[(kh * 3 + t) * 64 + lane]);
-  const float bias1 = b1[i16];
-  __syncthreads();
-
-  // ---- conv1 ----
-  for (int m = wid; m < C1_P / 16; m += 8) {
-    const int p = 16 * m + i16;
-    const int oy = p / C1_O, ox = p - oy * C1_O;
-    const uint16_t* row = xb + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;    // cin = j4
-    const uint8_t* row8 = x8 + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accb = {0.f, 0.f, 0.f, 0.f};   // two chains by kh parity
-#pragma unroll
-    for (int kh = 0; kh < C1_K; ++kh) {
-      bf16x8 a;
-      if constexpr (U8) {
-        const uint32_t* q = (const uint32_t*)(row8 + kh * IMG);              // 4-byte aligned
-        a = u8x8_to_bf16(q[0], q[1]);
-      } else {
-        const uint2* q = (const uint2*)(row + kh * IMG);                      // 8-byte aligned
-        const uint2 lo = q[0], hi = q[1];
-        a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-      }
-      f32x4& c = (kh & 1) ? accb : acc;
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][1], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][2], c, 0, 0, 0);
-    }
-    acc += accb;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int pos = 16 * m + 4 * j4 + r;
-      float v = fmaxf(acc[r] * (1.0f / 255.0f) + bias1, 0.f);
-      l1s[pos * L1S_LD + i16] = v;
-      if (SAVE_L1) act_l1[(b * C1_P + pos) * C1_N + i16] = v;
-    }
-  }
-
-  if (!EW) {
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk)
-#pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) w2r[kk * 4 + c4] = W2[(kk * C1_N + 4 * j4 + c4) * C2_N + 16 * nt + i16];
-  }
-  __syncthreads();
-
-  // ---- conv2: 6 M-tiles (81 rows padded to 96) x 2 N-tiles, K = 16 (kh,kw) x 16 cin ----
-  const int nm = grp + 4 < 6 ? 2 : 1;
-  int pos0[2];
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi) {
-    int q = 16 * (grp + 4 * mi) + i16;
-    q = q < C2_Q ? q : C2_Q - 1;
-    int oy = q / C2_O, ox = q - oy * C2_O;
-    pos0[mi] = (C2_S * oy) * C1_O + C2_S * ox;
-  }
-  f32x4 acc2[2], acc2b[2];                         // two chains per tile (kw parity)
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi) acc2[mi] = acc2b[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kh = 0; kh < C2_K; ++kh)
-#pragma unroll
-    for (int kw = 0; kw < C2_K; ++kw)
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi) {
-        if (mi >= nm) break;
-        f32x4 a = *(const f32x4*)(l1s + (pos0[mi] + kh * C1_O + kw) * L1S_LD + 4 * j4);
-        f32x4& c = (kw & 1) ? acc2b[mi] : acc2[mi];
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4)
-          c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c4], w2r[(kh * 4 + kw) * 4 + c4], c, 0, 0, 0);
-      }
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi) acc2[mi] += acc2b[mi];
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi) {
-    if (mi >= nm) break;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int q = 16 * (grp + 4 * mi) + 4 * j4 + r;
-      if (q < C2_Q) act_l2[b * FLAT + q * C2_N + 16 * nt + i16] = fmaxf(acc2[mi][r] + bias2, 0.f);
-    }
-  }
+  conv12_core<SAVE_L1, EW, U8>(x8, xb, l1s, b, w1s, b1, W2, act_l1, act_l2, w2r, bias2);
   WG_T1(act_l2 + b * FLAT);
 }
 
@@ -430,47 +443,33 @@ __global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, 
 }
 
 // engine rollout step tail, one workgroup per env: head + action draw (wave 0) while wave 1
-// runs the env act up to the frame (env_act_pre: nothing but the frame depends on the action),
-// then the whole workgroup computes Environment.screen (environment.py:49-53, bit-exact) of
-// the post-act frame straight from the HBM pool into the env's frame-ring slot
-template <int HS_THREADS>
-__global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restrict__ h3,
-                                                            const float* __restrict__ Wp,
-                                                            const float* __restrict__ bp,
-                                                            const float* __restrict__ Wv,
-                                                            const float* __restrict__ bv, int A, int zs,
-                                                            float* __restrict__ z, HeadSelect sel) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+// runs the env act up to the frame (env_act_pre: nothing but the frame depends on the action);
+// returns the post-act frame (pool index) of env b
+__device__ inline int32_t head_act_env(const float* __restrict__ h3, const float* __restrict__ Wp,
+                                       const float* __restrict__ bp, const float* __restrict__ Wv,
+                                       const float* __restrict__ bv, int A, int zs, float* __restrict__ z,
+                                       const HeadSelect& sel, int64_t b, int64_t tau, uint64_t* dbg) {
   __shared__ int32_t s_act;
   __shared__ uint32_t s_draw, s_term;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t b = blockIdx.x;
-  const int64_t tau = *sel.tau_ptr + sel.tau_add;
   const int e = (int)b;
   const int64_t nxt = ((tau + 1) & 1) * (int64_t)sel.par_E + e;
-  WG_T0();
-#ifdef HS_TIMES
-  uint64_t* dbg = blockIdx.x == HS_TIMES ? (uint64_t*)z : nullptr;
-  if (dbg && threadIdx.x == 0) dbg[0] = __builtin_readcyclecounter();
-#endif
   if (wid == 0) {
     const float eps = sel.mode != 0 && sel.eps ? sel.eps[e] : 0.f;
     u32x4 x;
     // the action draw does not depend on the head: computed under its load latency
     const float myz = head_row(h3, b, Wp, bp, Wv, bv, A, lane, [&]() { x = action_draw(sel, b, tau); });
-#ifdef HS_TIMES
-    if (dbg && lane == 0) dbg[1] = __builtin_readcyclecounter() + (uint64_t)(myz * 0.f);
-#else
-    if (lane < zs) z[b * zs + lane] = myz;
-#endif
+    if (dbg) {
+      if (lane == 0) dbg[1] = __builtin_readcyclecounter() + (uint64_t)(myz * 0.f);
+    } else if (lane < zs) {
+      z[b * zs + lane] = myz;
+    }
     const int32_t a = select_with(myz, lane, A, sel.mode, x, eps);
     if (lane == 0) {
       sel.actions[b] = a;
       s_act = a;
+      if (dbg) dbg[2] = __builtin_readcyclecounter() + (uint64_t)a * 0;
     }
-#ifdef HS_TIMES
-    if (dbg && lane == 0) dbg[2] = __builtin_readcyclecounter() + (uint64_t)a * 0;
-#endif
   } else if (wid == 1 && lane == 0 && sel.env_on) {
     const int64_t cur = (tau & 1) * (int64_t)sel.par_E + e;
     const uint32_t id = (uint32_t)(sel.env_id_base + e);
@@ -498,14 +497,83 @@ __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restr
   } else {
     frame = sel.frames_out[b];                               // last frame (no env act)
   }
-#ifdef HS_TIMES
   if (dbg && threadIdx.x == 0) dbg[3] = __builtin_readcyclecounter();
+  return frame;
+}
+
+// head + action draw + env act (head_act_env), then the whole workgroup computes
+// Environment.screen (environment.py:49-53, bit-exact) of the post-act frame straight from the
+// HBM pool into the env's frame-ring slot
+template <int HS_THREADS>
+__global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restrict__ h3,
+                                                            const float* __restrict__ Wp,
+                                                            const float* __restrict__ bp,
+                                                            const float* __restrict__ Wv,
+                                                            const float* __restrict__ bv, int A, int zs,
+                                                            float* __restrict__ z, HeadSelect sel) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int64_t b = blockIdx.x;
+  const int64_t tau = *sel.tau_ptr + sel.tau_add;
+  WG_T0();
+  uint64_t* dbg = nullptr;
+#ifdef HS_TIMES
+  dbg = blockIdx.x == HS_TIMES ? (uint64_t*)z : nullptr;
+  if (dbg && threadIdx.x == 0) dbg[0] = __builtin_readcyclecounter();
+#endif
+  const int32_t frame = head_act_env(h3, Wp, bp, Wv, bv, A, zs, z, sel, b, tau, dbg);
   atari::screen_frame<HS_THREADS>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3),
                                   sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE, smem, dbg);
-  return;
-#endif
-  atari::screen_frame<HS_THREADS>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3),
-                                  sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE, smem);
+  WG_T1(z + b * zs);
+}
+
+// Rollout step t's tail fused with step t+1's head: head + act + Environment.screen of env b
+// (as k_head_screen), then conv1 + conv2 of env b's next state s_{t+1} in the same workgroup --
+// the next state is the 3 newest ring planes (prefetched into registers at kernel start, they
+// are final) plus the screen just computed (kept in LDS).  One kernel boundary and the conv
+// staging latency fewer per rollout step.  LDS: screen scratch (54 KB, later overlaid by l1) |
+// x8 (28 KB).
+#define HSC_X8_OFF (((SCREEN_FRAME_SMEM) + 15) / 16 * 16)
+#define HSC_SMEM (HSC_X8_OFF + HIST * PLANE)
+static_assert(C1_P * L1S_LD * 4 <= SCREEN_FRAME_SMEM, "l1 overlays the screen scratch");
+template <bool SAVE_L1>
+__global__ void __launch_bounds__(512) k_head_screen_conv12(const float* __restrict__ h3,
+                                                            const float* __restrict__ Wp,
+                                                            const float* __restrict__ bp,
+                                                            const float* __restrict__ Wv,
+                                                            const float* __restrict__ bv, int A, int zs,
+                                                            float* __restrict__ z, HeadSelect sel,
+                                                            Conv12Next nx) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* x8 = smem + HSC_X8_OFF;
+  const int64_t b = blockIdx.x;
+  const int64_t tau = *sel.tau_ptr + sel.tau_add;
+  const int64_t tau0 = *nx.sa.tau_ptr;
+  WG_T0();
+  // the next state's planes 0..2 (frames tau-1 .. tau+1 - 1): already in the ring
+  constexpr int NCH3 = (HIST - 1) * (PLANE / 16);        // 1323 chunks of 16 pixels
+  constexpr int PER3 = (NCH3 + 511) / 512;               // 3
+  uint4 pv[PER3];
+#pragma unroll
+  for (int k = 0; k < PER3; ++k) {
+    const int i = min((int)threadIdx.x + 512 * k, NCH3 - 1);
+    const int c = i / (PLANE / 16), j = i - c * (PLANE / 16);
+    pv[k] = ((const uint4*)state_plane(nx.sa, b, c, tau0))[j];
+  }
+  const int32_t frame = head_act_env(h3, Wp, bp, Wv, bv, A, zs, z, sel, b, tau, nullptr);
+#pragma unroll
+  for (int k = 0; k < PER3; ++k) {
+    const int i = (int)threadIdx.x + 512 * k;
+    if (i < NCH3) ((uint4*)x8)[i] = pv[k];
+  }
+  // plane 3 = the new screen: to the ring slot (tau + 1) % R and to x8
+  atari::screen_frame<512>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3),
+                           sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE, smem, nullptr,
+                           x8 + (HIST - 1) * PLANE);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float w2r[64];
+  const float bias2 = nx.b2[16 * (wid & 1) + (lane & 15)];
+  conv12_core<SAVE_L1, false, true>(x8, nullptr, (float*)smem, b, nx.w1s, nx.b1, nx.W2,
+                                    SAVE_L1 ? nx.act_l1 : nullptr, nx.act_l2, w2r, bias2);
   WG_T1(z + b * zs);
 }
 
@@ -522,15 +590,21 @@ __global__ void __launch_bounds__(256) k_select(const float* __restrict__ z, int
 int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s,
                       const float* Wrows = nullptr);
 
+// skip_conv12: conv1 + conv2 of these states already ran (fused into the previous step's
+// k_head_screen_conv12); next: fuse the next states' conv1 + conv2 into this step's head + screen
+int a3c_head_screen_conv12_launch(const NetLayout& L, const float* P, const float* act_l3, int64_t B, float* z,
+                                  const HeadSelect& sel, const Conv12Next& nx, hipStream_t s);
 int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* prep, const StateAddr& sa,
                        int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
-                       hipStream_t s, const LstmStep* ls) {
+                       hipStream_t s, const LstmStep* ls, bool skip_conv12, const Conv12Next* next) {
   if (B <= 0) return 0;
   if (L.lstm != (ls != nullptr))
     return a3c_set_error(A3C_ERR_INVALID, "a3c_forward", "the LSTM head needs its recurrent state");
   const float* P = params;
-  int rc0 = a3c_conv12_launch(L, P, prep, sa, B, act_l1, act_l2, s);
-  if (rc0) return rc0;
+  if (!skip_conv12) {
+    int rc0 = a3c_conv12_launch(L, P, prep, sa, B, act_l1, act_l2, s);
+    if (rc0) return rc0;
+  }
   int rc = a3c_fc_fwd_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), P + L.off[T_FCB], act_l3, B, s,
                              P + L.off[T_FCW]);
   if (rc) return rc;
@@ -542,6 +616,9 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
   }
   const float* Wv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VW] : nullptr;
   const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
+  if (sel.mode >= 0 && sel.env_on && sel.ring && next)
+    return a3c_head_screen_conv12_launch(L, P, head_in, B, z, sel, *next, s);
+  if (next) return a3c_set_error(A3C_ERR_INVALID, "a3c_forward", "conv fusion needs the fused env screen");
   if (sel.mode >= 0 && sel.env_on && sel.ring)
     return a3c_head_screen_launch(L, P, head_in, B, z, sel, s);
   else
@@ -565,6 +642,22 @@ int a3c_head_screen_launch(const NetLayout& L, const float* P, const float* act_
   else
     hipLaunchKernelGGL(k_head_screen<512>, dim3((unsigned)B), dim3(512), SCREEN_FRAME_SMEM, s, act_l3,
                        P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+int a3c_head_screen_conv12_launch(const NetLayout& L, const float* P, const float* act_l3, int64_t B, float* z,
+                                  const HeadSelect& sel, const Conv12Next& nx, hipStream_t s) {
+  const float* Wv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VW] : nullptr;
+  const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
+  if (!nx.sa.tau_ptr || !sel.tau_ptr)
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_head_screen_conv12", "device tau counters required");
+  if (nx.act_l1)
+    hipLaunchKernelGGL(k_head_screen_conv12<true>, dim3((unsigned)B), dim3(512), HSC_SMEM, s, act_l3,
+                       P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel, nx);
+  else
+    hipLaunchKernelGGL(k_head_screen_conv12<false>, dim3((unsigned)B), dim3(512), HSC_SMEM, s, act_l3,
+                       P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel, nx);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
@@ -611,6 +704,10 @@ void a3c_conv12_set_smem() {
   C12_SMEM(true, true, false); C12_SMEM(true, false, false); C12_SMEM(false, true, false); C12_SMEM(false, false, false);
   C12_SMEM(true, true, true); C12_SMEM(true, false, true); C12_SMEM(false, true, true); C12_SMEM(false, false, true);
 #undef C12_SMEM
+  (void)hipFuncSetAttribute((const void*)k_head_screen_conv12<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            HSC_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_head_screen_conv12<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            HSC_SMEM);
   (void)hipFuncSetAttribute((const void*)k_head_screen<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             SCREEN_FRAME_SMEM);
   (void)hipFuncSetAttribute((const void*)k_head_screen<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -628,12 +725,21 @@ void a3c_conv12_set_smem() {
 // ---------------------------------------------------------------------------------------
 template <int NW>
 __global__ void __launch_bounds__(64 * NW) k_fc_fwd(const float* __restrict__ A, const float* __restrict__ Wp,
-                                                    const float* __restrict__ bias, float* __restrict__ C, int M) {
+                                                    const float* __restrict__ bias, float* __restrict__ C, int M,
+                                                    int xcd_rows) {
   __shared__ f32x4 red[NW - 1][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i16 = lane & 15, j4 = lane >> 4;
-  const int ct = blockIdx.x;
-  const int m0 = blockIdx.y * 16, n0 = ct * 16;
+  // xcd_rows: 1-D grid, workgroup id -> XCD id % 8 gets a contiguous band of row tiles (all 16
+  // column tiles each), so an XCD reads 1/8 of A and all of W (which is the same every step)
+  int ct = blockIdx.x, mt = blockIdx.y;
+  if (xcd_rows) {
+    const int ntiles = gridDim.x, id = blockIdx.x;
+    const int t = (id & 7) * (ntiles >> 3) + (id >> 3);
+    ct = t % (FC / 16);
+    mt = t / (FC / 16);
+  }
+  const int m0 = mt * 16, n0 = ct * 16;
   const int m = min(m0 + i16, M - 1);
   WG_T0();
   // chunks [c0, c1) of this wave: the 162 chunks split as evenly as possible
@@ -679,7 +785,7 @@ __global__ void __launch_bounds__(64 * NW) k_fc_fwd(const float* __restrict__ A,
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + 4 * j4 + r;
-      if (row < M) C[(int64_t)row * FC + n] = fmaxf(acc[r] + bb, 0.f);
+      if (row < M) st_act(C + (int64_t)row * FC + n, fmaxf(acc[r] + bb, 0.f));
     }
   }
   WG_T1(C + (int64_t)m0 * FC + n0);   // debug: the tile's first 4 outputs
@@ -755,12 +861,18 @@ int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* 
   if (nw == 0 && Wrows)
     hipLaunchKernelGGL(k_fc_fwd_rows, dim3(FC / 16, (unsigned)((M + 15) / 16)), dim3(256), 0, s, A, Wrows, bias, C,
                        (int)M);
-  else if (nw == 4)
-    hipLaunchKernelGGL(k_fc_fwd<4>, dim3(FC / 16, (unsigned)((M + 15) / 16)), dim3(256), 0, s, A, W, bias, C, (int)M);
-  else if (nw == 16)
-    hipLaunchKernelGGL(k_fc_fwd<16>, dim3(FC / 16, (unsigned)((M + 15) / 16)), dim3(1024), 0, s, A, W, bias, C, (int)M);
-  else
-    hipLaunchKernelGGL(k_fc_fwd<8>, dim3(FC / 16, (unsigned)((M + 15) / 16)), dim3(512), 0, s, A, W, bias, C, (int)M);
+  else {
+    static const int env_x = getenv("A3C_FC_XCD") ? atoi(getenv("A3C_FC_XCD")) : 0;
+    const int mt = (int)((M + 15) / 16), ntiles = mt * (FC / 16);
+    const int xr = env_x && ntiles % 8 == 0;
+    const dim3 grid = xr ? dim3((unsigned)ntiles) : dim3(FC / 16, (unsigned)mt);
+    if (nw == 4)
+      hipLaunchKernelGGL(k_fc_fwd<4>, grid, dim3(256), 0, s, A, W, bias, C, (int)M, xr);
+    else if (nw == 16)
+      hipLaunchKernelGGL(k_fc_fwd<16>, grid, dim3(1024), 0, s, A, W, bias, C, (int)M, xr);
+    else
+      hipLaunchKernelGGL(k_fc_fwd<8>, grid, dim3(512), 0, s, A, W, bias, C, (int)M, xr);
+  }
   A3C_CHECK(hipGetLastError());
   return 0;
 }

@@ -184,7 +184,7 @@ __device__ inline void hpass_seg(const uint8_t* __restrict__ grow, uint8_t* __re
 #define SCREEN_FRAME_SMEM (210 * 160 + 210 * 84 + 96 + SCREEN_KV_BYTES)
 template <int NT>
 __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __restrict__ out, uint8_t* smem,
-                                    uint64_t* dbg = nullptr) {
+                                    uint64_t* dbg = nullptr, uint8_t* lds_copy = nullptr) {
   uint8_t* gray = smem;
   uint8_t* tmp = smem + IH * IW;
   int* kvs = (int*)(tmp + IH * OW + 96);              // [yy][8]: 7 taps, xmin
@@ -242,7 +242,8 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
       uint32_t packed = 0;
 #pragma unroll
       for (int c = 0; c < 4; ++c) packed |= (uint32_t)(acc[c] >> A3C_PRECISION_BITS) << (8 * c);
-      *(uint32_t*)(out + yy * OW + 4 * cq) = packed;
+      st_act((uint32_t*)(out + yy * OW + 4 * cq), packed);
+      if (lds_copy) *(uint32_t*)(lds_copy + yy * OW + 4 * cq) = packed;   // (fused conv12: x8 plane 3)
     }
   }
   if (dbg) {

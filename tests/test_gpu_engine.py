@@ -160,6 +160,23 @@ def test_fused_iterate_equals_rollout_grad_then_apply(overlap):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
 
 
+@pytest.mark.parametrize('overlap', [False, True])
+def test_conv_fusion_is_bit_exact(overlap, monkeypatch):
+    """k_head_screen_conv12 (step t+1's conv1 + conv2 inside step t's head + screen kernel) gives
+    the same rollouts, activations and updates as the separate kernels, bit for bit."""
+    engs = []
+    for fuse in ('0', '1'):
+        monkeypatch.setenv('A3C_FUSE_CONV', fuse)
+        engs.append(build('a3c', 6, 16, 5, 0, seed=13, overlap=overlap)[0])
+    a, b = engs
+    for _ in range(4):
+        a.iterate()
+        b.iterate()
+    torch.cuda.synchronize()
+    for name in ('params', 'ms', 'mom', 'frame_ring', 'loss', 'counters', 'actions', 'act_l1', 'act_l2', 'z'):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+
+
 def test_engine_bench_shape_runs():
     """The bench configuration (Pong, 256 envs, n=5) runs and stays finite."""
     eng, _, ns = build('a3c', 6, 256, 5, 0, seed=123, frames=256, scale=1.0)
