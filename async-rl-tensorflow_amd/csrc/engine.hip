@@ -867,7 +867,7 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
   if (e->rs) A3C_CHECK(hipStreamSynchronize(e->rs));
   a3c_set_shared_gpu(e->overlap != 0);      // time the variants the engine runs
   struct ResetShared { ~ResetShared() { a3c_set_shared_gpu(false); } } reset_shared;
-  if (kernel == A3C_KER_CONV12_FWD || kernel == A3C_KER_FC_FWD) {
+  if (kernel == A3C_KER_CONV12_FWD || kernel == A3C_KER_FC_FWD || kernel == A3C_KER_HEAD_SCREEN_CONV12) {
     int rc0 = a3c_prep_fwd_launch(L, e->params, sl.prep, s);
     if (rc0) return rc0;
   }
@@ -884,7 +884,8 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
                                  sl.act_l3, E, s, e->params + L.off[T_FCW]);
       case A3C_KER_ENV_STEP:
         return a3c_env_screen_launch(E, sl.frames, e->pool, e->ring, e->R, e->counters, 0, s);
-      case A3C_KER_HEAD_SCREEN: {
+      case A3C_KER_HEAD_SCREEN:
+      case A3C_KER_HEAD_SCREEN_CONV12: {
         // head + action draw + env act + Environment.screen as in rollout step 0 (idempotent:
         // the env state is read from the tau-parity half and written to the other one)
         HeadSelect sel = {};
@@ -900,7 +901,16 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
         sel.frames_out = sl.frames;
         sel.pool = e->pool; sel.ring = e->ring; sel.R = e->R;
         sel.frame_salt = salt;
-        return a3c_head_screen_launch(L, e->params, L.lstm ? sl.lh : sl.act_l3, E, sl.z, sel, s);
+        if (kernel == A3C_KER_HEAD_SCREEN)
+          return a3c_head_screen_launch(L, e->params, L.lstm ? sl.lh : sl.act_l3, E, sl.z, sel, s);
+        // + conv1 + conv2 of the next states into step 1's activation rows (as rollout step 0)
+        Conv12Next nx = {};
+        nx.sa = ring_addr(e, 1, e->counters);
+        nx.w1s = (const uint16_t*)sl.prep;
+        nx.b1 = e->params + L.off[T_L1B]; nx.W2 = e->params + L.off[T_L2W]; nx.b2 = e->params + L.off[T_L2B];
+        nx.act_l1 = sl.act_l1 + (int64_t)E * C1_P * C1_N;
+        nx.act_l2 = sl.act_l2 + (int64_t)E * FLAT;
+        return a3c_head_screen_conv12_launch(L, e->params, L.lstm ? sl.lh : sl.act_l3, E, sl.z, sel, nx, s);
       }
       case A3C_KER_CONV_BWD: {
         const BwdPlan p = a3c_bwd_plan(L, e->nE);

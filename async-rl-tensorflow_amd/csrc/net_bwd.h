@@ -68,6 +68,8 @@ void a3c_conv12_set_smem();
 void a3c_conv_bwd_set_smem();
 int a3c_head_screen_launch(const NetLayout& L, const float* P, const float* act_l3, int64_t B, float* z,
                            const HeadSelect& sel, hipStream_t s);
+int a3c_head_screen_conv12_launch(const NetLayout& L, const float* P, const float* act_l3, int64_t B, float* z,
+                                  const HeadSelect& sel, const Conv12Next& nx, hipStream_t s);
 int a3c_conv12_launch(const NetLayout& L, const float* P, const uint8_t* prep, const StateAddr& sa, int64_t B,
                       float* act_l1, float* act_l2, hipStream_t s);
 int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,

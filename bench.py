@@ -178,28 +178,50 @@ def main():
 
     roofline, kernels = None, {}
     if rank == 0 and not args.no_kernel_timing and not host:
+        # overlap mode fuses step t+1's conv1+conv2 into step t's head+screen kernel
+        # (k_head_screen_conv12, engine.hip conv_fused): conv12 then runs once per rollout
+        fused = args.update == 'overlap' and os.environ.get('A3C_FUSE_CONV', '1') != '0'
         ms = {
             'k_conv12_fwd': eng.time_kernel(_lib.KER_CONV12_FWD, 20),
             'k_conv_bwd': eng.time_kernel(_lib.KER_CONV_BWD, 10),
             'k_fc_fwd': eng.time_kernel(_lib.KER_FC_FWD, 20),
-            'k_head_screen': eng.time_kernel(_lib.KER_HEAD_SCREEN, 20),
         }
-        count = {'k_conv12_fwd': n + 1, 'k_conv_bwd': 1, 'k_fc_fwd': n + 1, 'k_head_screen': n}
+        count = {'k_conv12_fwd': 1 if fused else n + 1, 'k_conv_bwd': 1, 'k_fc_fwd': n + 1}
         work = {
             'k_conv12_fwd': ('mfma', CONV12_FWD_FLOP * E),
             'k_conv_bwd': ('mfma', CONV_BWD_FLOP * n * E),
             'k_fc_fwd': ('mfma', FC_FWD_FLOP * E),
-            'k_head_screen': ('hbm', ENV_STEP_BYTES * E),
         }
+        if fused:
+            ms['k_head_screen_conv12'] = eng.time_kernel(_lib.KER_HEAD_SCREEN_CONV12, 20)
+            count['k_head_screen_conv12'] = n
+            # two serial phases per workgroup: Environment.screen (HBM) then conv1+conv2 (MFMA);
+            # roofline time = bytes / HBM peak + FLOP / FP32 MFMA peak
+            work['k_head_screen_conv12'] = ('hbm+mfma', (ENV_STEP_BYTES * E, CONV12_FWD_FLOP * E))
+        else:
+            ms['k_head_screen'] = eng.time_kernel(_lib.KER_HEAD_SCREEN, 20)
+            count['k_head_screen'] = n
+            work['k_head_screen'] = ('hbm', ENV_STEP_BYTES * E)
         iter_ms = el / args.steps * 1e3
         for k in ms:
             bound, w = work[k]
-            ach = w / (ms[k] * 1e-3) / (1e12 if bound == 'mfma' else 1e9)
             kernels[k] = dict(avg_ms=round(ms[k], 4), per_iter=count[k],
-                              share=round(ms[k] * count[k] / iter_ms, 3), bound=bound,
-                              achieved=round(ach, 2), unit='TFLOP/s' if bound == 'mfma' else 'GB/s')
+                              share=round(ms[k] * count[k] / iter_ms, 3), bound=bound)
+            if bound == 'hbm+mfma':
+                byt, flop = w
+                t_roof = byt / (PEAK_HBM_GBS * 1e9) + flop / (PEAK_FP32_TFLOPS * 1e12)
+                kernels[k].update(achieved_gbs=round(byt / (ms[k] * 1e-3) / 1e9, 2),
+                                  achieved_tflops=round(flop / (ms[k] * 1e-3) / 1e12, 2),
+                                  achieved=round(t_roof / (ms[k] * 1e-3), 4), unit='fraction of roofline time')
+            else:
+                ach = w / (ms[k] * 1e-3) / (1e12 if bound == 'mfma' else 1e9)
+                kernels[k].update(achieved=round(ach, 2), unit='TFLOP/s' if bound == 'mfma' else 'GB/s')
         dom = max(ms, key=lambda k: ms[k] * count[k])
         bound, w = work[dom]
+        if bound == 'hbm+mfma':                  # report the phase that dominates its roofline time
+            byt, flop = w
+            bound, w = ('hbm', byt) if byt / PEAK_HBM_GBS / 1e9 >= flop / PEAK_FP32_TFLOPS / 1e12 else ('mfma', flop)
+        dom_ach = round(w / (ms[dom] * 1e-3) / (1e12 if bound == 'mfma' else 1e9), 2)
         peak = PEAK_FP32_TFLOPS if bound == 'mfma' else PEAK_HBM_GBS
         # HBM bytes per launch from the committed PMC passes (tools/profile_round.sh):
         # (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 FETCH_SIZE correction per MI355X_MICROARCH.md
@@ -211,9 +233,9 @@ def main():
                 traffic = None if t is None else int(round(t))
             except Exception:
                 traffic = None
-        roofline = dict(kernel=dom, bound=bound, achieved=kernels[dom]['achieved'], peak=peak,
+        roofline = dict(kernel=dom, bound=bound, achieved=dom_ach, peak=peak,
                         unit='TFLOP/s' if bound == 'mfma' else 'GB/s',
-                        frac=round(kernels[dom]['achieved'] / peak, 4), traffic=traffic,
+                        frac=round(dom_ach / peak, 4), traffic=traffic,
                         work_per_launch=w, work_unit='FLOP' if bound == 'mfma' else 'B')
 
     if world > 1:

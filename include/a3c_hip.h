@@ -384,6 +384,7 @@ int a3c_engine_slot_buffers(a3c_engine* eng, int slot, a3c_engine_buffers* out);
 #define A3C_KER_ENV_STEP 2     /* Environment.screen of the post-act frames into the ring */
 #define A3C_KER_CONV_BWD 3     /* fused conv backward over B = n*E                       */
 #define A3C_KER_HEAD_SCREEN 4  /* fused head + action draw + Environment.screen, B = E    */
+#define A3C_KER_HEAD_SCREEN_CONV12 5  /* ... + conv1+conv2 of the next states (overlap mode) */
 int a3c_engine_time_kernel(a3c_engine* eng, int kernel, int iters, void* stream, float* avg_ms);
 
 #ifdef __cplusplus
