@@ -116,7 +116,7 @@ __device__ inline void conv12_core(const uint8_t* x8, const uint16_t* xb, float*
     const int oy = p / C1_O, ox = p - oy * C1_O;
     const uint16_t* row = xb + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;    // cin = j4
     const uint8_t* row8 = x8 + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accb = {0.f, 0.f, 0.f, 0.f};   // two chains by kh parity
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accb = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kh = 0; kh < C1_K; ++kh) {
       bf16x8 a;
@@ -128,6 +128,8 @@ __device__ inline void conv12_core(const uint8_t* x8, const uint16_t* xb, float*
         const uint2 lo = q[0], hi = q[1];
         a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
       }
+      // two chains by kh parity (a third accumulator measured +46 VGPRs: 170, which breaks the
+      // overlap-mode co-residency budget of 128, and 3.85M -> 3.13M env-steps/s)
       f32x4& c = (kh & 1) ? accb : acc;
       c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][0], c, 0, 0, 0);
       c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][1], c, 0, 0, 0);
@@ -172,7 +174,7 @@ __device__ inline void conv12_core(const uint8_t* x8, const uint16_t* xb, float*
       for (int mi = 0; mi < 2; ++mi) {
         if (mi >= nm) break;
         f32x4 a = *(const f32x4*)(l1s + (pos0[mi] + kh * C1_O + kw) * L1S_LD + 4 * j4);
-        f32x4& c = (kw & 1) ? acc2b[mi] : acc2[mi];
+        f32x4& c = (kw & 1) ? acc2b[mi] : acc2[mi];   // (alternating by c4 instead: measured no change)
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4)
           c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c4], w2r[(kh * 4 + kw) * 4 + c4], c, 0, 0, 0);
@@ -535,8 +537,10 @@ __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restr
 #define HSC_X8_OFF (((SCREEN_FRAME_SMEM) + 15) / 16 * 16)
 #define HSC_SMEM (HSC_X8_OFF + HIST * PLANE)
 static_assert(C1_P * L1S_LD * 4 <= SCREEN_FRAME_SMEM, "l1 overlays the screen scratch");
+// waves_per_eu(4) caps it at 128 VGPRs: with the concurrent k_conv_bwd<false,4> (254 VGPRs,
+// one wave per SIMD) two of its waves per SIMD must fit in the remaining 258
 template <bool SAVE_L1>
-__global__ void __launch_bounds__(512) k_head_screen_conv12(const float* __restrict__ h3,
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k_head_screen_conv12(const float* __restrict__ h3,
                                                             const float* __restrict__ Wp,
                                                             const float* __restrict__ bp,
                                                             const float* __restrict__ Wv,
@@ -549,6 +553,11 @@ __global__ void __launch_bounds__(512) k_head_screen_conv12(const float* __restr
   const int64_t tau = *sel.tau_ptr + sel.tau_add;
   const int64_t tau0 = *nx.sa.tau_ptr;
   WG_T0();
+  uint64_t* dbg = nullptr;
+#ifdef HS_TIMES
+  dbg = blockIdx.x == HS_TIMES ? (uint64_t*)z : nullptr;
+  if (dbg && threadIdx.x == 0) dbg[0] = __builtin_readcyclecounter();
+#endif
   // the next state's planes 0..2 (frames tau-1 .. tau+1 - 1): already in the ring
   constexpr int NCH3 = (HIST - 1) * (PLANE / 16);        // 1323 chunks of 16 pixels
   constexpr int PER3 = (NCH3 + 511) / 512;               // 3
@@ -559,7 +568,7 @@ __global__ void __launch_bounds__(512) k_head_screen_conv12(const float* __restr
     const int c = i / (PLANE / 16), j = i - c * (PLANE / 16);
     pv[k] = ((const uint4*)state_plane(nx.sa, b, c, tau0))[j];
   }
-  const int32_t frame = head_act_env(h3, Wp, bp, Wv, bv, A, zs, z, sel, b, tau, nullptr);
+  const int32_t frame = head_act_env(h3, Wp, bp, Wv, bv, A, zs, z, sel, b, tau, dbg);
 #pragma unroll
   for (int k = 0; k < PER3; ++k) {
     const int i = (int)threadIdx.x + 512 * k;
@@ -567,13 +576,18 @@ __global__ void __launch_bounds__(512) k_head_screen_conv12(const float* __restr
   }
   // plane 3 = the new screen: to the ring slot (tau + 1) % R and to x8
   atari::screen_frame<512>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3),
-                           sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE, smem, nullptr,
+                           sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE, smem, dbg,
                            x8 + (HIST - 1) * PLANE);
+  if (dbg && threadIdx.x == 0) dbg[9] = __builtin_readcyclecounter();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float w2r[64];
   const float bias2 = nx.b2[16 * (wid & 1) + (lane & 15)];
   conv12_core<SAVE_L1, false, true>(x8, nullptr, (float*)smem, b, nx.w1s, nx.b1, nx.W2,
                                     SAVE_L1 ? nx.act_l1 : nullptr, nx.act_l2, w2r, bias2);
+  if (dbg) {
+    __syncthreads();
+    if (threadIdx.x == 0) dbg[10] = __builtin_readcyclecounter();
+  }
   WG_T1(z + b * zs);
 }
 
