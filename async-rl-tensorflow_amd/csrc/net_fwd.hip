@@ -20,9 +20,14 @@
 #include "screen_atari.h"
 
 #define XB_BYTES (HIST * PLANE * 2)                  // 56448: state planes as bf16
-#define L1S_BYTES (C1_P * L1S_LD * 4)                // 32000
-#define CONV12_SMEM (XB_BYTES + L1S_BYTES)           // 88448
-#define CONV12_SMEM_U8 (HIST * PLANE + L1S_BYTES)    // 60224: u8 planes, converted per operand
+#ifdef C2_FP32
+#define L1S_BYTES (C1_P * L1S_LD * 4)                // 32000: conv1 out fp32, rows of 20 floats
+#else
+#define L1T_LD 56                                    // bf16 per position: 3 terms x 16 ch + pad
+#define L1S_BYTES (C1_P * L1T_LD * 2)                // 44800: conv1 out as three bf16 terms
+#endif
+#define CONV12_SMEM (XB_BYTES + L1S_BYTES)           // 101248
+#define CONV12_SMEM_U8 (HIST * PLANE + L1S_BYTES)    // 73024: u8 planes, converted per operand
 
 // ---------------------------------------------------------------------------------------
 // conv1 weights as three bf16 terms.  A u8 pixel is exact in bf16, so conv1 runs on the bf16
@@ -35,8 +40,20 @@
 // Forward weight preparation, once per parameter version (rollout start): the conv1 bf16
 // terms above and the fc weights in MFMA fragment order, Wp[ct][c][lane][c4] =
 // W[16c + 4(lane>>4) + c4][16ct + (lane&15)], so a lane's B operands for 4 MFMAs are one 16-byte load.
+// conv2 weights as three bf16 terms in fragment order (w2f, at PREP_W2F_OFF):
+// w2f[nt][ks][term][lane][j], lane = (j4 = lane>>4, i16 = lane&15), holds B[k][n] of K-step ks
+// (taps kk = 2 ks + (j4>>1), cin = 8 (j4&1) + j) for cout n = 16 nt + i16.
+__device__ inline void split3_bits(float w, uint32_t& h, uint32_t& m, uint32_t& l) {
+#pragma clang fp contract(off)
+  h = bf16_rn_bits(w);
+  const float r1 = w - __uint_as_float(h << 16);
+  m = bf16_rn_bits(r1);
+  const float r2 = r1 - __uint_as_float(m << 16);
+  l = bf16_rn_bits(r2);
+}
+
 __global__ void __launch_bounds__(256) k_prep_fwd(const float* __restrict__ W1, const float* __restrict__ Wfc,
-                                                  uint8_t* __restrict__ prep) {
+                                                  const float* __restrict__ W2, uint8_t* __restrict__ prep) {
 #pragma clang fp contract(off)
   const int t = blockIdx.x * 256 + threadIdx.x;
   if (t < C1_K * 64 * 8) {                                   // (kh, lane, j): conv1 split
@@ -55,7 +72,19 @@ __global__ void __launch_bounds__(256) k_prep_fwd(const float* __restrict__ W1, 
     return;
   }
   const int q = t - C1_K * 64 * 8;                          // (ct, c, lane): one f32x4 of the fc pack
-  if (q >= (FC / 16) * FC_CH * 64) return;
+  if (q >= (FC / 16) * FC_CH * 64) {
+    const int r = q - (FC / 16) * FC_CH * 64;               // (nt, ks, lane, j): conv2 split
+    if (r >= W2F_ELEMS) return;
+    const int nt = r >> 12, ks = (r >> 9) & 7, lane = (r >> 3) & 63, j = r & 7;
+    const int j4 = lane >> 4, kk = 2 * ks + (j4 >> 1), ci = 8 * (j4 & 1) + j;
+    uint32_t h, m, l;
+    split3_bits(W2[(kk * C1_N + ci) * C2_N + 16 * nt + (lane & 15)], h, m, l);
+    uint16_t* w2f = (uint16_t*)(prep + PREP_W2F_OFF) + ((nt * 8 + ks) * 3) * 512 + lane * 8 + j;
+    w2f[0] = (uint16_t)h;
+    w2f[512] = (uint16_t)m;
+    w2f[1024] = (uint16_t)l;
+    return;
+  }
   const int lane = q & 63, c = (q >> 6) % FC_CH, ct = (q >> 6) / FC_CH;
   const int j4 = lane >> 4, n = 16 * ct + (lane & 15);
   f32x4 v;
@@ -65,9 +94,9 @@ __global__ void __launch_bounds__(256) k_prep_fwd(const float* __restrict__ W1, 
 }
 
 int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s) {
-  const int total = C1_K * 64 * 8 + (FC / 16) * FC_CH * 64;
+  const int total = C1_K * 64 * 8 + (FC / 16) * FC_CH * 64 + W2F_ELEMS;
   hipLaunchKernelGGL(k_prep_fwd, dim3((total + 255) / 256), dim3(256), 0, s, P + L.off[T_L1W], P + L.off[T_FCW],
-                     prep);
+                     P + L.off[T_L2W], prep);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
@@ -140,17 +169,35 @@ __device__ inline void conv12_core(const uint8_t* x8, const uint16_t* xb, float*
     for (int r = 0; r < 4; ++r) {
       const int pos = 16 * m + 4 * j4 + r;
       float v = fmaxf(acc[r] * (1.0f / 255.0f) + bias1, 0.f);
+#ifdef C2_FP32
       l1s[pos * L1S_LD + i16] = v;
+#else
+      // l1 = h + m + l, three round-to-nearest bf16 terms (exact: 24 significant bits)
+      uint32_t th, tm, tl;
+      split3_bits(v, th, tm, tl);
+      uint16_t* d = (uint16_t*)l1s + pos * L1T_LD + i16;
+      d[0] = (uint16_t)th;
+      d[16] = (uint16_t)tm;
+      d[32] = (uint16_t)tl;
+#endif
       if (SAVE_L1) st_act(act_l1 + (b * C1_P + pos) * C1_N + i16, v);
     }
   }
 
+#ifdef C2_FP32
   if (!EW) {
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk)
 #pragma unroll
       for (int c4 = 0; c4 < 4; ++c4) w2r[kk * 4 + c4] = W2[(kk * C1_N + 4 * j4 + c4) * C2_N + 16 * nt + i16];
   }
+#else
+  // conv2 B fragments: K-step 0's three terms now, each next step's under the current MFMAs
+  const uint4* w2f = (const uint4*)((const uint8_t*)w1s + PREP_W2F_OFF) + nt * (8 * 3 * 64) + lane;
+  uint4 bq[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) bq[t] = w2f[t * 64];
+#endif
   __syncthreads();
 
   // ---- conv2: 6 M-tiles (81 rows padded to 96) x 2 N-tiles, K = 16 (kh,kw) x 16 cin ----
@@ -163,9 +210,43 @@ __device__ inline void conv12_core(const uint8_t* x8, const uint16_t* xb, float*
     int oy = q / C2_O, ox = q - oy * C2_O;
     pos0[mi] = (C2_S * oy) * C1_O + C2_S * ox;
   }
-  f32x4 acc2[2], acc2b[2];                         // two chains per tile (kw parity)
+  f32x4 acc2[2], acc2b[2];                         // two chains per tile
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi) acc2[mi] = acc2b[mi] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#ifndef C2_FP32
+  // bf16x6: l1 = a0+a1+a2 and W2 = b0+b1+b2 (bf16 terms); the six products with i + j <= 2 carry
+  // each fp32 product to ~2^-24 relative (the dropped a1b2 + a2b1 + a2b2 are below 2^-24), every
+  // product exact in the fp32 accumulator.  K-step ks = taps 2ks, 2ks+1 x 16 cin: 6 MFMAs of
+  // 16x16x32 bf16 (96 cycles) for what took 8 fp32 16x16x4 ones (256 cycles).
+  const uint16_t* l1t = (const uint16_t*)l1s;
+#pragma unroll 2
+  for (int ks = 0; ks < 8; ++ks) {
+    uint4 bn[3];
+    if (ks < 7) {
+#pragma unroll
+      for (int t = 0; t < 3; ++t) bn[t] = w2f[((ks + 1) * 3 + t) * 64];
+    }
+    const int kk = 2 * ks + (j4 >> 1), kh = kk >> 2, kw = kk & 3;
+    const bf16x8 b0 = __builtin_bit_cast(bf16x8, bq[0]), bm = __builtin_bit_cast(bf16x8, bq[1]),
+                 bl = __builtin_bit_cast(bf16x8, bq[2]);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      if (mi >= nm) break;
+      const uint16_t* ap = l1t + (pos0[mi] + kh * C1_O + kw) * L1T_LD + 8 * (j4 & 1);
+      const bf16x8 a0 = *(const bf16x8*)ap, a1 = *(const bf16x8*)(ap + 16), a2 = *(const bf16x8*)(ap + 32);
+      acc2[mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc2[mi], 0, 0, 0);
+      acc2b[mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bm, acc2b[mi], 0, 0, 0);
+      acc2[mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b0, acc2[mi], 0, 0, 0);
+      acc2b[mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bl, acc2b[mi], 0, 0, 0);
+      acc2[mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bm, acc2[mi], 0, 0, 0);
+      acc2b[mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b0, acc2b[mi], 0, 0, 0);
+    }
+    if (ks < 7) {
+#pragma unroll
+      for (int t = 0; t < 3; ++t) bq[t] = bn[t];
+    }
+  }
+#else
 #pragma unroll
   for (int kh = 0; kh < C2_K; ++kh)
 #pragma unroll
@@ -179,6 +260,7 @@ __device__ inline void conv12_core(const uint8_t* x8, const uint16_t* xb, float*
         for (int c4 = 0; c4 < 4; ++c4)
           c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c4], w2r[(kh * 4 + kw) * 4 + c4], c, 0, 0, 0);
       }
+#endif
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi) acc2[mi] += acc2b[mi];
 #pragma unroll
@@ -252,12 +334,14 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
   // loaded after conv1 (the small-footprint variant for overlap mode)
   const int nt = wid & 1, grp = wid >> 1;          // M-tiles grp and grp + 4 (when < 6)
   float w2r[64];
+#ifdef C2_FP32
   if (EW) {
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk)
 #pragma unroll
       for (int c4 = 0; c4 < 4; ++c4) w2r[kk * 4 + c4] = W2[(kk * C1_N + 4 * j4 + c4) * C2_N + 16 * nt + i16];
   }
+#endif
   const float bias2 = b2[16 * nt + i16];
   if (EW) {
 #pragma unroll
@@ -536,7 +620,7 @@ __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restr
 // x8 (28 KB).
 #define HSC_X8_OFF (((SCREEN_FRAME_SMEM) + 15) / 16 * 16)
 #define HSC_SMEM (HSC_X8_OFF + HIST * PLANE)
-static_assert(C1_P * L1S_LD * 4 <= SCREEN_FRAME_SMEM, "l1 overlays the screen scratch");
+static_assert(L1S_BYTES <= SCREEN_FRAME_SMEM, "l1 overlays the screen scratch");
 // waves_per_eu(4) caps it at 128 VGPRs: with the concurrent k_conv_bwd<false,4> (254 VGPRs,
 // one wave per SIMD) two of its waves per SIMD must fit in the remaining 258
 template <bool SAVE_L1>
