@@ -642,21 +642,29 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   dbg = blockIdx.x == HS_TIMES ? (uint64_t*)z : nullptr;
   if (dbg && threadIdx.x == 0) dbg[0] = __builtin_readcyclecounter();
 #endif
-  // the next state's planes 0..2 (frames tau-1 .. tau+1 - 1): already in the ring
+  // the next state's planes 0..2 (frames tau-1 .. tau+1 - 1): already in the ring.  Prefetched by
+  // waves 2..7 only: in waves 0 (head) and 1 (env act) these loads would queue ahead of the head's
+  // and the env state's (in-order vmcnt) -- measured +3k cycles on the head
   constexpr int NCH3 = (HIST - 1) * (PLANE / 16);        // 1323 chunks of 16 pixels
-  constexpr int PER3 = (NCH3 + 511) / 512;               // 3
+  constexpr int PT = 512 - 128;                          // prefetching threads
+  constexpr int PER3 = (NCH3 + PT - 1) / PT;             // 4
+  const int pt = (int)threadIdx.x - 128;
   uint4 pv[PER3];
+  if (pt >= 0) {
 #pragma unroll
-  for (int k = 0; k < PER3; ++k) {
-    const int i = min((int)threadIdx.x + 512 * k, NCH3 - 1);
-    const int c = i / (PLANE / 16), j = i - c * (PLANE / 16);
-    pv[k] = ((const uint4*)state_plane(nx.sa, b, c, tau0))[j];
+    for (int k = 0; k < PER3; ++k) {
+      const int i = min(pt + PT * k, NCH3 - 1);
+      const int c = i / (PLANE / 16), j = i - c * (PLANE / 16);
+      pv[k] = ((const uint4*)state_plane(nx.sa, b, c, tau0))[j];
+    }
   }
   const int32_t frame = head_act_env(h3, Wp, bp, Wv, bv, A, zs, z, sel, b, tau, dbg);
+  if (pt >= 0) {
 #pragma unroll
-  for (int k = 0; k < PER3; ++k) {
-    const int i = (int)threadIdx.x + 512 * k;
-    if (i < NCH3) ((uint4*)x8)[i] = pv[k];
+    for (int k = 0; k < PER3; ++k) {
+      const int i = pt + PT * k;
+      if (i < NCH3) ((uint4*)x8)[i] = pv[k];
+    }
   }
   // plane 3 = the new screen: to the ring slot (tau + 1) % R and to x8
   atari::screen_frame<512>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3),
