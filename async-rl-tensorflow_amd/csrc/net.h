@@ -125,6 +125,7 @@ struct HeadSelect {
 #define W1S_ELEMS (C1_K * 3 * 64 * 8)   // 12288 bf16
 #define PREP_W1S_BYTES (W1S_ELEMS * 2)  // 24576
 #define FC_CH (FLAT / 16)               // 162 K-chunks of 16
+#define FC_CH32 (FLAT / 32)             // 81 K-chunks of 32
 #define PREP_W2F_OFF (PREP_W1S_BYTES + FLAT * FC * 4)
 #define W2F_ELEMS (2 * 8 * 64 * 8)      // conv2 weights (16x16x32), as three bf16 terms each
 #define PREP_BYTES (PREP_W2F_OFF + W2F_ELEMS * 3 * 2)
