@@ -80,7 +80,28 @@ struct StateAddr {
   int L;                 // history length
   int tau_offset;        // added to tau (+1 for next states)
   const int64_t* tau_ptr;  // device counter (nullable -> 0)
+  // launch-span record (engine measurement, a3c_engine_span_stats): a kernel reading these
+  // states stores its workgroups' start and end s_memrealtime stamps (plain stores, one slot per
+  // workgroup: no same-address atomics) into launch record (tau + tau_offset) / span_div % SPAN_RECS
+  unsigned long long* span = nullptr;
+  int span_div = 1;
 };
+#define SPAN_RECS 1024
+#define SPAN_WGS 512              // workgroup slots per launch record
+__device__ inline unsigned long long* span_rec(const StateAddr& a, int64_t tau0) {
+  if (!a.span || blockIdx.x >= SPAN_WGS) return nullptr;
+  return a.span + 2 * ((((tau0 + a.tau_offset) / a.span_div) % SPAN_RECS) * SPAN_WGS + blockIdx.x);
+}
+// the workgroup's start stamp (thread 0, at its start)
+__device__ inline void span_begin(unsigned long long* r) {
+  if (r && threadIdx.x == 0) r[0] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+}
+// its end stamp (after a workgroup barrier, once all of the workgroup's work is issued)
+__device__ inline void span_end(unsigned long long* r) {
+  if (!r) return;
+  __syncthreads();
+  if (threadIdx.x == 0) r[1] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+}
 
 __device__ inline const uint8_t* state_plane(const StateAddr& a, int64_t b, int c, int64_t tau0) {
   int64_t t = b / a.E, e = b - t * a.E;

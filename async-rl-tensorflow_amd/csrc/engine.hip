@@ -65,6 +65,7 @@ struct a3c_engine {
   int overlap, nslot;
   int fused_screen;        // 1: screen kernel fused into the head (k_head_screen)
   int fuse_conv;           // 1: step t+1's conv1 + conv2 fused into step t's head + screen
+  unsigned long long* spans;  // [2][SPAN_RECS][2]: live launch spans of k_conv_bwd, k_head_screen_conv12
   Slot slot[2];
   float* loss;
   float* sumsq;
@@ -258,6 +259,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     ALLOC(e->ldh, nE * LSTM_U * 4);
   }
   ALLOC(e->prep_t, PREP_BYTES);
+  ALLOC(e->spans, 2 * (size_t)SPAN_RECS * SPAN_WGS * 2 * sizeof(unsigned long long));
   ALLOC(e->zt, scrB * zs * 4);
   ALLOC(e->eps, E * 4);
   ALLOC(e->ep_end, E * 4);
@@ -350,6 +352,11 @@ static StateAddr ring_addr(const a3c_engine* e, int tau_offset, const int64_t* t
   return sa;
 }
 
+// live launch-span stamps in k_conv_bwd / k_head_screen_conv12 (A3C_SPANS=0 turns them off)
+static bool spans_on() {
+  static const bool on = !getenv("A3C_SPANS") || atoi(getenv("A3C_SPANS")) != 0;
+  return on;
+}
 // conv fusion (k_head_screen_conv12) runs with the device envs and the fused screen
 static bool conv_fused(const a3c_engine* e) { return e->fuse_conv && !e->ext && e->fused_screen; }
 
@@ -453,6 +460,7 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
   const bool has_next = fuse && (t + 1 < n || !q);
   if (has_next) {
     nx.sa = ring_addr(e, t + 1, e->counters);
+    nx.sa.span = spans_on() ? e->spans + (size_t)SPAN_RECS * SPAN_WGS * 2 : nullptr;   // per launch
     nx.w1s = (const uint16_t*)sl.prep;
     nx.b1 = sl.P + L.off[T_L1B];
     nx.W2 = sl.P + L.off[T_L2W];
@@ -547,7 +555,10 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
     lb.h = sl.lh; lb.c = sl.lc; lb.hp = sl.lhp; lb.cp = sl.lcp; lb.gates = sl.lg;
     lb.dh = e->ldh; lb.ws = e->lws;
   }
-  rc = a3c_backward_launch(L, sl.P, ring_addr(e, 0, sl.tau), e->nE, sl.act_l1, sl.act_l2, sl.act_l3, sl.z,
+  StateAddr bsa = ring_addr(e, 0, sl.tau);
+  bsa.span = spans_on() ? e->spans : nullptr;   // one record per backward (tau advances by n)
+  bsa.span_div = n;
+  rc = a3c_backward_launch(L, sl.P, bsa, e->nE, sl.act_l1, sl.act_l2, sl.act_l3, sl.z,
                            sl.actions, sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra,
                            fork ? e->gs : nullptr, fork ? e->ev_gfork : nullptr, fork ? e->ev_gjoin : nullptr,
                            L.lstm ? &lb : nullptr);
@@ -935,5 +946,46 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
   (void)hipEventDestroy(b);
   if (rc) return rc;
   *avg_ms = ms / (float)iters;
+  return 0;
+}
+
+// Live launch spans of the engine's dominant kernels (which 0: k_conv_bwd, 1:
+// k_head_screen_conv12), recorded by the kernels themselves inside the replayed graphs: per
+// launch, last workgroup end - first workgroup start (s_memrealtime, 100 MHz).  reset = 1 clears
+// the records (call it synchronised, before a timed region); otherwise the average / max span
+// in microseconds over the launches recorded since.
+extern "C" int a3c_engine_span_stats(a3c_engine* e, int which, int reset, double* avg_us, double* max_us,
+                                     int64_t* launches) {
+  if (!e || which < 0 || which > 1) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_span_stats", "bad argument");
+  const size_t per = (size_t)SPAN_RECS * SPAN_WGS * 2;
+  unsigned long long* d = e->spans + (size_t)which * per;
+  std::vector<unsigned long long> h(per);
+  if (reset) {                            // start stamps ~0, end stamps 0 = not written
+    for (size_t i = 0; i < per; i += 2) { h[i] = ~0ull; h[i + 1] = 0ull; }
+    A3C_CHECK(hipDeviceSynchronize());
+    A3C_CHECK(hipMemcpy(d, h.data(), per * sizeof(unsigned long long), hipMemcpyHostToDevice));
+    return 0;
+  }
+  A3C_CHECK(hipDeviceSynchronize());
+  A3C_CHECK(hipMemcpy(h.data(), d, per * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  double sum = 0.0, mx = 0.0;
+  int64_t n = 0;
+  for (int r = 0; r < SPAN_RECS; ++r) {
+    unsigned long long lo = ~0ull, hi = 0ull;
+    for (int w = 0; w < SPAN_WGS; ++w) {
+      const unsigned long long a = h[2 * ((size_t)r * SPAN_WGS + w)], b = h[2 * ((size_t)r * SPAN_WGS + w) + 1];
+      if (a == ~0ull || b == 0ull) continue;
+      lo = a < lo ? a : lo;
+      hi = b > hi ? b : hi;
+    }
+    if (hi == 0ull || lo == ~0ull || hi < lo) continue;
+    const double us = (double)(hi - lo) * 0.01;
+    sum += us;
+    mx = us > mx ? us : mx;
+    ++n;
+  }
+  if (avg_us) *avg_us = n ? sum / (double)n : 0.0;
+  if (max_us) *max_us = mx;
+  if (launches) *launches = n;
   return 0;
 }

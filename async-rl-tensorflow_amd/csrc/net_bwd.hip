@@ -200,6 +200,8 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
   const int64_t b0 = (int64_t)blockIdx.x * per_wg;
   const int64_t b1 = min(B, b0 + per_wg);
   WG_T0();
+  unsigned long long* srec = span_rec(sa, tau0);
+  span_begin(srec);
 
   // parity class of this wave for dl1: (py, px); with 8 waves two waves share a class and
   // split its 7 M-tiles (0-3 / 4-6)
@@ -474,6 +476,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     out[CB_OFF_B1 + tid] = v;
   }
   if (tid < C2_N) out[CB_OFF_B2 + tid] = db2acc;
+  span_end(srec);
   WG_T1(act_l1 + b0 * C1_P * C1_N);   // debug: over this workgroup's own (consumed) l1 rows
 }
 

@@ -646,6 +646,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   const int64_t tau = *sel.tau_ptr + sel.tau_add;
   const int64_t tau0 = *nx.sa.tau_ptr;
   WG_T0();
+  unsigned long long* srec = span_rec(nx.sa, tau0);
+  span_begin(srec);
   uint64_t* dbg = nullptr;
 #ifdef HS_TIMES
   dbg = blockIdx.x == HS_TIMES ? (uint64_t*)z : nullptr;
@@ -685,6 +687,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   const float bias2 = nx.b2[16 * (wid & 1) + (lane & 15)];
   conv12_core<SAVE_L1, false, true>(x8, nullptr, (float*)smem, b, nx.w1s, nx.b1, nx.W2,
                                     SAVE_L1 ? nx.act_l1 : nullptr, nx.act_l2, w2r, bias2);
+  span_end(srec);
   if (dbg) {
     __syncthreads();
     if (threadIdx.x == 0) dbg[10] = __builtin_readcyclecounter();

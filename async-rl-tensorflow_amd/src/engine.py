@@ -255,6 +255,14 @@ class Engine:
             exchange(self.grads)
         self.apply()
 
+    def span_stats(self, which, reset=False):
+        """Live launch spans recorded inside the graphs (which 0: k_conv_bwd, 1:
+        k_head_screen_conv12): reset=True clears; else (avg_us, max_us, launches)."""
+        avg, mx, cnt = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+        check(lib().a3c_engine_span_stats(self._h, int(which), 1 if reset else 0, ctypes.byref(avg),
+                                          ctypes.byref(mx), ctypes.byref(cnt)), 'a3c_engine_span_stats')
+        return float(avg.value), float(mx.value), int(cnt.value)
+
     def time_kernel(self, kernel, iters=20):
         """Average device ms of one engine kernel (HIP events on the current stream)."""
         out = ctypes.c_float()

@@ -163,6 +163,10 @@ def main():
         step()
     barrier()
     torch.cuda.synchronize()
+    live = not host and args.update != 'hogwild'
+    if live:                      # live launch spans of the dominant kernels, recorded in-graph
+        eng.span_stats(0, reset=True)
+        eng.span_stats(1, reset=True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -173,6 +177,10 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device='cuda')
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    spans = {}
+    if live:
+        spans['k_conv_bwd'] = eng.span_stats(0)
+        spans['k_head_screen_conv12'] = eng.span_stats(1)
     loss = eng.loss.cpu().numpy().tolist()
     finite = bool(torch.isfinite(eng.params).all().item())
 
@@ -203,10 +211,15 @@ def main():
             count['k_head_screen'] = n
             work['k_head_screen'] = ('hbm', ENV_STEP_BYTES * E)
         iter_ms = el / args.steps * 1e3
+        # live = the average in-graph launch span over the timed region (contended in overlap
+        # mode); avg_ms = the same kernel alone, back-to-back on the engine's buffers
+        live_ms = {k: spans[k][0] * 1e-3 for k in spans if k in ms and spans[k][2] > 0}
         for k in ms:
             bound, w = work[k]
             kernels[k] = dict(avg_ms=round(ms[k], 4), per_iter=count[k],
-                              share=round(ms[k] * count[k] / iter_ms, 3), bound=bound)
+                              share=round(live_ms.get(k, ms[k]) * count[k] / iter_ms, 3), bound=bound)
+            if k in live_ms:
+                kernels[k].update(live_avg_ms=round(live_ms[k], 4), live_launches=spans[k][2])
             if bound == 'hbm+mfma':
                 byt, flop = w
                 t_roof = byt / (PEAK_HBM_GBS * 1e9) + flop / (PEAK_FP32_TFLOPS * 1e12)
@@ -216,12 +229,18 @@ def main():
             else:
                 ach = w / (ms[k] * 1e-3) / (1e12 if bound == 'mfma' else 1e9)
                 kernels[k].update(achieved=round(ach, 2), unit='TFLOP/s' if bound == 'mfma' else 'GB/s')
-        dom = max(ms, key=lambda k: ms[k] * count[k])
+        dom = max(ms, key=lambda k: live_ms.get(k, ms[k]) * count[k])
         bound, w = work[dom]
+        t_dom = live_ms.get(dom, ms[dom])
+        combined = None
+        if bound == 'hbm+mfma':
+            byt, flop = w
+            combined = round((byt / PEAK_HBM_GBS / 1e9 + flop / PEAK_FP32_TFLOPS / 1e12) / (t_dom * 1e-3), 4)
         if bound == 'hbm+mfma':                  # report the phase that dominates its roofline time
             byt, flop = w
             bound, w = ('hbm', byt) if byt / PEAK_HBM_GBS / 1e9 >= flop / PEAK_FP32_TFLOPS / 1e12 else ('mfma', flop)
-        dom_ach = round(w / (ms[dom] * 1e-3) / (1e12 if bound == 'mfma' else 1e9), 2)
+        dom_ach = round(w / (t_dom * 1e-3) / (1e12 if bound == 'mfma' else 1e9), 2)
+        iso_ach = round(w / (ms[dom] * 1e-3) / (1e12 if bound == 'mfma' else 1e9), 2)
         peak = PEAK_FP32_TFLOPS if bound == 'mfma' else PEAK_HBM_GBS
         # HBM bytes per launch from the committed PMC passes (tools/profile_round.sh):
         # (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 FETCH_SIZE correction per MI355X_MICROARCH.md
@@ -236,7 +255,13 @@ def main():
         roofline = dict(kernel=dom, bound=bound, achieved=dom_ach, peak=peak,
                         unit='TFLOP/s' if bound == 'mfma' else 'GB/s',
                         frac=round(dom_ach / peak, 4), traffic=traffic,
+                        timing=('live: average in-graph launch span over the timed region (s_memrealtime, '
+                                'a3c_engine_span_stats)' if dom in live_ms else 'isolated (HIP events)'),
+                        avg_us=round(t_dom * 1e3, 2), isolated_us=round(ms[dom] * 1e3, 2),
+                        isolated_achieved=iso_ach,
                         work_per_launch=w, work_unit='FLOP' if bound == 'mfma' else 'B')
+        if combined is not None:   # two serial phases: (bytes/HBM peak + FLOP/MFMA peak) / time
+            roofline['frac_combined_hbm_mfma'] = combined
 
     if world > 1:
         dist.barrier()
