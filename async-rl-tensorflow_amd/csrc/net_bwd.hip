@@ -178,6 +178,20 @@ __device__ inline void glds_copy(const uint8_t* g, uint8_t* dst, int nbytes, int
 // workgroup barrier that keeps LDS-DMA loads in flight (retires LDS ops only)
 __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Debug builds only (-DCB_PHASES, tools/cb_phases.py): wave 0 of every workgroup sums the
+// s_memrealtime ticks of each phase over its samples -- staging, (a), (b), dl1 split, (c) -- and
+// writes them as u64[6] (last: the whole workgroup) over its own consumed l1 rows.
+#ifdef CB_PHASES
+#define CB_PH_INIT() uint64_t cb_ph_[6] = {0, 0, 0, 0, 0, 0}; uint64_t cb_t_ = __builtin_amdgcn_s_memrealtime(); const uint64_t cb_t0_ = cb_t_
+#define CB_PH(i) do { const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); cb_ph_[i] += t_ - cb_t_; cb_t_ = t_; } while (0)
+#define CB_PH_OUT(dst) do { if (threadIdx.x == 0) { cb_ph_[5] = __builtin_amdgcn_s_memrealtime() - cb_t0_; \
+    for (int i_ = 0; i_ < 6; ++i_) ((uint64_t*)(dst))[i_] = cb_ph_[i_]; } } while (0)
+#else
+#define CB_PH_INIT() ((void)0)
+#define CB_PH(i) ((void)0)
+#define CB_PH_OUT(dst) ((void)0)
+#endif
+
 template <bool DMA, int NW>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) k_conv_bwd(StateAddr sa, int64_t B, int per_wg,
                                                   const float* __restrict__ act_l1,
@@ -245,6 +259,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     glds_copy((const uint8_t*)(dl2 + bb * FLAT), dl2st, CB_DL2ST, wid, lane, NW);
   };
   if (DMA && b0 < b1) issue(b0, x8buf);
+  CB_PH_INIT();
 
   for (int64_t b = b0; b < b1; ++b) {
     uint8_t* x8 = x8buf + (DMA ? ((b - b0) & 1) * CB_X8 : 0);
@@ -263,19 +278,34 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
       __syncthreads();                                    // staging buffers free again
       if (b + 1 < b1) issue(b + 1, x8buf + ((b + 1 - b0) & 1) * CB_X8);
     } else {
+      // every load of the sample's l1 and dl2 rows in flight at once, then the LDS stores
+      constexpr int NL1 = (C1_P * 4 + NT - 1) / NT, ND2 = (C2_Q * 8 + NT - 1) / NT;
+      f32x4 rl1[NL1], rd2[ND2];
+      const f32x4* gl1 = (const f32x4*)(act_l1 + b * C1_P * C1_N);
+      const f32x4* gd2 = (const f32x4*)(dl2 + b * FLAT);
+#pragma unroll
+      for (int u = 0; u < NL1; ++u) rl1[u] = gl1[min(tid + NT * u, C1_P * 4 - 1)];
+#pragma unroll
+      for (int u = 0; u < ND2; ++u) rd2[u] = gd2[min(tid + NT * u, C2_Q * 8 - 1)];
       __syncthreads();                                    // previous sample done with LDS
-      stage_state(sa, b, tau0, x8);
-      for (int i = tid; i < C1_P * 4; i += NT) {
-        const int p = i >> 2, q4 = i & 3;
-        *(f32x4*)(l1s + p * CB_L1_LD + 4 * q4) = *(const f32x4*)(act_l1 + (b * C1_P + p) * C1_N + 4 * q4);
+#pragma unroll
+      for (int u = 0; u < NL1; ++u) {
+        const int i = tid + NT * u;
+        if (i < C1_P * 4) *(f32x4*)(l1s + (i >> 2) * CB_L1_LD + 4 * (i & 3)) = rl1[u];
       }
-      for (int i = tid; i < C2_Q * 8; i += NT) {
-        const int q = i >> 3, q4 = i & 7;
-        *(f32x4*)(dl2s + q * CB_DL2_LD + 4 * q4) = *(const f32x4*)(dl2 + b * FLAT + q * C2_N + 4 * q4);
+#pragma unroll
+      for (int u = 0; u < ND2; ++u) {
+        const int i = tid + NT * u;
+        if (i < C2_Q * 8) *(f32x4*)(dl2s + (i >> 3) * CB_DL2_LD + 4 * (i & 7)) = rd2[u];
       }
       if (tid < 8) *(f32x4*)(dl2s + C2_Q * CB_DL2_LD + 4 * tid) = (f32x4){0.f, 0.f, 0.f, 0.f};
       __syncthreads();
+      // the state planes are read in (c) only: DMA them global -> LDS now and let the copy run
+      // under phases (a) and (b) (their barriers retire LDS ops only)
+#pragma unroll
+      for (int c = 0; c < HIST; ++c) glds_copy(state_plane(sa, b, c, tau0), x8 + c * PLANE, PLANE, wid, lane, NW);
     }
+    CB_PH(0);
 
     // ---- (a) dW2[(kh,kw,ci)][n] += sum_q l1[2oy+kh][2ox+kw][ci] * dl2[q][n] ----
     for (int s = 0; s < (C2_Q + 3) / 4; ++s) {
@@ -296,6 +326,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     }
 
     lds_barrier();   // every wave done reading l1 in (a): (b) overwrites it with dl1
+    CB_PH(1);
 
     // ---- (b) dl1 for parity class (py,px): 100 positions in 7 M-tiles of 16 ----
     constexpr int MTB = NW == 8 ? 4 : 7;
@@ -348,6 +379,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
       db2acc += s2;
     }
     lds_barrier();   // dl1 complete in l1s
+    CB_PH(2);
     // dl1 -> three bf16 terms in dlb, which overlays l1s / dl2s: all reads first
     {
       constexpr int PER = (C1_P * C1_N + NT - 1) / NT;
@@ -381,7 +413,9 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
       const int row = i / C1_O, oy = i - row * C1_O;
       *(uint2*)(dlb + row * CB_DLB_LD + 8 * dlb_slot(3 * oy + 2, row & 15) + 4) = make_uint2(0u, 0u);
     }
-    lds_barrier();   // dl1 terms complete
+    if constexpr (!DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's x8 DMA landed
+    lds_barrier();   // dl1 terms complete (and every wave's x8 DMA)
+    CB_PH(3);
 
     // ---- (c) dW1[(kh,kw,cin)][n] += sum_p x[cin][4oy+kh][4ox+kw] * dl1[p][n]  (x unscaled) ----
     // v_mfma_f32_16x16x32_bf16: a u8 pixel is exact in bf16, dl1 = three bf16 terms, so every
@@ -428,6 +462,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
       if (c + 2 * c_step < 15) load_chunk(c + 2 * c_step, d0, b0);
       if (has1) mma_chunk(d1, b1);
     }
+    CB_PH(4);
   }
 
   // ---- write this workgroup's partial slab ----
@@ -477,6 +512,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
   }
   if (tid < C2_N) out[CB_OFF_B2 + tid] = db2acc;
   span_end(srec);
+  CB_PH_OUT(act_l1 + b0 * C1_P * C1_N);
   WG_T1(act_l1 + b0 * C1_P * C1_N);   // debug: over this workgroup's own (consumed) l1 rows
 }
 
