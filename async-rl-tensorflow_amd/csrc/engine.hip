@@ -745,7 +745,37 @@ extern "C" int a3c_engine_apply(a3c_engine* e, void* stream) {
   if (!e->grad_ready || e->grad_applied) return 0;
   // overlap: the snapshot is for the next rollout (iter), whose slot's previous rollout (iter - 2)
   // has just been back-propagated on this stream
-  return enqueue_apply(e, (int)(e->iter & 1), (hipStream_t)stream);
+  int rc = enqueue_apply(e, (int)(e->iter & 1), (hipStream_t)stream);
+  e->grad_applied = rc == 0;
+  return rc;
+}
+
+// Partitioned parameter server, step 1 (after the all-to-all of the clipped gradients): the
+// nranks sequential RMSProp steps of this rank's range [lo, lo + n); new weights -> w_out.
+extern "C" int a3c_engine_apply_shard(a3c_engine* e, const float* grads_by_rank, int nranks, int64_t lo, int64_t n,
+                                      float* w_out, void* stream) {
+  if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_apply_shard", "null");
+  if (nranks < 1 || lo < 0 || n < 0 || lo + n > e->L.total || (n > 0 && (!grads_by_rank || !w_out)))
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_apply_shard", "bad shard");
+  if (!e->grad_ready || e->grad_applied) return 0;
+  if (e->cfg.world_size == 1)   // one rank: the per-worker clip has not run (a3c_engine_apply fuses it)
+    return a3c_set_error(A3C_ERR_STATE, "a3c_engine_apply_shard", "world_size 1 engines use a3c_engine_apply");
+  const a3c_engine_config& c = e->cfg;
+  return a3c_apply_seq_launch(e->params + lo, e->ms + lo, e->mom + lo, grads_by_rank, nranks, n, e->sched, c.decay,
+                              c.momentum, c.epsilon, w_out, (hipStream_t)stream);
+}
+
+// Partitioned parameter server, step 2 (after the all-gather assembled every rank's range in
+// params_src, nullable = already in params): params / overlap snapshot / target sync, counters.
+extern "C" int a3c_engine_apply_commit(a3c_engine* e, const float* params_src, void* stream) {
+  if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_apply_commit", "null");
+  if (!e->grad_ready || e->grad_applied) return 0;
+  const OptParams op = opt_params(e);
+  float* snap = e->overlap ? e->slot[(int)(e->iter & 1)].P : nullptr;
+  int rc = a3c_commit_launch(params_src ? params_src : e->params, e->L.total, e->params, snap, op.target, e->sched,
+                             e->counters, op.dtau, op.step_add, (hipStream_t)stream);
+  e->grad_applied = rc == 0;
+  return rc;
 }
 
 // ---- external (host) environments (env workers feeding host RGB buffers) ----

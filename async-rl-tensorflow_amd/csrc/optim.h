@@ -40,3 +40,9 @@ int a3c_sumsq_launch(const float* grads, const TensorTab& tt, const OptParams& o
 int a3c_apply_launch(float* w, float* ms, float* mom, float* grads, const TensorTab& tt, const OptParams& op,
                      const double* part, float* sumsq_out, hipStream_t s);
 int a3c_fill_launch(float* p, int64_t n, float v, hipStream_t s);
+// partitioned PS: nranks sequential RMSProp steps of the owned range (lr = sched[0]) -> w_out
+int a3c_apply_seq_launch(const float* w, float* ms, float* mom, const float* g, int nranks, int64_t n,
+                         const float* sched, float rho, float momentum, float eps, float* w_out, hipStream_t s);
+// params / snapshot / target (if sched[1]) <- src, counters += (dtau, dstep)
+int a3c_commit_launch(const float* src, int64_t total, float* params, float* snap, float* target, const float* sched,
+                      int64_t* counters, int64_t dtau, int64_t dstep, hipStream_t s);

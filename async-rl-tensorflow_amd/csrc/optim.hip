@@ -60,7 +60,10 @@ __global__ void __launch_bounds__(256) k_sumsq(const float* __restrict__ g, Tens
     if (blockIdx.x == 0 && op.sched && op.step_ptr) {
       const int64_t g0 = *op.step_ptr;
       const double step = (double)(g0 + op.step_add);
-      op.sched[0] = (float)((double)(op.max_step - step + 1.0) / (double)op.max_step * op.lr0);
+      // agent.py:393-395; the reference never trains past max_step (agent.py:46,55-57), so the
+      // schedule is clamped at 0 there instead of turning negative (RMSProp would ascend)
+      const double lr = (double)(op.max_step - step + 1.0) / (double)op.max_step * op.lr0;
+      op.sched[0] = (float)(lr > 0.0 ? lr : 0.0);
       int copy = 0;
       if (op.target_period > 0)
         copy = (g0 + op.step_add + 1) / op.target_period != (g0 + 1) / op.target_period;
@@ -142,6 +145,77 @@ __global__ void __launch_bounds__(256) k_apply(float* __restrict__ w, float* __r
     if (op.dtau) op.counters[0] += op.dtau;   // overlap mode: the rollout owns tau
     op.counters[1] += op.step_add;
   }
+}
+
+// ---- partitioned parameter server (multi-GPU sequential exchange) ----------------------------
+// The reference's PS applies every worker's clipped gradient as an RMSProp step of its own, in
+// arrival order (one shared optimizer, main.py:63-65; each worker's apply_gradients, agent.py:321).
+// Rank r owns [lo, lo + n) of params / ms / mom.  After the all-to-all it holds every rank's
+// clipped gradient of that range (g + q*n, q = 0 .. nranks-1) and applies them one after the
+// other in rank order: one legal arrival order of the reference PS, and deterministic.  The new
+// weights go to w_out (the all-gather's input); ms / mom are updated in place (only the owner
+// reads its range).  The element math is k_apply's, so one rank reproduces it bit for bit.
+__global__ void __launch_bounds__(256) k_apply_seq(const float* __restrict__ w, float* __restrict__ ms,
+                                                   float* __restrict__ mom, const float* __restrict__ g,
+                                                   int nranks, int64_t n, const float* __restrict__ sched,
+                                                   float rho, float momentum, float eps,
+                                                   float* __restrict__ w_out) {
+#pragma clang fp contract(off)
+  const float lr = sched[0];
+  const float one_m_rho = 1.0f - rho;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float wv = w[i], m2 = ms[i], mo = mom[i];
+    for (int q = 0; q < nranks; ++q) {
+      const float gi = g[(int64_t)q * n + i];
+      m2 = m2 + (gi * gi - m2) * one_m_rho;
+      mo = mo * momentum + (gi * lr) / sqrtf(m2 + eps);
+      wv = wv - mo;
+    }
+    ms[i] = m2;
+    mom[i] = mo;
+    w_out[i] = wv;
+  }
+}
+
+int a3c_apply_seq_launch(const float* w, float* ms, float* mom, const float* g, int nranks, int64_t n,
+                         const float* sched, float rho, float momentum, float eps, float* w_out, hipStream_t s) {
+  if (n <= 0) return 0;
+  const int64_t blocks = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  hipLaunchKernelGGL(k_apply_seq, dim3((unsigned)blocks), dim3(256), 0, s, w, ms, mom, g, nranks, n, sched, rho,
+                     momentum, eps, w_out);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+// The rest of an apply once the all-gather has assembled the new parameters in src: params (and
+// the overlap pipeline's snapshot) <- src, target sync when the schedule flagged one (agent.py:
+// 166-167, 342-344), and block 0 advances the counters.  n4 = float4 count.
+__global__ void __launch_bounds__(256) k_commit(const float* __restrict__ src, int64_t n4, float* __restrict__ params,
+                                                float* __restrict__ snap, float* __restrict__ target,
+                                                const float* __restrict__ sched, int64_t* counters, int64_t dtau,
+                                                int64_t dstep) {
+  const bool tsync = target && sched[1] != 0.f;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+    const f32x4 v = ((const f32x4*)src)[q];
+    if (src != params) ((f32x4*)params)[q] = v;
+    if (snap) ((f32x4*)snap)[q] = v;
+    if (tsync) ((f32x4*)target)[q] = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
+    counters[0] += dtau;
+    counters[1] += dstep;
+  }
+}
+
+int a3c_commit_launch(const float* src, int64_t total, float* params, float* snap, float* target, const float* sched,
+                      int64_t* counters, int64_t dtau, int64_t dstep, hipStream_t s) {
+  const int64_t n4 = total >> 2;
+  int64_t blocks = (n4 + 255) / 256;
+  blocks = blocks > 1024 ? 1024 : (blocks < 1 ? 1 : blocks);
+  hipLaunchKernelGGL(k_commit, dim3((unsigned)blocks), dim3(256), 0, s, src, n4, params, snap, target, sched, counters,
+                     dtau, dstep);
+  A3C_CHECK(hipGetLastError());
+  return 0;
 }
 
 __global__ void k_fill(float* __restrict__ p, int64_t n, float v) {
@@ -228,6 +302,7 @@ extern "C" int a3c_copy_params(float* dst, const float* src, int64_t n, void* st
 __global__ void k_rmsprop_range(float* __restrict__ w, float* __restrict__ ms, float* __restrict__ mom,
                                 const float* __restrict__ g, int64_t n, const float* __restrict__ lr_dev, float lr,
                                 float rho, float momentum, float eps) {
+#pragma clang fp contract(off)
   const float l = lr_dev ? lr_dev[0] : lr;
   const float one_m_rho = 1.0f - rho;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {

@@ -61,9 +61,23 @@ def parse_flags(argv=None):
   p.add_argument('--max_step', type=int, default=None)
   p.add_argument('--log_every', type=int, default=100)
   p.add_argument('--update', choices=['overlap', 'sync', 'hogwild'], default='overlap',
-                 help='engine mode: stale-1 overlapped A3C, synchronous all-reduce, or Hogwild sharded PS')
+                 help='engine mode: stale-1 overlapped A3C, synchronous exchange, or Hogwild sharded PS')
+  p.add_argument('--exchange', choices=['sequential', 'sum'], default='sequential',
+                 help='multi-GPU sync/overlap exchange: sequential = partitioned PS applying every '
+                      "worker's clipped gradient as its own RMSProp step in rank order (the reference "
+                      'PS semantics); sum = one all-reduce, one RMSProp step of the summed gradients')
   p.add_argument('--logdir', default='./logs')
   return p.parse_args(argv)
+
+
+def initial_params(eng, action_size, algo, seed):
+  """Flat host parameters initialised as the reference does: conv weights
+  truncated_normal(0, 0.02) (agent.py:214), linear weights normal(0.02) (ops.py:36-37),
+  zero biases (ops.py:24,38-39)."""
+  from src.initializers import flatten_host, init_params
+  from src.kernels import param_names_shapes
+  ns = param_names_shapes(action_size, algo, lstm=eng.lstm)
+  return flatten_host(ns, eng.offsets, eng.params.numel(), init_params(ns, seed=seed))
 
 
 def run_engine(config, flags):
@@ -84,24 +98,30 @@ def run_engine(config, flags):
   eng = Engine(num_envs=E, n_step=flags.n_step, action_size=A, algo=flags.algo, start_lives=lives,
                num_frames=flags.num_frames, seed=flags.random_seed, env_id_base=rank * E, world_size=world,
                overlap=overlap, **opts)
-  eng.reset()
+  eng.reset(initial_params(eng, A, flags.algo, flags.random_seed))
   D.broadcast_params(eng.params, src=0)
   if flags.algo == 'q':
     eng.target_params.copy_(eng.params)
   if overlap:
     eng.reset()    # keeps the broadcast parameters, re-takes the pipeline snapshots
-  xch = D.GradExchange() if world > 1 else None
+  xch = None
+  if world > 1:
+    xch = D.PartitionedPS(eng.params.numel()) if flags.exchange == 'sequential' else D.GradExchange()
   ps = None
   if flags.update == 'hogwild':
     from src.hogwild import HogwildPS
     ps = HogwildPS(eng.params, decay=config.decay, momentum=config.momentum, epsilon=config.epsilon)
+  # the reference trains until the global step reaches max_step (agent.py:46,55-57): every
+  # applied update adds E*n*world env-steps, the overlap pipeline's first call applies none
+  per_update = E * flags.n_step * world
+  iterations = min(flags.iterations, -(-int(config.max_step) // per_update) + (1 if overlap else 0))
   torch.cuda.synchronize()
   t0 = time.time()
   log = None
   if rank == 0:
     os.makedirs(flags.logdir, exist_ok=True)
     log = open(os.path.join(flags.logdir, 'engine.jsonl'), 'a')
-  for it in range(flags.iterations):
+  for it in range(iterations):
     if ps is not None:
       eng.iterate_hogwild(ps)
     else:

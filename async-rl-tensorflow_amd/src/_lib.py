@@ -113,6 +113,8 @@ SIGNATURES = {
     'a3c_engine_slot_buffers': (c_int, [c_void_p, c_int, ctypes.POINTER(EngineBuffers)]),
     'a3c_engine_grad_ready': (c_int, [c_void_p]),
     'a3c_engine_advance': (c_int, [c_void_p, c_void_p]),
+    'a3c_engine_apply_shard': (c_int, [c_void_p, c_void_p, c_int, c_i64, c_i64, c_void_p, c_void_p]),
+    'a3c_engine_apply_commit': (c_int, [c_void_p, c_void_p, c_void_p]),
     'a3c_engine_ext_begin': (c_int, [c_void_p, c_void_p, c_void_p]),
     'a3c_hostenv_create': (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_u64, c_int, c_int,
                                    ctypes.POINTER(c_void_p)]),

@@ -7,8 +7,8 @@ Same constructor, attributes and loop as the reference.  The compute is on devic
   ops with autograd;
 * TD target (agent.py:176-190): a3c_td_target (fp64 arithmetic, as numpy does);
 * clip_by_norm(40) per tensor + RMSProp apply (agent.py:316-321, main.py:63-65):
-  a3c_clip_rmsprop_apply, after an optional RCCL SUM all-reduce over worker processes
-  (src/distributed.py replaces the parameter server);
+  a3c_clip_rmsprop_apply; with several worker processes every worker's clipped gradient is
+  applied as its own step, in rank order (src/distributed.py replaces the parameter server);
 * history (agent.py:18, history.py): device u8 frame stack.
 Exploration uses Python's ``random`` exactly like agent.py:141-151.  ``sv`` is any object with
 ``request_stop()`` and ``summary_computed(step, dict)`` (see ``Supervisor`` below).
@@ -24,7 +24,7 @@ import torch
 from . import kernels as K
 from . import ops
 from .base import BaseModel, load_checkpoint, save_checkpoint
-from .distributed import GradExchange
+from .distributed import GradExchange, gather_grads
 from .history import History
 from .utils import get_time
 
@@ -220,9 +220,11 @@ class Agent(BaseModel):
       grads, q_t = flat.grad.detach(), q.detach()
       loss = loss.detach()
     if self.exchange.world > 1:
+      # the PS applies every worker's clipped push as an RMSProp step of its own (main.py:63-65,
+      # agent.py:321): gather all workers' clipped gradients and apply them in rank order
       self.optimizer.clip_only(grads, self.offsets, self.sizes)
-      self.exchange(grads)
-      self.optimizer.apply_gradients(self.params, grads, self.offsets, self.sizes, lr=self.lr, clip=False)
+      for g in gather_grads(grads):
+        self.optimizer.apply_gradients(self.params, g, self.offsets, self.sizes, lr=self.lr, clip=False)
     else:
       self.optimizer.apply_gradients(self.params, grads, self.offsets, self.sizes, lr=self.lr)
 

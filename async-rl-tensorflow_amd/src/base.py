@@ -1,6 +1,11 @@
-"""BaseModel (base.py:13-41): copies the config's attributes onto the model (``_x`` -> ``x``),
-``model_dir`` / ``checkpoint_dir`` strings.  Checkpoints (the Saver of agent.py:29 /
-main.py:74-80) are written as ``.npz`` keyed by the TF variable names plus the step."""
+"""BaseModel (reference src/base.py:13-41) and the checkpoint format.
+
+The model copies every public attribute of its config onto itself (a leading underscore is
+dropped: ``_test_step`` -> ``test_step``), and derives ``model_dir`` from the config values
+(everything but ``display``), which the reference uses as the run / checkpoint directory.
+Checkpoints (the Saver of agent.py:29 / main.py:74-80) are ``.npz`` files keyed by the TF
+variable names plus the global step.
+"""
 import inspect
 import os
 import pprint
@@ -11,27 +16,37 @@ pp = pprint.PrettyPrinter().pprint
 
 
 def class_vars(obj):
-  return {k: v for k, v in inspect.getmembers(obj)
-          if not k.startswith('__') and not callable(k)}
+  """Public (non-dunder) members of a config class or object, as a dict."""
+  out = {}
+  for name, value in inspect.getmembers(obj):
+    if name.startswith('__') or callable(name):
+      continue
+    out[name] = value
+  return out
+
+
+def _config_attrs(config):
+  # tf.app.flags objects keep their values in __dict__['__flags']; plain classes do not
+  flags = getattr(config, '__dict__', {})
+  if isinstance(flags, dict) and '__flags' in flags:
+    return flags['__flags']
+  return class_vars(config)
+
+
+def _fmt(value):
+  return ','.join(str(v) for v in value) if isinstance(value, list) else value
 
 
 class BaseModel(object):
   """Abstract object representing an Reader model."""
+
   def __init__(self, config, verbose=True):
     self.config = config
-
-    try:
-      self._attrs = config.__dict__['__flags']
-    except (KeyError, AttributeError, TypeError):
-      self._attrs = class_vars(config)
+    self._attrs = _config_attrs(config)
     if verbose:
       pp(self._attrs)
-
-    self.config = config
-
-    for attr in self._attrs:
-      name = attr if not attr.startswith('_') else attr[1:]
-      setattr(self, name, getattr(self.config, attr))
+    for key in self._attrs:
+      setattr(self, key[1:] if key.startswith('_') else key, getattr(config, key))
 
   @property
   def checkpoint_dir(self):
@@ -39,12 +54,10 @@ class BaseModel(object):
 
   @property
   def model_dir(self):
-    model_dir = self.config.env_name
-    for k, v in self._attrs.items():
-      if not k.startswith('_') and k not in ['display']:
-        model_dir += "/%s-%s" % (k, ",".join([str(i) for i in v])
-            if type(v) == list else v)
-    return model_dir + '/'
+    parts = [self.config.env_name]
+    parts += ['%s-%s' % (k, _fmt(v)) for k, v in self._attrs.items()
+              if not k.startswith('_') and k != 'display']
+    return '/'.join(parts) + '/'
 
 
 def save_checkpoint(path, named_tensors, step):

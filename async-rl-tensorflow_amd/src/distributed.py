@@ -1,15 +1,30 @@
-"""Multi-GPU gradient exchange that replaces the TF parameter server (main.py:50-66).
+"""Multi-GPU update paths that replace the TF parameter server (main.py:50-66).
 
-The reference runs W worker processes that push per-worker-clipped gradients (agent.py:316-319)
-to a PS which applies shared RMSProp unlocked and asynchronously (main.py:64-65,
-``replica_device_setter`` main.py:60-62).  Here every GPU is one process (torch.distributed,
-backend "nccl" = RCCL over xGMI); each GPU clips its own gradient per tensor, the clipped
-gradients are SUMMED with one all-reduce of the flat fp32 vector (2.71 MB for Pong), and every
-GPU applies the identical RMSProp step to its replica of the parameters and slots.
+The reference runs W worker processes.  Each clips its own gradient per tensor
+(agent.py:316-319) and pushes it to the PS, whose shared RMSProp (main.py:63-65, rms slot
+initialised to 1) applies every push as an update of its own, unlocked, in arrival order
+(``replica_device_setter`` main.py:60-62, ``apply_gradients`` agent.py:321).  Here every GPU is
+one process (torch.distributed, backend "nccl" = RCCL over xGMI) and two exchanges exist:
 
-Semantics vs the reference: the sum of W clipped gradients is applied as ONE RMSProp step,
-where the reference applies W steps in arrival order; first-order equivalent, and
-deterministic (no lock-free races).  DESIGN.md "Multi-GPU".
+``PartitionedPS`` (default, ``--exchange sequential``): the PS partitioned across the GPUs.
+  Rank r owns a 1/W byte range of params / ms / mom.  Per iteration:
+    1. all-to-all of the clipped gradients: rank r receives every rank's gradient of its range;
+    2. ``a3c_engine_apply_shard``: the W RMSProp steps of the range, one per rank, in rank order;
+    3. all-gather of the updated ranges into every replica;
+    4. ``a3c_engine_apply_commit``: snapshot / target sync / counters.
+  That is the reference PS's update rule, W separate steps, in one fixed arrival order (rank
+  order), so it is deterministic and every replica is bit-identical.  Traffic per GPU equals a
+  ring all-reduce's: (W-1)/W of the 2.71 MB gradient out and in, twice.
+
+``GradExchange`` (``--exchange sum``): one SUM all-reduce, then every GPU applies ONE RMSProp
+  step of the summed gradient.  That is NOT the reference's rule: RMSProp divides by
+  sqrt(ms), and ms tracks the square of the gradient it is given, so once ms has warmed up a
+  summed step moves about lr*sign(g) where the reference's W steps move about W*lr*sign(g).
+  It learns up to W times slower per env-step and is kept only as the plain data-parallel
+  baseline (tests/test_dist_gloo.py shows the two rules differ).
+
+``sequential_apply`` is the agent-mode (one env per process) form of the PS rule: all-gather
+the clipped gradients, apply them in rank order.
 """
 import os
 
@@ -34,21 +49,118 @@ def init_from_env(backend=None):
     return rank, world, local
 
 
+def _world(group):
+    return dist.get_world_size(group) if dist.is_initialized() else 1
+
+
+def _rank(group):
+    return dist.get_rank(group) if dist.is_initialized() else 0
+
+
+def _host_staged(t, group):
+    """gloo moves CPU tensors only: device tensors are staged through host memory."""
+    return t.is_cuda and dist.is_initialized() and dist.get_backend(group) == 'gloo'
+
+
+def shard_ranges(total, world, align=64):
+    """(lo, n) of every rank: contiguous ranges of ceil(total / world) floats rounded up to
+    `align` (tensor offsets are 64-float aligned, so are the ranges); the last may be short."""
+    shard = -(-int(total) // int(world))
+    shard = -(-shard // align) * align
+    lo = [min(total, r * shard) for r in range(world)]
+    n = [min(total, (r + 1) * shard) - lo[r] for r in range(world)]
+    return shard, lo, n
+
+
+class PartitionedPS:
+    """Partitioned parameter server over ``torch.distributed`` (module docstring).  Handed to
+    ``Engine.iterate(exchange=...)``; performs the apply itself (``owns_apply``)."""
+
+    owns_apply = True
+
+    def __init__(self, total, group=None, device='cuda'):
+        self.group = group
+        self.world, self.rank = _world(group), _rank(group)
+        self.total = int(total)
+        self.shard, self.lo, self.n = shard_ranges(self.total, self.world)
+        r = self.rank
+        self.recv = torch.zeros(max(1, self.world * self.n[r]), dtype=torch.float32, device=device)
+        self.w_out = torch.zeros(self.shard, dtype=torch.float32, device=device)
+        self.gathered = torch.zeros(self.world * self.shard, dtype=torch.float32, device=device)
+
+    def all_to_all(self, grads):
+        """recv[q*n_r : (q+1)*n_r] <- rank q's gradient of this rank's range."""
+        r = self.rank
+        if self.world == 1:
+            self.recv[:self.n[0]].copy_(grads[:self.n[0]])
+            return self.recv
+        out_splits, in_splits = [self.n[r]] * self.world, list(self.n)
+        if _host_staged(grads, self.group):
+            out = torch.empty(self.recv.numel(), dtype=torch.float32)
+            dist.all_to_all_single(out, grads.cpu(), out_splits, in_splits, group=self.group)
+            self.recv.copy_(out)
+        else:
+            dist.all_to_all_single(self.recv[:self.world * self.n[r]], grads, out_splits, in_splits, group=self.group)
+        return self.recv
+
+    def all_gather(self):
+        """gathered[q*shard : q*shard + n_q] <- rank q's updated range."""
+        if self.world == 1:
+            self.gathered.copy_(self.w_out)
+        elif _host_staged(self.w_out, self.group):
+            out = torch.empty(self.gathered.numel(), dtype=torch.float32)
+            dist.all_gather_into_tensor(out, self.w_out.cpu(), group=self.group)
+            self.gathered.copy_(out)
+        else:
+            dist.all_gather_into_tensor(self.gathered, self.w_out, group=self.group)
+        return self.gathered
+
+    def apply(self, eng):
+        r = self.rank
+        self.all_to_all(eng.grads)
+        eng.apply_shard(self.recv, self.world, self.lo[r], self.n[r], self.w_out)
+        self.all_gather()
+        eng.apply_commit(self.gathered)
+
+
 class GradExchange:
-    """Callable handed to ``Engine.iterate(exchange=...)``: sum-all-reduce of the clipped grads."""
+    """Callable handed to ``Engine.iterate(exchange=...)``: SUM all-reduce of the clipped grads
+    (the plain data-parallel rule, NOT the reference PS's: module docstring)."""
 
     def __init__(self, group=None):
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.world = _world(group)
 
     def __call__(self, grads):
         if self.world > 1:
-            dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=self.group)
+            if _host_staged(grads, self.group):
+                h = grads.cpu()
+                dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+                grads.copy_(h)
+            else:
+                dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=self.group)
         return grads
+
+
+def gather_grads(grads, group=None):
+    """Every rank's flat gradient, in rank order (agent mode: one env per process)."""
+    world = _world(group)
+    if world == 1:
+        return [grads]
+    staged = _host_staged(grads, group)
+    src = grads.cpu() if staged else grads
+    out = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(out, src, group=group)
+    return [o.to(grads.device) for o in out] if staged else out
 
 
 def broadcast_params(t, src=0, group=None):
     """Start every replica from rank ``src``'s parameters (the PS's initial values)."""
     if dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.broadcast(t, src=src, group=group)
+        if _host_staged(t, group):
+            h = t.cpu()
+            dist.broadcast(h, src=src, group=group)
+            t.copy_(h)
+        else:
+            dist.broadcast(t, src=src, group=group)
     return t

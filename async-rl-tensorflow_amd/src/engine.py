@@ -172,15 +172,29 @@ class Engine:
     def grad_ready(self):
         return bool(lib().a3c_engine_grad_ready(self._h))
 
+    def apply_shard(self, grads_by_rank, nranks, lo, n, w_out):
+        """Partitioned PS step 1: nranks sequential RMSProp steps of [lo, lo+n) -> w_out."""
+        check(lib().a3c_engine_apply_shard(self._h, _lib.ptr(grads_by_rank), int(nranks), int(lo), int(n),
+                                           _lib.ptr(w_out), _lib.stream_handle()), 'a3c_engine_apply_shard')
+
+    def apply_commit(self, params_src=None):
+        """Partitioned PS step 2: params <- params_src, snapshot / target sync, counters."""
+        check(lib().a3c_engine_apply_commit(self._h, _lib.ptr(params_src), _lib.stream_handle()),
+              'a3c_engine_apply_commit')
+
     def iterate(self, exchange=None):
         """One iteration: rollout + gradient, [exchange(grads)], apply.  Single-GPU device-env
         engines without an exchange take the fused path (a3c_engine_iterate: the apply captured
-        into the same hipGraphs, bit-identical to rollout_grad() + apply())."""
+        into the same hipGraphs, bit-identical to rollout_grad() + apply()).  An exchange with
+        ``owns_apply`` (src.distributed.PartitionedPS) performs the apply itself."""
         if exchange is None and self.cfg.world_size == 1 and not self.external_env:
             check(lib().a3c_engine_iterate(self._h, _lib.stream_handle()), 'a3c_engine_iterate')
             return
         self.rollout_grad()
         if not self.grad_ready:          # overlap pipeline filling: no gradient yet
+            return
+        if getattr(exchange, 'owns_apply', False):
+            exchange.apply(self)
             return
         if exchange is not None:
             exchange(self.grads)
@@ -251,6 +265,9 @@ class Engine:
             pool.step(self._ext_actions.numpy())
             self.ext_observe(pool.rgb, pool.rewards, pool.terminals)
         self.rollout_grad()
+        if getattr(exchange, 'owns_apply', False):
+            exchange.apply(self)
+            return
         if exchange is not None:
             exchange(self.grads)
         self.apply()

@@ -64,6 +64,14 @@ def parse():
                     help='process group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the '
                          'multi-rank path with several ranks on one GPU)')
     ap.add_argument('--no-kernel-timing', action='store_true')
+    ap.add_argument('--exchange', default='sequential', choices=['sequential', 'sum'],
+                    help='N > 1 sync/overlap: sequential = partitioned PS (all-to-all, every worker\'s clipped '
+                         'gradient its own RMSProp step in rank order, all-gather: the reference PS rule); '
+                         'sum = one SUM all-reduce + one step (plain data parallel)')
+    ap.add_argument('--min-seconds', type=float, default=1.0,
+                    help='repeat the K-step timed window until about this much time is measured; value = '
+                         'median window rate, spread reported')
+    ap.add_argument('--max-windows', type=int, default=50)
     return ap.parse_args()
 
 
@@ -151,13 +159,29 @@ def main():
             eng.iterate(exchange)
 
     exchange = None
-    if world > 1:
-        def exchange(g):
-            dist.all_reduce(g, op=dist.ReduceOp.SUM)   # sync SUM of per-worker-clipped grads
+    if world > 1 and args.update != 'hogwild':
+        from src.distributed import GradExchange, PartitionedPS
+        exchange = PartitionedPS(eng.params.numel()) if args.exchange == 'sequential' else GradExchange()
 
     def barrier():
         if world > 1:
             dist.barrier()
+
+    def timed_window():
+        # exactly K steps between a barrier + device sync on both sides; max over ranks
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device='cuda')
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
 
     for _ in range(args.warmup):
         step()
@@ -167,16 +191,13 @@ def main():
     if live:                      # live launch spans of the dominant kernels, recorded in-graph
         eng.span_stats(0, reset=True)
         eng.span_stats(1, reset=True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device='cuda')
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    # a short K-step window is a few ms of GPU time: repeat it until ~min_seconds are measured
+    # (every rank derives the same count from the max-over-ranks first window) and report the
+    # median window with the spread
+    windows = [timed_window()]
+    nwin = max(1, min(args.max_windows, int(np.ceil(args.min_seconds / max(windows[0], 1e-9)))))
+    windows += [timed_window() for _ in range(nwin - 1)]
+    el = float(np.median(windows))
     spans = {}
     if live:
         spans['k_conv_bwd'] = eng.span_stats(0)
@@ -284,13 +305,20 @@ def main():
                        'parallelism': (f'dp{world} hogwild: unlocked RMSProp pushes into {world} IPC-mapped HBM '
                                        f'shards over xGMI, pull at rollout start, no collective'
                                        if args.update == 'hogwild' else
-                                       f'dp{world} all-reduce (RCCL) of per-worker-clipped grads')
+                                       f'dp{world} partitioned PS: RCCL all-to-all of per-worker-clipped grads, '
+                                       f'{world} sequential RMSProp steps per owned shard, RCCL all-gather'
+                                       if args.exchange == 'sequential' else
+                                       f'dp{world} all-reduce (RCCL) of per-worker-clipped grads, one summed step')
                        if world > 1 else 'dp1', 'hipgraph': not args.no_graph,
                        'update': {'overlap': 'overlap: rollout k uses params after update k-2 (A3C stale-1 async), '
                                              'backward+apply of k-1 concurrent with rollout k',
                                   'sync': 'synchronous: rollout -> backward -> apply',
                                   'hogwild': 'hogwild: sharded lock-free parameter server (reference PS semantics)'
                                   }[args.update]},
+            'timing': {'windows': len(windows), 'steps_per_window': args.steps,
+                       'window_ms': [round(w * 1e3, 3) for w in windows],
+                       'value_spread': [round(steps_total / max(windows), 1), round(steps_total / min(windows), 1)],
+                       'value_mean_over_windows': round(steps_total * len(windows) / sum(windows), 1)},
             'roofline': roofline, 'cpu_baseline': cpu, 'kernels': kernels,
             'final_loss': loss, 'params_finite': finite,
         }

@@ -311,6 +311,22 @@ int a3c_engine_grad_ready(a3c_engine* eng);
  * (Hogwild: the gradient went to the shared shards instead) */
 int a3c_engine_advance(a3c_engine* eng, void* stream);
 
+/* Partitioned parameter server: the multi-GPU form of the reference's PS (main.py:58-66), where
+ * every worker's per-worker-clipped gradient (agent.py:316-319) is its own RMSProp step on the
+ * shared variables (agent.py:321), applied in arrival order.  Rank r of W owns the flat range
+ * [lo, lo + n) of params / ms / mom.  Per iteration, after a3c_engine_rollout_grad (world_size > 1:
+ * grads hold this worker's clipped gradient):
+ *   host: all-to-all of grads -> grads_by_rank [W][n] (rank q's gradient of this range);
+ *   a3c_engine_apply_shard: the W RMSProp steps of the range, in rank order q = 0..W-1 (lr from the
+ *     device schedule), new weights -> w_out [n];
+ *   host: all-gather of every rank's w_out -> the full parameter vector;
+ *   a3c_engine_apply_commit: params <- params_src (nullable: already there), overlap snapshot,
+ *     target sync (q), counters -- the rest of a3c_engine_apply.
+ * Both are no-ops when no gradient is pending (overlap pipeline filling). */
+int a3c_engine_apply_shard(a3c_engine* eng, const float* grads_by_rank, int nranks, int64_t lo, int64_t n,
+                           float* w_out, void* stream);
+int a3c_engine_apply_commit(a3c_engine* eng, const float* params_src, void* stream);
+
 /* ----------------------------------------------------------------------------
  * External (host-stepped) environments, cfg.external_env = 1.  Per rollout:
  *   for t in 0..n-1:  a3c_engine_ext_act -> sync -> host steps every env with its action

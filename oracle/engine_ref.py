@@ -179,12 +179,31 @@ class EngineRef:
     def apply(self, clipped, advance_tau=True):
         """RMSProp apply (+ q target sync).  advance_tau=False: the caller advances tau at
         rollout time (the engine's overlap pipeline, where rollout k+1 precedes apply k)."""
+        return self.apply_sequence([clipped], advance_tau)
+
+    def apply_sequence(self, clipped_seq, advance_tau=True):
+        """The reference PS's rule for several workers (main.py:63-65, agent.py:321): every
+        worker's clipped gradient is an RMSProp step of its own, applied in the given (arrival)
+        order with this iteration's learning rate; then the target sync / counters once."""
+        h = self.h
+        lr = self.next_lr()
+        for clipped in clipped_seq:
+            for k in self.params:
+                R.rmsprop_apply(self.params[k], self.ms[k], self.mom[k], clipped[k].astype(np.float32), lr,
+                                h['decay'], h['momentum'], h['epsilon'])
+        self.finish_update(advance_tau)
+        return lr
+
+    def next_lr(self):
+        """Learning rate of the pending update (agent.py:393-395 at the step after it)."""
         h = self.h
         inc = self.n * self.E * self.world
-        lr = R.learning_rate(self.global_step + inc, h['max_step'], h['learning_rate'])
-        for k in self.params:
-            R.rmsprop_apply(self.params[k], self.ms[k], self.mom[k], clipped[k].astype(np.float32), lr,
-                            h['decay'], h['momentum'], h['epsilon'])
+        return R.learning_rate(self.global_step + inc, h['max_step'], h['learning_rate'])
+
+    def finish_update(self, advance_tau=True):
+        """Target sync (q, agent.py:166-167) and counter advance of an applied update."""
+        h = self.h
+        inc = self.n * self.E * self.world
         if self.algo == 'q':
             P = h['target_q_update_step']
             if (self.global_step + inc + 1) // P != (self.global_step + 1) // P:   # agent.py:166-167
@@ -192,4 +211,3 @@ class EngineRef:
         if advance_tau:
             self.tau += self.n
         self.global_step += inc
-        return lr

@@ -413,8 +413,9 @@ def rmsprop_apply(var, ms, mom, grad, lr, decay=0.99, momentum=0.0, epsilon=0.1)
 
 
 def learning_rate(step, max_step=80_000_000, learning_rate=0.0007):
-    """agent.py:393-395."""
-    return (max_step - step + 1.) / max_step * learning_rate
+    """agent.py:393-395.  The reference stops training at max_step (agent.py:46,55-57), where this
+    is still > 0; past it the build clamps at 0 (a negative rate would make RMSProp ascend)."""
+    return max(0.0, (max_step - step + 1.) / max_step * learning_rate)
 
 
 def epsilon_schedule(step, ep_start=1., ep_end=0.1, ep_end_t=4_000_000, learn_start=32):

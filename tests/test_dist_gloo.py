@@ -1,7 +1,14 @@
-"""World-size-2 CPU (gloo) test of the multi-GPU gradient exchange semantics used by bench.py:
-each rank runs the oracle iteration on its own env shard (env ids rank*E..), clips per tensor
-(agent.py:319), GradExchange SUM-all-reduces, every rank applies RMSProp; the replicas must stay
-bit-identical and equal a single-process application of the summed clipped gradients."""
+"""World-size-2 CPU (gloo) tests of the multi-GPU update paths (src/distributed.py).
+
+Each rank runs the oracle iteration on its own env shard (env ids rank*E..) and clips per tensor
+(agent.py:319).  Then:
+* PartitionedPS (the default exchange): the real all-to-all / all-gather protocol drives a
+  CPU stand-in of the engine's shard apply (oracle RMSProp on flat arrays).  The replicas must
+  stay bit-identical and equal ONE process applying rank 0's then rank 1's clipped gradient as
+  two RMSProp steps (EngineRef.apply_sequence) -- the reference PS's rule (main.py:63-65,
+  agent.py:321) in rank order.
+* GradExchange (``--exchange sum``): SUM all-reduce, one step of the sum, for comparison.
+And, without processes: the summed single step is NOT the reference's W steps."""
 import os
 import socket
 
@@ -10,6 +17,8 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -20,19 +29,60 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out):
+def _setup_paths():
     import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [root, os.path.join(root, 'async-rl-tensorflow_amd')]
+    for p in (ROOT, os.path.join(ROOT, 'async-rl-tensorflow_amd')):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+class _CpuShardEngine:
+    """The engine's partitioned-PS interface (apply_shard / apply_commit) over an EngineRef:
+    flat float32 params / ms / mom in the oracle's name order, RMSProp from oracle/ref_cpu."""
+
+    def __init__(self, ref, names):
+        self.ref, self.names = ref, names
+        self.sizes = [ref.params[n].size for n in names]
+        self.flat = lambda d: np.concatenate([d[n].reshape(-1) for n in names]).astype(np.float32)
+        self.ms, self.mom = self.flat(ref.ms), self.flat(ref.mom)
+        self.grads = None
+
+    def set_grads(self, clipped):
+        self.grads = torch.as_tensor(self.flat(clipped))
+
+    def apply_shard(self, recv, nranks, lo, n, w_out):
+        from oracle import ref_cpu as R
+        h = self.ref.h
+        lr = self.ref.next_lr()
+        w = self.flat(self.ref.params)[lo:lo + n].copy()
+        g = recv.numpy()[:nranks * n].reshape(nranks, n)
+        for q in range(nranks):                     # rank order: one arrival order of the PS
+            R.rmsprop_apply(w, self.ms[lo:lo + n], self.mom[lo:lo + n], g[q], lr, h['decay'], h['momentum'],
+                            h['epsilon'])
+        w_out[:n] = torch.as_tensor(w)
+
+    def apply_commit(self, gathered):
+        flat = gathered.numpy()[:sum(self.sizes)]
+        parts = np.split(flat, np.cumsum(self.sizes)[:-1])
+        for name, part in zip(self.names, parts):
+            self.ref.params[name] = part.reshape(self.ref.params[name].shape).astype(np.float32).copy()
+        self.ref.finish_update()
+
+
+def _init(rank, world, port):
+    _setup_paths()
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
-    from src.distributed import GradExchange, broadcast_params, init_from_env
-    from src.initializers import init_params
-    from src.kernels import param_names_shapes
-    from oracle.engine_ref import EngineRef
-    from oracle import ref_cpu as R
+    from src.distributed import init_from_env
     r, w, _ = init_from_env(backend='gloo')
     assert (r, w) == (rank, world)
+
+
+def _shared_start(rank):
+    """Every rank starts from rank 0's parameters (broadcast, as main.py / bench.py do)."""
+    from src.distributed import broadcast_params
+    from src.initializers import init_params
+    from src.kernels import param_names_shapes
     ns = param_names_shapes(6, 'a3c')
     p = init_params(ns, seed=5 + rank, stddev=0.08)       # different on purpose: broadcast fixes it
     names = [n for n, _ in ns]
@@ -40,42 +90,59 @@ def _worker(rank, world, port, out):
     broadcast_params(flat, src=0)
     sizes = [int(np.prod(s)) for _, s in ns]
     parts = torch.split(flat, sizes)
-    p = {n: parts[i].reshape(s).numpy().copy() for i, (n, s) in enumerate(ns)}
+    return {n: parts[i].reshape(s).numpy().copy() for i, (n, s) in enumerate(ns)}, names
+
+
+def _worker_partitioned(rank, world, port, out):
+    _init(rank, world, port)
+    from src.distributed import PartitionedPS
+    from oracle.engine_ref import EngineRef
+    p, names = _shared_start(rank)
     ref = EngineRef(p, 3, 2, 6, 'a3c', 0, 16, seed=9, env_id_base=rank * 3, world_size=world)
     ref.reset()
-    xch = GradExchange()
-    history = []
-    for it in range(2):
+    eng = _CpuShardEngine(ref, names)
+    ps = PartitionedPS(sum(ref.params[n].size for n in names), device='cpu')
+    mine = []
+    for it in range(3):
         o = ref.iterate()
-        g = torch.cat([torch.as_tensor(o['clipped'][n]).reshape(-1) for n in names])
-        mine = g.clone()
-        xch(g)                                             # SUM over ranks
-        gs = torch.split(g, sizes)
-        summed = {n: gs[i].reshape(ref.params[n].shape).numpy().copy() for i, n in enumerate(names)}
-        ref.apply(summed)
-        history.append(mine.numpy())
-    flat_p = np.concatenate([ref.params[n].reshape(-1) for n in names])
-    out[rank] = dict(params=flat_p, grads=history)
+        eng.set_grads(o['clipped'])
+        mine.append(eng.grads.numpy().copy())
+        ps.apply(eng)
+    out[rank] = dict(params=eng.flat(ref.params), grads=mine, ms=eng.ms.copy(), lo=ps.lo, n=ps.n)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.timeout(300)
-def test_gloo_two_rank_sync_exchange():
-    world = 2
+def _worker_sum(rank, world, port, out):
+    _init(rank, world, port)
+    from src.distributed import GradExchange
+    from oracle.engine_ref import EngineRef
+    p, names = _shared_start(rank)
+    ref = EngineRef(p, 3, 2, 6, 'a3c', 0, 16, seed=9, env_id_base=rank * 3, world_size=world)
+    ref.reset()
+    xch = GradExchange()
+    for it in range(2):
+        o = ref.iterate()
+        g = torch.cat([torch.as_tensor(o['clipped'][n]).reshape(-1) for n in names])
+        xch(g)                                             # SUM over ranks
+        gs = torch.split(g, [ref.params[n].size for n in names])
+        ref.apply({n: gs[i].reshape(ref.params[n].shape).numpy().copy() for i, n in enumerate(names)})
+    out[rank] = dict(params=np.concatenate([ref.params[n].reshape(-1) for n in names]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _spawn(fn, world=2):
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
-        res = dict(out)
-    # replicas identical
-    assert np.array_equal(res[0]['params'], res[1]['params'])
-    # the two shards saw different envs -> different local gradients
-    assert not np.allclose(res[0]['grads'][0], res[1]['grads'][0])
-    # single-process restatement: both shards' clipped grads summed, one RMSProp step each iteration
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [root, os.path.join(root, 'async-rl-tensorflow_amd')]
+        mp.spawn(fn, args=(world, port, out), nprocs=world, join=True)
+        return dict(out)
+
+
+def _replay(world, iters, combine):
+    """Single process: every shard's EngineRef from rank 0's parameters, combine(refs, outs)."""
+    _setup_paths()
     from src.initializers import init_params
     from src.kernels import param_names_shapes
     from oracle.engine_ref import EngineRef
@@ -85,10 +152,56 @@ def test_gloo_two_rank_sync_exchange():
     refs = [EngineRef(p, 3, 2, 6, 'a3c', 0, 16, seed=9, env_id_base=r * 3, world_size=world) for r in range(world)]
     for r in refs:
         r.reset()
-    for it in range(2):
-        outs = [r.iterate() for r in refs]
-        summed = {n: sum(o['clipped'][n] for o in outs).astype(np.float32) for n in names}
+    for _ in range(iters):
+        combine(refs, [r.iterate() for r in refs], names)
+    return np.concatenate([refs[0].params[n].reshape(-1) for n in names])
+
+
+@pytest.mark.timeout(300)
+def test_gloo_two_rank_partitioned_ps_is_the_reference_ps_rule():
+    world = 2
+    res = _spawn(_worker_partitioned, world)
+    assert np.array_equal(res[0]['params'], res[1]['params'])           # replicas identical
+    assert not np.allclose(res[0]['grads'][0], res[1]['grads'][0])      # different shards, grads
+    assert res[0]['lo'] == [0, res[0]['n'][0]] and sum(res[0]['n']) == res[0]['params'].size
+
+    def sequential(refs, outs, names):
         for r in refs:
-            r.apply(summed)
-    flat = np.concatenate([refs[0].params[n].reshape(-1) for n in names])
-    np.testing.assert_allclose(res[0]['params'], flat, rtol=1e-6, atol=1e-9)
+            r.apply_sequence([o['clipped'] for o in outs])             # rank 0's step, then rank 1's
+    flat = _replay(world, 3, sequential)
+    np.testing.assert_array_equal(res[0]['params'], flat)
+
+
+@pytest.mark.timeout(300)
+def test_gloo_two_rank_sum_exchange():
+    world = 2
+    res = _spawn(_worker_sum, world)
+    assert np.array_equal(res[0]['params'], res[1]['params'])
+
+    def summed(refs, outs, names):
+        s = {n: sum(o['clipped'][n] for o in outs).astype(np.float32) for n in names}
+        for r in refs:
+            r.apply(s)
+    np.testing.assert_allclose(res[0]['params'], _replay(world, 2, summed), rtol=1e-6, atol=1e-9)
+
+
+def test_summed_step_is_not_the_reference_ps_rule():
+    """Once the rms slot has adapted, one RMSProp step of the sum of W equal gradients moves
+    about lr*sign(g) per iteration, while the reference's W separate pushes move about
+    W*lr*sign(g): the summed rule learns up to W times slower."""
+    _setup_paths()
+    from oracle import ref_cpu as R
+    W, lr, iters = 8, 7e-4, 1000
+    g = np.full(64, 0.5, np.float32)
+
+    def run(steps_per_iter, grad):
+        v, ms, mom = np.zeros(64, np.float32), np.ones(64, np.float32), np.zeros(64, np.float32)
+        for _ in range(iters):
+            before = float(v[0])
+            for _ in range(steps_per_iter):
+                R.rmsprop_apply(v, ms, mom, grad, lr)
+        return before - float(v[0])                                    # last iteration's move
+    seq = run(W, g)                                                    # the reference PS
+    summed = run(1, (W * g).astype(np.float32))                        # all-reduce + one step
+    assert seq > 0.0 and summed > 0.0
+    assert seq / summed > 0.75 * W

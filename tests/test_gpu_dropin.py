@@ -352,3 +352,33 @@ def test_main_engine_mode_runs(tmp_path, update):
     assert torch.isfinite(eng.params).all()
     lines = open(tmp_path / 'engine.jsonl').read().splitlines()
     assert len(lines) == 2
+
+
+def test_main_engine_mode_initialises_params_and_stops_at_max_step(tmp_path):
+    """main.py --mode engine starts from the reference initialisers (conv truncated_normal(0,
+    0.02) agent.py:214, linear normal(0.02) ops.py:36-37, zero biases), not from whatever
+    hipMalloc returned, and trains no further than max_step (agent.py:46,55-57)."""
+    import main
+    from src.kernels import param_names_shapes
+    E, n = 16, 5
+    eng = main.main(['--mode', 'engine', '--env_name', 'Pong-v0', '--num_envs', str(E), '--num_frames', '64',
+                     '--iterations', '50', '--log_every', '100', '--logdir', str(tmp_path), '--update', 'sync',
+                     '--max_step', str(3 * E * n - 1), '--random_seed', '7'])
+    torch.cuda.synchronize()
+    assert int(eng.counters[1].item()) == 3 * E * n          # 3 updates reach max_step, then stop
+    flat = eng.params.cpu().numpy()
+    ns = param_names_shapes(6, 'a3c')
+    for (name, shp), off, size in zip(ns, eng.offsets, eng.sizes):
+        v = flat[off:off + size]
+        if name.endswith('_b'):
+            assert np.abs(v).max() < 0.05, name              # zero-initialised, 3 small updates
+        else:
+            assert abs(float(v.std()) - 0.02) < 0.006, (name, float(v.std()))
+            assert np.count_nonzero(v) == v.size
+    # past max_step the schedule is clamped at 0 (agent.py:393-395 would turn negative)
+    from src.engine import _view
+    before = eng.params.clone()
+    eng.iterate()
+    torch.cuda.synchronize()
+    assert _view(eng.sched_ptr, (2,), torch.float32)[0].item() == 0.0
+    assert torch.equal(before, eng.params)

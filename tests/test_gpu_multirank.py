@@ -90,6 +90,81 @@ def test_two_ranks_stay_identical_and_match_manual_exchange(overlap):
     np.testing.assert_array_equal(engs[0].params.cpu().numpy(), res[0]['params'])
 
 
+# ------------------------------------------------------- partitioned PS (default multi-GPU exchange)
+def _pps_worker(rank, world, port, overlap, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, 'async-rl-tensorflow_amd')]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK='0')
+    import torch.distributed as dist
+    from src.distributed import PartitionedPS
+    dist.init_process_group('gloo')
+    eng = _make(rank, world, overlap)
+    ps = PartitionedPS(eng.params.numel())
+    for _ in range(ITERS):
+        eng.iterate(exchange=ps)
+    torch.cuda.synchronize()
+    out[rank] = dict(params=eng.params.cpu().numpy(), step=int(eng.counters[1].item()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('overlap', [False, True])
+def test_partitioned_ps_two_ranks(overlap):
+    """Two ranks on one GPU (gloo, host-staged collectives) run the default multi-GPU exchange:
+    all-to-all of the clipped gradients, each rank's W sequential RMSProp steps on its range,
+    all-gather.  Replicas stay identical and equal one process driving both shards through the
+    same C-ABI by hand; in sync mode that also equals applying rank 0's then rank 1's clipped
+    gradient to full copies with a3c_rmsprop_range (the reference PS rule, rank order)."""
+    import ctypes
+    import torch.multiprocessing as mp
+    from src._lib import lib, ptr, stream_handle
+    from src.distributed import shard_ranges
+    world = 2
+    ctx = mp.get_context('spawn')
+    with ctx.Manager() as m:
+        out = m.dict()
+        port = _free_port()
+        procs = [ctx.Process(target=_pps_worker, args=(r, world, port, overlap, out)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(500)
+            assert p.exitcode == 0
+        res = dict(out)
+    assert np.array_equal(res[0]['params'], res[1]['params'])
+    assert res[0]['step'] == res[1]['step'] == ITERS * N * E * world - (N * E * world if overlap else 0)
+    engs = [_make(r, world, overlap) for r in range(world)]
+    total = engs[0].params.numel()
+    shard, lo, n = shard_ranges(total, world)
+    w_out = [torch.zeros(shard, device='cuda') for _ in range(world)]
+    if not overlap:
+        w = engs[0].params.clone()
+        ms, mom = torch.ones_like(w), torch.zeros_like(w)
+    for _ in range(ITERS):
+        for e in engs:
+            e.rollout_grad()
+        if not engs[0].grad_ready:
+            continue
+        if not overlap:
+            for e in engs:
+                lib().a3c_rmsprop_range(ptr(w), ptr(ms), ptr(mom), ptr(e.grads), total, ctypes.c_void_p(e.sched_ptr),
+                                        0.0, 0.99, 0.0, 0.1, stream_handle())
+        for r, e in enumerate(engs):
+            recv = torch.cat([engs[q].grads[lo[r]:lo[r] + n[r]] for q in range(world)])
+            e.apply_shard(recv, world, lo[r], n[r], w_out[r])
+        gathered = torch.cat(w_out)
+        for e in engs:
+            e.apply_commit(gathered)
+    torch.cuda.synchronize()
+    assert torch.equal(engs[0].params, engs[1].params)
+    np.testing.assert_array_equal(engs[0].params.cpu().numpy(), res[0]['params'])
+    if not overlap:
+        np.testing.assert_array_equal(w.cpu().numpy(), res[0]['params'])
+
+
 # ------------------------------------------------------------------ Hogwild (SURVEY §8(e) async)
 def _hog_worker(rank, world, port, out, lockstep):
     import sys
