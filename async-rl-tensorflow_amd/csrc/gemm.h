@@ -24,14 +24,6 @@ struct GemmArgs {
 };
 
 int a3c_gemm(bool a_kcontig, bool b_ncontig, GemmArgs g, hipStream_t s);
-// fc backward (gemm.hip): C = (A B^T) * (mask > 0) with A [M][K], B [N][K] k-contiguous, K % 8 == 0
-int a3c_gemm_nt_mask(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
-                     const float* mask, int64_t ldm, int M, int N, int K, hipStream_t s);
-// C = A^T B with A [K][M], B [K][N]; K split over nsplit workgroups folded in-launch (slab:
-// nsplit * tiles * 4096 floats, cnt: tiles zeroed words, tiles = ceil(M/64) * ceil(N/64));
-// colsum (nullable) [nsplit][N] per-split column sums of B
-int a3c_gemm_tn_splitk(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int M, int N,
-                       int K, int nsplit, float* slab, uint32_t* cnt, float* colsum, hipStream_t s);
 int a3c_gemm_plan_split(int M, int N, int K, int target_blocks);
 
 inline int a3c_gemm_effective_split(int K, int nsplit) {

@@ -131,10 +131,7 @@ struct HeadSelect {
 #define PREP_BYTES (PREP_W2F_OFF + W2F_ELEMS * 3 * 2)
 // fc forward split-K scratch after the prepared weights: per-tile arrival counters (zeroed by
 // k_prep_fwd, reset by each tile's last workgroup) then the partial slabs [FC_SPLIT][tiles][1024]
-#ifndef FC_SPLIT
 #define FC_SPLIT 4                      // workgroups per 32x32 output tile (K split)
-#endif
-#define FC_SPLIT_MAX 8                  // slab scratch is sized for this many
 #define FC_ROWS_MAX 16384               // rows per launch (longer batches: several launches)
 #define FC_CNT_MAX ((FC_ROWS_MAX / 32) * (FC / 32))   // 4096 tiles
 #define PREP_FC_CNT_OFF (((PREP_BYTES) + 255) / 256 * 256)
@@ -142,7 +139,7 @@ struct HeadSelect {
 // bytes of a prep buffer whose forward runs batches of up to M rows
 inline int64_t a3c_prep_bytes(int64_t M) {
   const int64_t rows = ((M < FC_ROWS_MAX ? M : FC_ROWS_MAX) + 31) / 32 * 32;
-  return PREP_FC_SLAB_OFF + (int64_t)FC_SPLIT_MAX * rows * FC * 4;
+  return PREP_FC_SLAB_OFF + (int64_t)FC_SPLIT * rows * FC * 4;
 }
 struct LstmStep;
 // the next state's conv1 + conv2, fused into rollout step t's head + screen kernel

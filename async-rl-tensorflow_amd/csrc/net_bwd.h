@@ -26,10 +26,8 @@ struct FinalizeSegs {
 
 struct BwdPlan {
   int nwg, per_wg, head_split, fc_split, groups;
-  int64_t dz, dh3, dl2, terms, hgrad, hcol, hslab, fccol, fcslab, fccnt, cslab, cgroup, total;  // float offsets
+  int64_t dz, dh3, dl2, terms, hgrad, hcol, hslab, fccol, fcslab, cslab, cgroup, total;  // float offsets
 };
-#define FCB_SPLIT 4                                  // K split of the fc weight-gradient GEMM
-#define FCB_TILES (((FLAT + 63) / 64) * (FC / 64))   // its 64x64 output tiles (164)
 
 // optional fused n-step returns in the head backward (engine a3c path)
 struct ReturnsArgs {

@@ -57,11 +57,8 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ z, i
                                                   const float* __restrict__ Wv, float beta,
                                                   int literal, float invB, int64_t B,
                                                   float* __restrict__ dz, float* __restrict__ dh3,
-                                                  float* __restrict__ terms, ReturnsArgs ra, int relu,
-                                                  uint32_t* __restrict__ zero_cnt) {
+                                                  float* __restrict__ terms, ReturnsArgs ra, int relu) {
   const int lane = threadIdx.x & 63;
-  // the fc weight-gradient GEMM's split-K counters: zero before it runs (it follows this launch)
-  if (blockIdx.x == 0 && zero_cnt) zero_cnt[threadIdx.x] = 0u;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
   const float myz = lane < zs ? z[b * zs + lane] : 0.f;
@@ -596,10 +593,7 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   const int nwg_alloc = std::max(count(nwg_shared, per_alloc), count(nwg_own, per_alloc));
   p.nwg = count(a3c_shared_gpu() ? nwg_shared : nwg_own, p.per_wg);
   p.head_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FC, L.zs, (int)B, 128));
-  {  // the effective K split of a3c_gemm_tn_splitk (its colsum partials are folded by k_finalize)
-    const int64_t kper = ((B + FCB_SPLIT - 1) / FCB_SPLIT + 7) / 8 * 8;
-    p.fc_split = (int)((B + kper - 1) / kper);
-  }
+  p.fc_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FLAT, FC, (int)B, 512));
   p.dz = take(B * L.zs);
   p.dh3 = take(B * FC);
   p.dl2 = take(B * FLAT);
@@ -608,8 +602,7 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   p.hcol = take((int64_t)p.head_split * L.zs);
   p.hslab = take(p.head_split > 1 ? (int64_t)p.head_split * FC * L.zs : 0);
   p.fccol = take((int64_t)p.fc_split * FC);
-  p.fcslab = take((int64_t)FCB_SPLIT * FCB_TILES * 4096);
-  p.fccnt = take(256);                       // split-K arrival counters (zeroed by k_head_bwd)
+  p.fcslab = take(p.fc_split > 1 ? (int64_t)p.fc_split * FLAT * FC : 0);
   p.cslab = take((int64_t)nwg_alloc * CB_SLAB);
   p.groups = p.nwg < 16 ? p.nwg : 16;
   p.cgroup = take((int64_t)16 * CB_SLAB);    // groups <= 16 in either mode
@@ -640,8 +633,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   const float* head_in = lb ? lb->h : act_l3;
   hipLaunchKernelGGL(k_head_bwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, z, L.zs, L.A, L.algo,
                      actions, target, head_in, P + L.off[T_HW], a3c ? P + L.off[T_VW] : nullptr, beta,
-                     literal, 1.0f / (float)B, B, dz, lb ? lb->dh : dh3, terms, ra, lb ? 0 : 1,
-                     (uint32_t*)(ws + p.fccnt));
+                     literal, 1.0f / (float)B, B, dz, lb ? lb->dh : dh3, terms, ra, lb ? 0 : 1);
   A3C_CHECK(hipGetLastError());
   if (lb) {
     // truncated BPTT: dL/dh_t -> dl3 (masked by the fc ReLU) + the gate-matrix gradients
@@ -670,16 +662,26 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   int rc = a3c_gemm(false, true, g, ws_s);
   if (rc) return rc;
 
-  // fc weights: dW[2592][256] = l2^T dl3 -> grads directly (in-launch split-K fold);
-  // db = colsum(dl3) per split -> k_finalize
-  rc = a3c_gemm_tn_splitk(act_l2, FLAT, dh3, FC, grads + L.off[T_FCW], FC, FLAT, FC, (int)B, p.fc_split,
-                          ws + p.fcslab, (uint32_t*)(ws + p.fccnt), ws + p.fccol, ws_s);
+  // fc weights: dW[2592][256] = l2^T dl3 -> grads directly ; db = colsum(dl3)
+  g = GemmArgs{};
+  g.A = act_l2; g.lda = FLAT;
+  g.B = dh3; g.ldb = FC;
+  g.C = grads + L.off[T_FCW]; g.ldc = FC;
+  g.M = FLAT; g.N = FC; g.K = (int)B;
+  g.epi = EPI_STORE; g.slab = ws + p.fcslab; g.nsplit = p.fc_split; g.colsum = ws + p.fccol;
+  rc = a3c_gemm(false, true, g, ws_s);
   if (rc) return rc;
 
   if (fork) A3C_CHECK(hipEventRecord(ev_join, side));
 
-  // dl2[B][2592] = (dl3 W^T) * (l2 > 0): A = dl3 [B][256], B = W [2592][256], both k-contiguous
-  rc = a3c_gemm_nt_mask(dh3, FC, P + L.off[T_FCW], FC, dl2, FLAT, act_l2, FLAT, (int)B, FLAT, FC, s);
+  // dl2[B][2592] = (dl3 W^T) * (l2 > 0)
+  g = GemmArgs{};
+  g.A = dh3; g.lda = FC;                 // A(m=b, k) = dl3[b][k]
+  g.B = P + L.off[T_FCW]; g.ldb = FC;    // B(k, n) = W[n][k]
+  g.C = dl2; g.ldc = FLAT;
+  g.M = (int)B; g.N = FLAT; g.K = FC;
+  g.epi = EPI_MASK; g.mask = act_l2; g.ldm = FLAT; g.nsplit = 1;
+  rc = a3c_gemm(true, false, g, s);
   if (rc) return rc;
 
   rc = a3c_conv_bwd_launch(L, P, sa, B, act_l1, dl2, ws, s);

@@ -837,9 +837,7 @@ void a3c_conv12_set_smem() {
 // the fold runs in a fixed order, so the result does not depend on which workgroup is last).
 // Grid: x = tile (row tile * 8 + column tile), y = K split.
 // ---------------------------------------------------------------------------------------
-#ifndef FC_WAVES
 #define FC_WAVES 4
-#endif
 template <int SPLIT>
 __global__ void __launch_bounds__(64 * FC_WAVES) k_fc_fwd(const float* __restrict__ A, const float* __restrict__ Wk,
                                                           const float* __restrict__ bias, float* __restrict__ C,
@@ -851,37 +849,33 @@ __global__ void __launch_bounds__(64 * FC_WAVES) k_fc_fwd(const float* __restric
   const int tile = blockIdx.x, mt = tile >> 3, ct = tile & 7;
   const int m0 = 32 * mt, n0 = 32 * ct;
   WG_T0();
-  // this wave's chunks [c0, c1) of the 324: the K range split as evenly as possible, NMAX or
-  // NMAX - 1 chunks per wave.  The loop is fully unrolled over NMAX with a D-deep register ring:
-  // every load is issued unconditionally (index clamped into the range) so hipcc keeps them in
-  // flight with counted waits, and only the last chunk's A operand is masked to zero when the
-  // wave has one fewer
-  constexpr int NPART = SPLIT * FC_WAVES;
-  constexpr int NMAX = (FC_NCH + NPART - 1) / NPART;
-  constexpr int D = NMAX < 8 ? NMAX : 8;                 // chunks in flight per wave
+  // this wave's chunks [c0, c1) of the 324: the K range split as evenly as possible
   const int part = blockIdx.y * FC_WAVES + wid;
-  const int c0 = (part * FC_NCH) / NPART, c1 = ((part + 1) * FC_NCH) / NPART;
+  const int c0 = (part * FC_NCH) / (SPLIT * FC_WAVES), c1 = ((part + 1) * FC_NCH) / (SPLIT * FC_WAVES);
   const float* a = A + (int64_t)min(m0 + i32, M - 1) * FLAT + 4 * h;
   const f32x4* b = (const f32x4*)Wk + (int64_t)ct * FC_NCH * 64 + lane;
+  constexpr int D = 6;                                   // chunks in flight per wave
   f32x4 ra[D], rb[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const int cc = min(c0 + d, c1 - 1);
+    ra[d] = *(const f32x4*)(a + 8 * cc);
+    rb[d] = b[(int64_t)cc * 64];
+  }
   f32x16 acc = {};
+  for (int c = c0; c < c1; c += D) {
 #pragma unroll
-  for (int i = 0; i < NMAX + D; ++i) {
-    if (i >= D) {                                        // consume chunk i - D
-      const int j = i - D;
-      f32x4 av = ra[j % D];
-      if (j == NMAX - 1 && c0 + j >= c1) av = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int d = 0; d < D; ++d) {
+      if (c + d < c1) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], rb[j % D][q], acc, 0, 0, 0);
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[d][j], rb[d][j], acc, 0, 0, 0);
+        const int cn = c + d + D;                        // refill this slot with chunk cn
+        if (cn < c1) {
+          ra[d] = *(const f32x4*)(a + 8 * cn);
+          rb[d] = b[(int64_t)cn * 64];
+        }
+      }
     }
-    if (i < NMAX) {                                      // issue chunk i
-      const int cc = min(c0 + i, c1 - 1);
-      ra[i % D] = *(const f32x4*)(a + 8 * cc);
-      rb[i % D] = b[(int64_t)cc * 64];
-    }
-    // keep each step's loads where they are issued (hipcc otherwise sinks them to their MFMAs
-    // and waits vmcnt(0) on every chunk)
-    __builtin_amdgcn_sched_barrier(0);
   }
   // fold the waves (fixed order)
   if (wid > 0) red[wid - 1][lane] = acc;
@@ -890,34 +884,27 @@ __global__ void __launch_bounds__(64 * FC_WAVES) k_fc_fwd(const float* __restric
 #pragma unroll
   for (int w = 0; w < FC_WAVES - 1; ++w) acc += red[w][lane];
   if constexpr (SPLIT > 1) {
-    // publish this workgroup's partial: write-through (sc1) 8-byte stores, drained before the
-    // ticket, so no release fence is needed (cdna_hip_programming.md Guideline 16 R1).  Layout
-    // [register pair][lane]: one 512-B store per pair of accumulator registers.
-    typedef __attribute__((address_space(1))) uint64_t gu64;
-    typedef __attribute__((address_space(1))) uint32_t gu32;
-    gu64* mine = (gu64*)(slab + ((int64_t)blockIdx.y * gridDim.x + tile) * 1024) + lane;
+    // publish this workgroup's partial (lane-major: one 256-B store per accumulator register)
+    float* mine = slab + ((int64_t)blockIdx.y * gridDim.x + tile) * 1024 + lane;
 #pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      const uint64_t v = (uint64_t)__float_as_uint(acc[r]) | ((uint64_t)__float_as_uint(acc[r + 1]) << 32);
-      __hip_atomic_store(mine + 32 * r, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    for (int r = 0; r < 16; ++r) mine[64 * r] = acc[r];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t ticket = 0;
-    if (lane == 0) ticket = __hip_atomic_fetch_add((gu32*)(cnt + tile), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) ticket = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ticket = __shfl(ticket, 0, 64);
     if (ticket != SPLIT - 1) return;                     // not the last of this tile's workgroups
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store((gu32*)(cnt + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const float2* ps = (const float2*)(slab + (int64_t)tile * 1024) + lane;
+    if (lane == 0) cnt[tile] = 0u;                       // ready for the next launch
+    const float* ps = slab + (int64_t)tile * 1024 + lane;
 #pragma unroll
-    for (int sp = 0; sp < SPLIT; ++sp)
+    for (int r = 0; r < 16; ++r) acc[r] = ps[64 * r];
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const float2 v = ps[(int64_t)sp * gridDim.x * 512 + 32 * r];
-        acc[r] = sp ? acc[r] + v.x : v.x;
-        acc[r + 1] = sp ? acc[r + 1] + v.y : v.y;
-      }
+    for (int sp = 1; sp < SPLIT; ++sp)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += ps[(int64_t)sp * gridDim.x * 1024 + 64 * r];
   }
   const float bb = bias[n0 + i32];
 #pragma unroll
