@@ -57,8 +57,7 @@ extern "C" int a3c_workspace_bytes(const a3c_net_desc* net, int64_t B, int64_t* 
     return a3c_set_error(A3C_ERR_INVALID, "a3c_workspace_bytes", "bad argument");
   // forward: the bf16-split conv1 weights; backward: its plan (they never run at once)
   BwdPlan p = a3c_bwd_plan(L, B > 0 ? B : 1);
-  const int64_t fwd = (a3c_prep_bytes(B > 0 ? B : 1) + 3) / 4;
-  int64_t m = p.total > fwd ? p.total : fwd;
+  int64_t m = p.total > PREP_BYTES / 4 ? p.total : PREP_BYTES / 4;
   *bytes = m * (int64_t)sizeof(float) + 256;
   return 0;
 }

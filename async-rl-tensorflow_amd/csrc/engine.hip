@@ -20,7 +20,8 @@
 #include "gemm.h"
 
 void a3c_init_once();
-int a3c_fc_fwd_launch(const float* A, uint8_t* prep, const float* bias, float* C, int64_t M, hipStream_t s);
+int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s,
+                      const float* Wrows = nullptr);
 
 // Per-rollout buffers.  Sync mode has one slot whose params are the live parameters and whose
 // tau is the live frame counter.  Overlap mode (cfg.overlap = 1) has two: rollout k fills slot
@@ -241,7 +242,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     ALLOC(sl.act_l3, nE * FC * 4);
     ALLOC(sl.scr_l2, scrB * FLAT * 4);
     ALLOC(sl.scr_l3, scrB * FC * 4);
-    ALLOC(sl.prep, a3c_prep_bytes(E));
+    ALLOC(sl.prep, PREP_BYTES);
     if (L.lstm) {
       ALLOC(sl.lh, nE * LSTM_U * 4);
       ALLOC(sl.lc, nE * LSTM_U * 4);
@@ -257,7 +258,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     ALLOC(e->lws, a3c_lstm_ws_floats(e->n, E) * 4);
     ALLOC(e->ldh, nE * LSTM_U * 4);
   }
-  ALLOC(e->prep_t, a3c_prep_bytes(nE));
+  ALLOC(e->prep_t, PREP_BYTES);
   ALLOC(e->spans, 2 * (size_t)SPAN_RECS * SPAN_WGS * 2 * sizeof(unsigned long long));
   ALLOC(e->zt, scrB * zs * 4);
   ALLOC(e->eps, E * 4);
@@ -920,7 +921,8 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
       case A3C_KER_CONV12_FWD:
         return a3c_conv12_launch(L, e->params, sl.prep, ring_addr(e, 0, e->counters), E, sl.act_l1, sl.act_l2, s);
       case A3C_KER_FC_FWD:
-        return a3c_fc_fwd_launch(sl.act_l2, sl.prep, e->params + L.off[T_FCB], sl.act_l3, E, s);
+        return a3c_fc_fwd_launch(sl.act_l2, (const float*)(sl.prep + PREP_W1S_BYTES), e->params + L.off[T_FCB],
+                                 sl.act_l3, E, s, e->params + L.off[T_FCW]);
       case A3C_KER_ENV_STEP:
         return a3c_env_screen_launch(E, sl.frames, e->pool, e->ring, e->R, e->counters, 0, s);
       case A3C_KER_HEAD_SCREEN:

@@ -120,27 +120,15 @@ struct HeadSelect {
 };
 
 // forward of B states; returns 0 or error
-// prep: the forward's prepared weights of `params` (a3c_prep_fwd_launch, a3c_prep_bytes(M)):
-// conv1 split into bf16 terms (W1S_ELEMS u16), the fc weights in MFMA fragment order, the
-// conv2 terms, then the fc split-K scratch
+// prep: the forward's prepared weights of `params` (a3c_prep_fwd_launch, PREP_BYTES):
+// conv1 split into bf16 terms (W1S_ELEMS u16) then the fc weights in MFMA fragment order
 #define W1S_ELEMS (C1_K * 3 * 64 * 8)   // 12288 bf16
 #define PREP_W1S_BYTES (W1S_ELEMS * 2)  // 24576
-#define FC_NCH (FLAT / 8)               // 324 K-chunks of 8 (fc forward, 32x32x2 f32 MFMA)
+#define FC_CH (FLAT / 16)               // 162 K-chunks of 16
+#define FC_CH32 (FLAT / 32)             // 81 K-chunks of 32
 #define PREP_W2F_OFF (PREP_W1S_BYTES + FLAT * FC * 4)
 #define W2F_ELEMS (2 * 8 * 64 * 8)      // conv2 weights (16x16x32), as three bf16 terms each
 #define PREP_BYTES (PREP_W2F_OFF + W2F_ELEMS * 3 * 2)
-// fc forward split-K scratch after the prepared weights: per-tile arrival counters (zeroed by
-// k_prep_fwd, reset by each tile's last workgroup) then the partial slabs [FC_SPLIT][tiles][1024]
-#define FC_SPLIT 4                      // workgroups per 32x32 output tile (K split)
-#define FC_ROWS_MAX 16384               // rows per launch (longer batches: several launches)
-#define FC_CNT_MAX ((FC_ROWS_MAX / 32) * (FC / 32))   // 4096 tiles
-#define PREP_FC_CNT_OFF (((PREP_BYTES) + 255) / 256 * 256)
-#define PREP_FC_SLAB_OFF (PREP_FC_CNT_OFF + FC_CNT_MAX * 4)
-// bytes of a prep buffer whose forward runs batches of up to M rows
-inline int64_t a3c_prep_bytes(int64_t M) {
-  const int64_t rows = ((M < FC_ROWS_MAX ? M : FC_ROWS_MAX) + 31) / 32 * 32;
-  return PREP_FC_SLAB_OFF + (int64_t)FC_SPLIT * rows * FC * 4;
-}
 struct LstmStep;
 // the next state's conv1 + conv2, fused into rollout step t's head + screen kernel
 // (k_head_screen_conv12): s_{t+1} addressing, conv weights (prep'd W1 terms) and outputs

@@ -38,12 +38,11 @@
 // holds B[k = 8g + j][i] = W1[kh][kw = j][cin = g][cout = i] (ops.py:21 layout).
 // ---------------------------------------------------------------------------------------
 // Forward weight preparation, once per parameter version (rollout start): the conv1 bf16
-// terms above, the fc weights in the fc kernel's fragment order, Wk[ct][c][lane][j] =
-// W[8c + 4(lane>>5) + j][32ct + (lane&31)] (a lane's B operands of 4 v_mfma_f32_32x32x2_f32 are
-// one 16-byte load), and the conv2 weights as three bf16 terms in fragment order (w2f, at
-// PREP_W2F_OFF): w2f[nt][ks][term][lane][j], lane = (j4 = lane>>4, i16 = lane&15), holds B[k][n]
-// of K-step ks (taps kk = 2 ks + (j4>>1), cin = 8 (j4&1) + j) for cout n = 16 nt + i16.  The fc
-// split-K arrival counters are zeroed here as well.
+// terms above and the fc weights in MFMA fragment order, Wp[ct][c][lane][c4] =
+// W[16c + 4(lane>>4) + c4][16ct + (lane&15)], so a lane's B operands for 4 MFMAs are one 16-byte load.
+// conv2 weights as three bf16 terms in fragment order (w2f, at PREP_W2F_OFF):
+// w2f[nt][ks][term][lane][j], lane = (j4 = lane>>4, i16 = lane&15), holds B[k][n] of K-step ks
+// (taps kk = 2 ks + (j4>>1), cin = 8 (j4&1) + j) for cout n = 16 nt + i16.
 __device__ inline void split3_bits(float w, uint32_t& h, uint32_t& m, uint32_t& l) {
 #pragma clang fp contract(off)
   h = bf16_rn_bits(w);
@@ -53,36 +52,29 @@ __device__ inline void split3_bits(float w, uint32_t& h, uint32_t& m, uint32_t& 
   l = bf16_rn_bits(r2);
 }
 
-#define PREP_T_W1 (C1_K * 64 * 8)                 // conv1 split threads
-#define PREP_T_FC ((FC / 32) * FC_NCH * 64)       // fc pack threads (one f32x4 each)
-#define PREP_T_CNT (FC_CNT_MAX / 4)               // counter-zeroing threads (one uint4 each)
 __global__ void __launch_bounds__(256) k_prep_fwd(const float* __restrict__ W1, const float* __restrict__ Wfc,
                                                   const float* __restrict__ W2, uint8_t* __restrict__ prep) {
 #pragma clang fp contract(off)
   const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t < PREP_T_W1) {                                       // (kh, lane, j): conv1 split
+  if (t < C1_K * 64 * 8) {                                   // (kh, lane, j): conv1 split
     uint16_t* w1s = (uint16_t*)prep;
     const int kh = t >> 9, lane = (t >> 3) & 63, j = t & 7;
     const int g = lane >> 4, i = lane & 15;
-    uint32_t h, m, l;
-    split3_bits(W1[((kh * C1_K + j) * HIST + g) * C1_N + i], h, m, l);
+    const float w = W1[((kh * C1_K + j) * HIST + g) * C1_N + i];
+    const uint32_t h = bf16_rn_bits(w);
+    const float r1 = w - __uint_as_float(h << 16);
+    const uint32_t m = bf16_rn_bits(r1);
+    const float r2 = r1 - __uint_as_float(m << 16);
+    const uint32_t l = bf16_rn_bits(r2);
     w1s[((kh * 3 + 0) * 64 + lane) * 8 + j] = (uint16_t)h;
     w1s[((kh * 3 + 1) * 64 + lane) * 8 + j] = (uint16_t)m;
     w1s[((kh * 3 + 2) * 64 + lane) * 8 + j] = (uint16_t)l;
     return;
   }
-  const int q = t - PREP_T_W1;
-  if (q < PREP_T_FC) {                                       // (ct, c, lane): one f32x4 of the fc pack
-    const int lane = q & 63, c = (q >> 6) % FC_NCH, ct = (q >> 6) / FC_NCH;
-    const int k0 = 8 * c + 4 * (lane >> 5), n = 32 * ct + (lane & 31);
-    f32x4 v;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = Wfc[(int64_t)(k0 + j) * FC + n];
-    ((f32x4*)(prep + PREP_W1S_BYTES))[q] = v;
-    return;
-  }
-  const int r = q - PREP_T_FC;
-  if (r < W2F_ELEMS) {                                       // (nt, ks, lane, j): conv2 split
+  const int q = t - C1_K * 64 * 8;                          // (ct, c, lane): one f32x4 of the fc pack
+  if (q >= (FC / 16) * FC_CH * 64) {
+    const int r = q - (FC / 16) * FC_CH * 64;               // (nt, ks, lane, j): conv2 split
+    if (r >= W2F_ELEMS) return;
     const int nt = r >> 12, ks = (r >> 9) & 7, lane = (r >> 3) & 63, j = r & 7;
     const int j4 = lane >> 4, kk = 2 * ks + (j4 >> 1), ci = 8 * (j4 & 1) + j;
     uint32_t h, m, l;
@@ -93,12 +85,25 @@ __global__ void __launch_bounds__(256) k_prep_fwd(const float* __restrict__ W1, 
     w2f[1024] = (uint16_t)l;
     return;
   }
-  const int z = r - W2F_ELEMS;
-  if (z < PREP_T_CNT) ((uint4*)(prep + PREP_FC_CNT_OFF))[z] = make_uint4(0u, 0u, 0u, 0u);
+#ifndef FC_K32
+  const int lane = q & 63, c = (q >> 6) % FC_CH, ct = (q >> 6) / FC_CH;
+  const int j4 = lane >> 4, n = 16 * ct + (lane & 15);
+  f32x4 v;
+#pragma unroll
+  for (int c4 = 0; c4 < 4; ++c4) v[c4] = Wfc[(int64_t)(16 * c + 4 * j4 + c4) * FC + n];
+#else
+  // 32-deep chunks: Wp[ct][c][lane][8] = W[32c + 8(lane>>4) + 0..7][16ct + (lane&15)], q = one f32x4
+  const int half = q & 1, lane = (q >> 1) & 63, c = (q >> 7) % FC_CH32, ct = (q >> 7) / FC_CH32;
+  const int j4 = lane >> 4, n = 16 * ct + (lane & 15);
+  f32x4 v;
+#pragma unroll
+  for (int c4 = 0; c4 < 4; ++c4) v[c4] = Wfc[(int64_t)(32 * c + 8 * j4 + 4 * half + c4) * FC + n];
+#endif
+  ((f32x4*)(prep + PREP_W1S_BYTES))[q] = v;
 }
 
 int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s) {
-  const int total = PREP_T_W1 + PREP_T_FC + W2F_ELEMS + PREP_T_CNT;
+  const int total = C1_K * 64 * 8 + (FC / 16) * FC_CH * 64 + W2F_ELEMS;
   hipLaunchKernelGGL(k_prep_fwd, dim3((total + 255) / 256), dim3(256), 0, s, P + L.off[T_L1W], P + L.off[T_FCW],
                      P + L.off[T_L2W], prep);
   A3C_CHECK(hipGetLastError());
@@ -700,7 +705,8 @@ __global__ void __launch_bounds__(256) k_select(const float* __restrict__ z, int
   if (lane == 0) sel.actions[b] = a;
 }
 
-int a3c_fc_fwd_launch(const float* A, uint8_t* prep, const float* bias, float* C, int64_t M, hipStream_t s);
+int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s,
+                      const float* Wrows = nullptr);
 
 // skip_conv12: conv1 + conv2 of these states already ran (fused into the previous step's
 // k_head_screen_conv12); next: fuse the next states' conv1 + conv2 into this step's head + screen
@@ -717,7 +723,8 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
     int rc0 = a3c_conv12_launch(L, P, prep, sa, B, act_l1, act_l2, s);
     if (rc0) return rc0;
   }
-  int rc = a3c_fc_fwd_launch(act_l2, const_cast<uint8_t*>(prep), P + L.off[T_FCB], act_l3, B, s);
+  int rc = a3c_fc_fwd_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), P + L.off[T_FCB], act_l3, B, s,
+                             P + L.off[T_FCW]);
   if (rc) return rc;
   const float* head_in = act_l3;
   if (ls) {   // C5: LSTM cell on the fc output, heads on its h
@@ -826,106 +833,211 @@ void a3c_conv12_set_smem() {
 }
 
 // ---------------------------------------------------------------------------------------
-// fc layer (agent.py:251 / network.py:51-52): l3 = relu(l2 @ W + b) for a batch of M states,
-// N = 256, K = 2592, on v_mfma_f32_32x32x2_f32 (exact fp32 products, fp32 accumulation).
-// One wave per 32x32 output tile and K-range: per 8-deep K chunk a lane loads one float4 of its
-// l2 row and one float4 of the fragment-packed weights (k_prep_fwd) and issues 4 MFMAs -- half
-// the operand bytes per FLOP of the 16x16x4 form, which matters here: the operands come from
-// L2 / MALL at ~30 B/clk/CU, not from LDS.  A workgroup is the FC_WAVES waves of one tile on
-// consecutive K-ranges, folded in LDS; FC_SPLIT workgroups split K further, and the last one to
-// finish a tile folds the partial slabs (in-launch split-K: agent-scope release, ticket, acquire;
-// the fold runs in a fixed order, so the result does not depend on which workgroup is last).
-// Grid: x = tile (row tile * 8 + column tile), y = K split.
+// fc layer of the rollout (agent.py:251 / network.py:51-52): l3 = relu(l2 @ W + b) for a
+// skinny batch (M = E states, N = 256, K = 2592).  One workgroup per 16x16 output tile; the
+// 4 waves split the 162 K-chunks of 16 and meet in LDS.  Per chunk a lane loads one 16-byte A
+// fragment (4 consecutive k of its row) and one 16-byte B fragment from the fragment-packed
+// weights (k_prep_fwd), feeding 4 v_mfma_f32_16x16x4_f32; a ring of D chunks keeps 2D loads in
+// flight per wave.  blockIdx.x (column tile) is the fast grid index, so the 8 XCDs each stream
+// 2 column tiles of W (L2-resident) and the l2 rows.
 // ---------------------------------------------------------------------------------------
-#define FC_WAVES 4
-template <int SPLIT>
-__global__ void __launch_bounds__(64 * FC_WAVES) k_fc_fwd(const float* __restrict__ A, const float* __restrict__ Wk,
-                                                          const float* __restrict__ bias, float* __restrict__ C,
-                                                          int M, float* __restrict__ slab,
-                                                          uint32_t* __restrict__ cnt) {
-  __shared__ f32x16 red[FC_WAVES - 1][64];
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_fc_fwd(const float* __restrict__ A, const float* __restrict__ Wp,
+                                                    const float* __restrict__ bias, float* __restrict__ C, int M,
+                                                    int xcd_rows) {
+  __shared__ f32x4 red[NW - 1][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int i32 = lane & 31, h = lane >> 5;
-  const int tile = blockIdx.x, mt = tile >> 3, ct = tile & 7;
-  const int m0 = 32 * mt, n0 = 32 * ct;
+  const int i16 = lane & 15, j4 = lane >> 4;
+  // xcd_rows: 1-D grid, workgroup id -> XCD id % 8 gets a contiguous band of row tiles (all 16
+  // column tiles each), so an XCD reads 1/8 of A and all of W (which is the same every step)
+  int ct = blockIdx.x, mt = blockIdx.y;
+  if (xcd_rows) {
+    const int ntiles = gridDim.x, id = blockIdx.x;
+    const int t = (id & 7) * (ntiles >> 3) + (id >> 3);
+    ct = t % (FC / 16);
+    mt = t / (FC / 16);
+  }
+  const int m0 = mt * 16, n0 = ct * 16;
+  const int m = min(m0 + i16, M - 1);
   WG_T0();
-  // this wave's chunks [c0, c1) of the 324: the K range split as evenly as possible
-  const int part = blockIdx.y * FC_WAVES + wid;
-  const int c0 = (part * FC_NCH) / (SPLIT * FC_WAVES), c1 = ((part + 1) * FC_NCH) / (SPLIT * FC_WAVES);
-  const float* a = A + (int64_t)min(m0 + i32, M - 1) * FLAT + 4 * h;
-  const f32x4* b = (const f32x4*)Wk + (int64_t)ct * FC_NCH * 64 + lane;
-  constexpr int D = 6;                                   // chunks in flight per wave
+  // the waves' partial tiles meet in LDS (fixed order), bias + relu, store
+  auto fc_epilogue = [&](f32x4 acc) {
+    if (wid > 0) red[wid - 1][lane] = acc;
+    __syncthreads();
+    if (wid == 0) {
+#pragma unroll
+      for (int w = 0; w < NW - 1; ++w) acc += red[w][lane];
+      const int n = n0 + i16;
+      const float bb = bias[n];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + 4 * j4 + r;
+        if (row < M) st_act(C + (int64_t)row * FC + n, fmaxf(acc[r] + bb, 0.f));
+      }
+    }
+    WG_T1(C + (int64_t)m0 * FC + n0);   // debug: the tile's first 4 outputs
+  };
+#ifdef FC_K32   // A/B: faster alone (8.7 vs 9.2 us), slower overlapped (3.82M vs 4.00M)
+  // 32-deep chunks [c0, c1) of this wave (81 split as evenly as possible): per chunk a lane loads
+  // 8 consecutive k of its row (32 B: the row's 128-B line is read whole by the 4 lane groups)
+  // and its 8 packed weights, for 8 MFMAs (k permuted within the chunk identically for A and B)
+  {
+    const int c0 = (wid * FC_CH32) / NW, c1 = ((wid + 1) * FC_CH32) / NW;
+    constexpr int D = 4;
+    const float* a = A + (int64_t)m * FLAT + 8 * j4;
+    const f32x4* b = (const f32x4*)Wp + (int64_t)ct * FC_CH32 * 128 + 2 * lane;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    f32x4 ra[D][2], rb[D][2];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int cc = min(c0 + d, c1 - 1);
+      ra[d][0] = *(const f32x4*)(a + 32 * cc);
+      ra[d][1] = *(const f32x4*)(a + 32 * cc + 4);
+      rb[d][0] = b[(int64_t)cc * 128];
+      rb[d][1] = b[(int64_t)cc * 128 + 1];
+    }
+    for (int c = c0; c < c1; c += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        if (c + d < c1) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][h][0], rb[d][h][0], acc, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][h][1], rb[d][h][1], acc1, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][h][2], rb[d][h][2], acc, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][h][3], rb[d][h][3], acc1, 0, 0, 0);
+          }
+          const int cn = c + d + D;
+          if (cn < c1) {
+            ra[d][0] = *(const f32x4*)(a + 32 * cn);
+            ra[d][1] = *(const f32x4*)(a + 32 * cn + 4);
+            rb[d][0] = b[(int64_t)cn * 128];
+            rb[d][1] = b[(int64_t)cn * 128 + 1];
+          }
+        }
+      }
+    }
+    fc_epilogue(acc + acc1);
+    return;
+  }
+#endif
+  // chunks [c0, c1) of this wave: the 162 chunks split as evenly as possible
+  const int c0 = (wid * FC_CH) / NW, c1 = ((wid + 1) * FC_CH) / NW;
+#ifndef FC_D
+#define FC_D 8
+#endif
+  constexpr int D = FC_D;
+  const float* a = A + (int64_t)m * FLAT + 4 * j4;
+  const f32x4* b = (const f32x4*)Wp + (int64_t)ct * FC_CH * 64 + lane;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   f32x4 ra[D], rb[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    const int cc = min(c0 + d, c1 - 1);
-    ra[d] = *(const f32x4*)(a + 8 * cc);
-    rb[d] = b[(int64_t)cc * 64];
+    ra[d] = *(const f32x4*)(a + 16 * (c0 + d));
+    rb[d] = b[(int64_t)(c0 + d) * 64];
   }
-  f32x16 acc = {};
   for (int c = c0; c < c1; c += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       if (c + d < c1) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[d][j], rb[d][j], acc, 0, 0, 0);
-        const int cn = c + d + D;                        // refill this slot with chunk cn
+        // two independent accumulation chains (MFMA dependent latency > issue interval)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][0], rb[d][0], acc, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][1], rb[d][1], acc1, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][2], rb[d][2], acc, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][3], rb[d][3], acc1, 0, 0, 0);
+        const int cn = c + d + D;                 // refill this slot with chunk cn
         if (cn < c1) {
-          ra[d] = *(const f32x4*)(a + 8 * cn);
+          ra[d] = *(const f32x4*)(a + 16 * cn);
           rb[d] = b[(int64_t)cn * 64];
         }
       }
     }
   }
-  // fold the waves (fixed order)
-  if (wid > 0) red[wid - 1][lane] = acc;
-  __syncthreads();
-  if (wid != 0) return;
-#pragma unroll
-  for (int w = 0; w < FC_WAVES - 1; ++w) acc += red[w][lane];
-  if constexpr (SPLIT > 1) {
-    // publish this workgroup's partial (lane-major: one 256-B store per accumulator register)
-    float* mine = slab + ((int64_t)blockIdx.y * gridDim.x + tile) * 1024 + lane;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) mine[64 * r] = acc[r];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t ticket = 0;
-    if (lane == 0) ticket = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ticket = __shfl(ticket, 0, 64);
-    if (ticket != SPLIT - 1) return;                     // not the last of this tile's workgroups
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) cnt[tile] = 0u;                       // ready for the next launch
-    const float* ps = slab + (int64_t)tile * 1024 + lane;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = ps[64 * r];
-#pragma unroll
-    for (int sp = 1; sp < SPLIT; ++sp)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] += ps[(int64_t)sp * gridDim.x * 1024 + 64 * r];
-  }
-  const float bb = bias[n0 + i32];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    if (row < M) st_act(C + (int64_t)row * FC + n0 + i32, fmaxf(acc[r] + bb, 0.f));
-  }
-  WG_T1(C + (int64_t)m0 * FC + n0);   // debug: the tile's first outputs
+  fc_epilogue(acc + acc1);
 }
 
-// prep: the prepared weights + split-K scratch of a3c_prep_bytes(>= min(M, FC_ROWS_MAX))
-int a3c_fc_fwd_launch(const float* A, uint8_t* prep, const float* bias, float* C, int64_t M, hipStream_t s) {
-  const float* Wk = (const float*)(prep + PREP_W1S_BYTES);
-  uint32_t* cnt = (uint32_t*)(prep + PREP_FC_CNT_OFF);
-  float* slab = (float*)(prep + PREP_FC_SLAB_OFF);
-  for (int64_t r0 = 0; r0 < M; r0 += FC_ROWS_MAX) {
-    const int rows = (int)(M - r0 < FC_ROWS_MAX ? M - r0 : FC_ROWS_MAX);
-    const dim3 grid((unsigned)(((rows + 31) / 32) * (FC / 32)), FC_SPLIT);
-    hipLaunchKernelGGL(k_fc_fwd<FC_SPLIT>, grid, dim3(64 * FC_WAVES), 0, s, A + r0 * FLAT, Wk, bias, C + r0 * FC,
-                       rows, slab, cnt);
-    A3C_CHECK(hipGetLastError());
+// row-major-weight variant (4 scalar B loads per chunk), kept for A/B measurement
+__global__ void __launch_bounds__(256) k_fc_fwd_rows(const float* __restrict__ A, const float* __restrict__ W,
+                                                const float* __restrict__ bias, float* __restrict__ C, int M) {
+  __shared__ f32x4 red[3][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i16 = lane & 15, j4 = lane >> 4;
+  const int m0 = blockIdx.y * 16, n0 = blockIdx.x * 16;
+  const int m = min(m0 + i16, M - 1);
+  constexpr int KW = FLAT / 4;                    // 648 per wave
+  constexpr int NCH = KW / 16;                    // 40 chunks of 16 (+ 8 left)
+  constexpr int D = 8;                            // chunks in flight per wave (register ring)
+  const float* a = A + (int64_t)m * FLAT + wid * KW + 4 * j4;
+  const float* b = W + (int64_t)(wid * KW + 4 * j4) * FC + n0 + i16;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 ra[D];
+  float rb[D][4];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    ra[d] = *(const f32x4*)(a + 16 * d);
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) rb[d][c4] = b[(int64_t)(16 * d + c4) * FC];
   }
+  for (int c0 = 0; c0 < NCH; c0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[d][c4], rb[d][c4], acc, 0, 0, 0);
+      const int cn = c0 + d + D;                  // refill this slot with chunk cn
+      if (cn < NCH) {
+        ra[d] = *(const f32x4*)(a + 16 * cn);
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) rb[d][c4] = b[(int64_t)(16 * cn + c4) * FC];
+      }
+    }
+  }
+  // tail: 8 = KW - 16*NCH values per wave -> lane groups j4 < 2 carry them, others add zeros
+  {
+    const bool live = j4 < 2;
+    const float* at = A + (int64_t)m * FLAT + wid * KW + 16 * NCH + 4 * (j4 & 1);
+    const float* bt = W + (int64_t)(wid * KW + 16 * NCH + 4 * (j4 & 1)) * FC + n0 + i16;
+    f32x4 x = *(const f32x4*)at;
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(live ? x[c4] : 0.f, live ? bt[c4 * FC] : 0.f, acc, 0, 0, 0);
+  }
+  if (wid > 0) red[wid - 1][lane] = acc;
+  __syncthreads();
+  if (wid == 0) {
+    acc += red[0][lane];
+    acc += red[1][lane];
+    acc += red[2][lane];
+    const int n = n0 + i16;
+    const float bb = bias[n];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + 4 * j4 + r;
+      if (row < M) C[(int64_t)row * FC + n] = fmaxf(acc[r] + bb, 0.f);
+    }
+  }
+}
+
+int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s,
+                      const float* Wrows) {
+  if (M <= 0) return 0;
+  static const int env_nw = getenv("A3C_FC_WAVES") ? atoi(getenv("A3C_FC_WAVES")) : -1;
+  const int nw = env_nw >= 0 ? env_nw : (a3c_shared_gpu() ? 4 : 8);
+  if (nw == 0 && Wrows)
+    hipLaunchKernelGGL(k_fc_fwd_rows, dim3(FC / 16, (unsigned)((M + 15) / 16)), dim3(256), 0, s, A, Wrows, bias, C,
+                       (int)M);
+  else {
+    static const int env_x = getenv("A3C_FC_XCD") ? atoi(getenv("A3C_FC_XCD")) : 0;
+    const int mt = (int)((M + 15) / 16), ntiles = mt * (FC / 16);
+    const int xr = env_x && ntiles % 8 == 0;
+    const dim3 grid = xr ? dim3((unsigned)ntiles) : dim3(FC / 16, (unsigned)mt);
+    if (nw == 4)
+      hipLaunchKernelGGL(k_fc_fwd<4>, grid, dim3(256), 0, s, A, W, bias, C, (int)M, xr);
+    else if (nw == 16)
+      hipLaunchKernelGGL(k_fc_fwd<16>, grid, dim3(1024), 0, s, A, W, bias, C, (int)M, xr);
+    else
+      hipLaunchKernelGGL(k_fc_fwd<8>, grid, dim3(512), 0, s, A, W, bias, C, (int)M, xr);
+  }
+  A3C_CHECK(hipGetLastError());
   return 0;
 }
