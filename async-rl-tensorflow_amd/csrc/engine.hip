@@ -399,7 +399,10 @@ static const Slot& prev_slot(const a3c_engine* e, const Slot& sl) {
 // rollout start: forward weights of the rollout's parameters (+ q: the epsilon schedule)
 static int enqueue_rollout_begin(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
-  int rc = a3c_prep_fwd_launch(e->L, sl.P, sl.prep, s);   // params are fixed for the rollout
+  // params are fixed for the rollout; overlap: the prep kernel also snapshots tau for the slot's
+  // backward (sync: the slot's tau is the live counter)
+  int rc = a3c_prep_fwd_launch(e->L, sl.P, sl.prep, s, e->overlap ? e->counters : nullptr,
+                               e->overlap ? sl.tau : nullptr);
   if (rc) return rc;
   if (e->L.lstm) {
     rc = a3c_lstm_transpose_launch(sl.P + e->L.off[T_LW], sl.lwt, s);
@@ -488,6 +491,10 @@ static int enqueue_rollout_end(a3c_engine* e, const Slot& sl, hipStream_t s) {
     HeadSelect none = {};
     none.mode = -1;
     none.E = E;
+    if (e->overlap) {          // the rollout advances tau: in its last kernel, the bootstrap head
+      none.adv_ptr = e->counters;
+      none.adv_n = n;
+    }
     LstmStep ls = {};
     if (L.lstm) {
       ls.wt = sl.lwt;
@@ -497,7 +504,7 @@ static int enqueue_rollout_end(a3c_engine* e, const Slot& sl, hipStream_t s) {
     int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, n, e->counters), E, nullptr, sl.scr_l2,
                                 sl.scr_l3, sl.z + e->nE * L.zs, none, s, L.lstm ? &ls : nullptr,
                                 conv_fused(e));   // s_n's convs ran in the last step's kernel
-    if (rc) return rc;
+    return rc;
   }
   if (e->overlap) {
     hipLaunchKernelGGL(k_advance_tau, dim3(1), dim3(1), 0, s, e->counters, n);
@@ -701,8 +708,7 @@ static int rollout_grad(a3c_engine* e, hipStream_t s, bool fused) {
   const Slot& sl = e->slot[p];
   A3C_CHECK(hipEventRecord(e->ev_start, s));
   A3C_CHECK(hipStreamWaitEvent(e->rs, e->ev_start, 0));
-  A3C_CHECK(hipMemcpyAsync(sl.tau, e->counters, 8, hipMemcpyDeviceToDevice, e->rs));
-  int rc = run_graph(e, 1 + p, 1, p, e->rs);
+  int rc = run_graph(e, 1 + p, 1, p, e->rs);   // (its prep kernel snapshots tau into sl.tau)
   if (rc) return rc;
   A3C_CHECK(hipEventRecord(e->ev_roll[p], e->rs));
   e->grad_ready = false;

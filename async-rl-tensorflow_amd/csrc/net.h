@@ -117,6 +117,10 @@ struct HeadSelect {
   // timed launch streams a different set of frames from HBM, as the live rollout does; 0 in
   // every product launch
   uint32_t frame_salt;
+  // k_head_fwd only (the overlap rollout's bootstrap head, its last kernel): *adv_ptr += adv_n
+  // once the launch's heads are written (the rollout's tau advance, no kernel of its own)
+  int64_t* adv_ptr;
+  int64_t adv_n;
 };
 
 // forward of B states; returns 0 or error
@@ -146,7 +150,9 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
                        int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
                        hipStream_t s, const LstmStep* ls = nullptr, bool skip_conv12 = false,
                        const Conv12Next* next = nullptr);
-int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s);
+// tau_src / tau_dst (nullable): *tau_dst = *tau_src as well (the overlap rollout's tau snapshot)
+int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s,
+                        const int64_t* tau_src = nullptr, int64_t* tau_dst = nullptr);
 // true while enqueuing work that runs concurrently with another stream (engine overlap mode)
 bool a3c_shared_gpu();
 void a3c_set_shared_gpu(bool v);

@@ -53,9 +53,11 @@ __device__ inline void split3_bits(float w, uint32_t& h, uint32_t& m, uint32_t& 
 }
 
 __global__ void __launch_bounds__(256) k_prep_fwd(const float* __restrict__ W1, const float* __restrict__ Wfc,
-                                                  const float* __restrict__ W2, uint8_t* __restrict__ prep) {
+                                                  const float* __restrict__ W2, uint8_t* __restrict__ prep,
+                                                  const int64_t* __restrict__ tau_src, int64_t* __restrict__ tau_dst) {
 #pragma clang fp contract(off)
   const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t == 0 && tau_dst) *tau_dst = *tau_src;
   if (t < C1_K * 64 * 8) {                                   // (kh, lane, j): conv1 split
     uint16_t* w1s = (uint16_t*)prep;
     const int kh = t >> 9, lane = (t >> 3) & 63, j = t & 7;
@@ -102,10 +104,11 @@ __global__ void __launch_bounds__(256) k_prep_fwd(const float* __restrict__ W1, 
   ((f32x4*)(prep + PREP_W1S_BYTES))[q] = v;
 }
 
-int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s) {
+int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s, const int64_t* tau_src,
+                        int64_t* tau_dst) {
   const int total = C1_K * 64 * 8 + (FC / 16) * FC_CH * 64 + W2F_ELEMS;
   hipLaunchKernelGGL(k_prep_fwd, dim3((total + 255) / 256), dim3(256), 0, s, P + L.off[T_L1W], P + L.off[T_FCW],
-                     P + L.off[T_L2W], prep);
+                     P + L.off[T_L2W], prep, tau_src, tau_src ? tau_dst : nullptr);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
@@ -535,6 +538,7 @@ __global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, 
   const float myz = head_row(h3, b, Wp, bp, Wv, bv, A, lane);
   if (lane < zs) z[b * zs + lane] = myz;   // padding columns are 0
   if (sel.mode >= 0) (void)head_act(myz, lane, A, sel, b);
+  if (sel.adv_ptr && blockIdx.x == 0 && threadIdx.x == 0) *sel.adv_ptr += sel.adv_n;   // (reads no tau)
 }
 
 // engine rollout step tail, one workgroup per env: head + action draw (wave 0) while wave 1
