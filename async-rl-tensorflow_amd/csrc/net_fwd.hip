@@ -34,8 +34,12 @@
 // matrix cores (16x16x32, 16x the fp32 MFMA rate) as x * (w_hi + w_mid + w_lo): the three
 // round-to-nearest bf16 terms carry w to ~2^-24 relative and every product is exact in the
 // fp32 accumulator -- fp32 accuracy for 3 MFMAs instead of 8 fp32 ones per 32-deep K step.
-// Fragment-ordered buffer w1s[kh][term][lane][j] (bf16): lane l = (cin g = l>>4, cout i = l&15)
-// holds B[k = 8g + j][i] = W1[kh][kw = j][cin = g][cout = i] (ops.py:21 layout).
+// The K = 256 reduction runs cin-major, so that the three older planes of a state can be
+// reduced before its newest plane exists (the fused rollout kernel hides that part under the
+// new frame's HBM load): K-step (cin c, half h2) covers kh = 4 h2 + 0..3, kw = 0..7.
+// Fragment-ordered buffer w1s[f][lane][j] (bf16), f = (2 c + h2) * 3 + term: lane l = (j4 = l>>4,
+// cout i = l&15) holds B[k = 8 j4 + j][i] = W1[kh = 4 h2 + j4][kw = j][cin = c][cout = i]
+// (ops.py:21 layout).
 // ---------------------------------------------------------------------------------------
 // Forward weight preparation, once per parameter version (rollout start): the conv1 bf16
 // terms above and the fc weights in MFMA fragment order, Wp[ct][c][lane][c4] =
@@ -60,17 +64,14 @@ __global__ void __launch_bounds__(256) k_prep_fwd(const float* __restrict__ W1, 
   if (t == 0 && tau_dst) *tau_dst = *tau_src;
   if (t < C1_K * 64 * 8) {                                   // (kh, lane, j): conv1 split
     uint16_t* w1s = (uint16_t*)prep;
-    const int kh = t >> 9, lane = (t >> 3) & 63, j = t & 7;
-    const int g = lane >> 4, i = lane & 15;
-    const float w = W1[((kh * C1_K + j) * HIST + g) * C1_N + i];
-    const uint32_t h = bf16_rn_bits(w);
-    const float r1 = w - __uint_as_float(h << 16);
-    const uint32_t m = bf16_rn_bits(r1);
-    const float r2 = r1 - __uint_as_float(m << 16);
-    const uint32_t l = bf16_rn_bits(r2);
-    w1s[((kh * 3 + 0) * 64 + lane) * 8 + j] = (uint16_t)h;
-    w1s[((kh * 3 + 1) * 64 + lane) * 8 + j] = (uint16_t)m;
-    w1s[((kh * 3 + 2) * 64 + lane) * 8 + j] = (uint16_t)l;
+    const int ks = t >> 9, lane = (t >> 3) & 63, j = t & 7;     // ks = 2 cin + h2
+    const int c = ks >> 1, kh = 4 * (ks & 1) + (lane >> 4), i = lane & 15;
+    const float w = W1[((kh * C1_K + j) * HIST + c) * C1_N + i];
+    uint32_t h, m, l;
+    split3_bits(w, h, m, l);
+    w1s[((ks * 3 + 0) * 64 + lane) * 8 + j] = (uint16_t)h;
+    w1s[((ks * 3 + 1) * 64 + lane) * 8 + j] = (uint16_t)m;
+    w1s[((ks * 3 + 2) * 64 + lane) * 8 + j] = (uint16_t)l;
     return;
   }
   const int q = t - C1_K * 64 * 8;                          // (ct, c, lane): one f32x4 of the fc pack
@@ -132,55 +133,104 @@ __device__ inline bf16x8 u8x8_to_bf16(uint32_t d0, uint32_t d1) {
   return __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
 }
 
-// conv1 (bf16x3 MFMA) + relu -> l1s (and act_l1), conv2 (fp32 MFMA) + relu -> act_l2 for state b,
-// whose HIST planes are staged in LDS (x8 u8 when U8, else xb bf16).  EW: w2r already loaded.
-template <bool SAVE_L1, bool EW, bool U8>
-__device__ inline void conv12_core(const uint8_t* x8, const uint16_t* xb, float* l1s, int64_t b,
-                                   const uint16_t* __restrict__ w1s, const float* __restrict__ b1,
-                                   const float* __restrict__ W2, float* __restrict__ act_l1,
-                                   float* __restrict__ act_l2, float (&w2r)[64], float bias2) {
+// workgroup barrier that retires LDS operations only (vector-memory loads stay in flight)
+__device__ inline void lds_only_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// conv1 of the state whose HIST planes are staged in LDS (x8 u8 when U8, else xb bf16) on the
+// bf16 matrix cores: wave w owns the M-tiles m = w + 8 i (25 tiles of 16 positions), acc[i]
+// accumulates the K-steps of input planes [CB, CE) in the fixed order (cin, h2, term), so a
+// reduction split over two calls equals one call over all planes bit for bit.  wfrag(f) returns
+// the lane's fragment f = (2 cin + h2) * 3 + term of the bf16-split weights (w1s layout).
+#define C1_TILES 4
+__device__ inline int conv1_ntiles(int wid) { return wid == 0 ? 4 : 3; }   // 25 = 4 + 7 * 3
+template <bool U8, int CB, int CE, bool PIPE = true, typename WF>
+__device__ inline void conv1_accum(const uint8_t* x8, const uint16_t* xb, f32x4 (&acc)[C1_TILES], WF wfrag) {
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i16 = lane & 15, j4 = lane >> 4;
+  const int nt = conv1_ntiles(wid);
+  int off[C1_TILES];
+#pragma unroll
+  for (int i = 0; i < C1_TILES; ++i) {
+    const int p = min(16 * (wid + 8 * i) + i16, C1_P - 1);
+    const int oy = p / C1_O, ox = p - oy * C1_O;
+    off[i] = (C1_S * oy + j4) * IMG + C1_S * ox;       // row 4 oy + 4 h2 + j4, columns 4 ox + 0..7
+  }
+  // one K-step's operands (3 weight fragments, the tiles' pixels) are all read before any is
+  // used, and (PIPE) the next step's are read before this step's MFMAs, at +28 VGPRs
+  constexpr int NS = (CE - CB) * 2;
+  auto read_step = [&](int st, bf16x8 (&w)[3], uint32_t (&q)[C1_TILES][4]) {
+    const int c = CB + (st >> 1), h2 = st & 1;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) w[t] = wfrag((2 * c + h2) * 3 + t);
+#pragma unroll
+    for (int i = 0; i < C1_TILES; ++i) {
+      if (i >= nt) break;
+      const int o = c * PLANE + off[i] + 4 * h2 * IMG;
+      if constexpr (U8) {
+        const uint32_t* p = (const uint32_t*)(x8 + o);            // 4-byte aligned
+        q[i][0] = p[0];
+        q[i][1] = p[1];
+      } else {
+        const uint2* p = (const uint2*)(xb + o);                   // 8-byte aligned
+        const uint2 lo = p[0], hi = p[1];
+        q[i][0] = lo.x; q[i][1] = lo.y; q[i][2] = hi.x; q[i][3] = hi.y;
+      }
+    }
+  };
+  bf16x8 w[3];
+  uint32_t q[C1_TILES][4];
+  read_step(0, w, q);
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    bf16x8 a[C1_TILES];
+#pragma unroll
+    for (int i = 0; i < C1_TILES; ++i) {
+      if (i >= nt) break;
+      if constexpr (U8) a[i] = u8x8_to_bf16(q[i][0], q[i][1]);
+      else a[i] = __builtin_bit_cast(bf16x8, make_uint4(q[i][0], q[i][1], q[i][2], q[i][3]));
+    }
+    const bf16x8 w0 = w[0], w1 = w[1], w2 = w[2];
+    if (PIPE && st + 1 < NS) read_step(st + 1, w, q);
+#pragma unroll
+    for (int i = 0; i < C1_TILES; ++i) {
+      if (i >= nt) break;
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w0, acc[i], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < C1_TILES; ++i) {
+      if (i >= nt) break;
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w1, acc[i], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < C1_TILES; ++i) {
+      if (i >= nt) break;
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w2, acc[i], 0, 0, 0);
+    }
+    if (!PIPE && st + 1 < NS) read_step(st + 1, w, q);
+  }
+}
+
+// conv1 bias + relu of the accumulated tiles -> l1s as three bf16 terms (and act_l1), then conv2
+// (bf16x6 MFMA) + relu -> act_l2 for state b.
+template <bool SAVE_L1, bool EW>
+__device__ inline void conv12_finish(f32x4 (&acc)[C1_TILES], float* l1s, int64_t b,
+                                     const uint16_t* __restrict__ w1s, const float* __restrict__ b1,
+                                     const float* __restrict__ W2, float* __restrict__ act_l1,
+                                     float* __restrict__ act_l2, float (&w2r)[64], float bias2,
+                                     uint64_t* dbg) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i16 = lane & 15, j4 = lane >> 4;
   const int nt = wid & 1, grp = wid >> 1;          // conv2: M-tiles grp and grp + 4 (when < 6)
-  // conv1 weight fragments (3 bf16 terms per K step)
-  bf16x8 wf[C1_K][3];
-#pragma unroll
-  for (int kh = 0; kh < C1_K; ++kh)
-#pragma unroll
-    for (int t = 0; t < 3; ++t) wf[kh][t] = __builtin_bit_cast(bf16x8, ((const uint4*)w1s)[(kh * 3 + t) * 64 + lane]);
   const float bias1 = b1[i16];
-  __syncthreads();
-
-  // ---- conv1 ----
-  for (int m = wid; m < C1_P / 16; m += 8) {
-    const int p = 16 * m + i16;
-    const int oy = p / C1_O, ox = p - oy * C1_O;
-    const uint16_t* row = xb + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;    // cin = j4
-    const uint8_t* row8 = x8 + j4 * PLANE + (C1_S * oy) * IMG + C1_S * ox;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accb = {0.f, 0.f, 0.f, 0.f};
+  const int n1 = conv1_ntiles(__builtin_amdgcn_readfirstlane(wid));
 #pragma unroll
-    for (int kh = 0; kh < C1_K; ++kh) {
-      bf16x8 a;
-      if constexpr (U8) {
-        const uint32_t* q = (const uint32_t*)(row8 + kh * IMG);              // 4-byte aligned
-        a = u8x8_to_bf16(q[0], q[1]);
-      } else {
-        const uint2* q = (const uint2*)(row + kh * IMG);                      // 8-byte aligned
-        const uint2 lo = q[0], hi = q[1];
-        a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-      }
-      // two chains by kh parity (a third accumulator measured +46 VGPRs: 170, which breaks the
-      // overlap-mode co-residency budget of 128, and 3.85M -> 3.13M env-steps/s)
-      f32x4& c = (kh & 1) ? accb : acc;
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][1], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[kh][2], c, 0, 0, 0);
-    }
-    acc += accb;
+  for (int i = 0; i < C1_TILES; ++i) {
+    if (i >= n1) break;
+    const int m = wid + 8 * i;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int pos = 16 * m + 4 * j4 + r;
-      float v = fmaxf(acc[r] * (1.0f / 255.0f) + bias1, 0.f);
+      float v = fmaxf(acc[i][r] * (1.0f / 255.0f) + bias1, 0.f);
 #ifdef C2_FP32
       l1s[pos * L1S_LD + i16] = v;
 #else
@@ -210,7 +260,9 @@ __device__ inline void conv12_core(const uint8_t* x8, const uint16_t* xb, float*
 #pragma unroll
   for (int t = 0; t < 3; ++t) bq[t] = w2f[t * 64];
 #endif
+  if (dbg && threadIdx.x == 0) dbg[12] = __builtin_readcyclecounter();
   __syncthreads();
+  if (dbg && threadIdx.x == 0) dbg[13] = __builtin_readcyclecounter();
 
   // ---- conv2: 6 M-tiles (81 rows padded to 96) x 2 N-tiles, K = 16 (kh,kw) x 16 cin ----
   const int nm = grp + 4 < 6 ? 2 : 1;
@@ -285,6 +337,29 @@ __device__ inline void conv12_core(const uint8_t* x8, const uint16_t* xb, float*
     }
   }
 }
+
+// conv1 + conv2 of state b (planes staged by the caller, not yet synchronised).  The conv1 weight
+// fragments (24 KB) are staged in the l1 region, which conv1's epilogue overwrites afterwards.
+static_assert(W1S_ELEMS * 2 <= L1S_BYTES, "conv1 weights staged in the l1 region");
+template <bool SAVE_L1, bool EW, bool U8>
+__device__ inline void conv12_core(const uint8_t* x8, const uint16_t* xb, float* l1s, int64_t b,
+                                   const uint16_t* __restrict__ w1s, const float* __restrict__ b1,
+                                   const float* __restrict__ W2, float* __restrict__ act_l1,
+                                   float* __restrict__ act_l2, float (&w2r)[64], float bias2,
+                                   uint64_t* dbg = nullptr) {
+  const int lane = threadIdx.x & 63;
+  uint4* wl = (uint4*)l1s;
+  for (int i = threadIdx.x; i < W1S_ELEMS / 8; i += blockDim.x) wl[i] = ((const uint4*)w1s)[i];
+  __syncthreads();
+  if (dbg && threadIdx.x == 0) dbg[11] = __builtin_readcyclecounter();
+  f32x4 acc[C1_TILES];
+#pragma unroll
+  for (int i = 0; i < C1_TILES; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  conv1_accum<U8, 0, HIST>(x8, xb, acc, [&](int f) { return __builtin_bit_cast(bf16x8, wl[f * 64 + lane]); });
+  lds_only_barrier();                                  // weights read: the l1 region is conv1's output
+  conv12_finish<SAVE_L1, EW>(acc, l1s, b, w1s, b1, W2, act_l1, act_l2, w2r, bias2, dbg);
+}
+
 
 // U8: the planes stay u8 in LDS (28 KB instead of 56 KB) and each conv1 A operand is converted
 // to bf16 in registers (8 pixels: 2 ds_read_b32 + 8 v_cvt_f32_ubyte + 4 v_perm) -- a 60 KB
@@ -584,6 +659,7 @@ __device__ inline int32_t head_act_env(const float* __restrict__ h3, const float
     } else {
       env_store(sel.envb, nxt, s, false);                    // frame: after the action draw
     }
+    if (dbg) dbg[17] = __builtin_readcyclecounter();
   }
   __syncthreads();
   int32_t frame;
@@ -660,11 +736,20 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   // the next state's planes 0..2 (frames tau-1 .. tau+1 - 1): already in the ring.  Prefetched by
   // waves 2..7 only: in waves 0 (head) and 1 (env act) these loads would queue ahead of the head's
   // and the env state's (in-order vmcnt) -- measured +3k cycles on the head
+  // ... and the conv1 weight fragments of those planes (18 KB).  LDS while the frame streams in:
+  // scratch [0, 42 KB) = planes 0..2 as bf16 (converted once here, not per conv1 operand),
+  // x8 region [0, 18 KB) = their weight fragments; after the screen the x8 region holds the new
+  // plane as bf16 (written by the vertical pass) and the scratch becomes conv1's output.
   constexpr int NCH3 = (HIST - 1) * (PLANE / 16);        // 1323 chunks of 16 pixels
   constexpr int PT = 512 - 128;                          // prefetching threads
   constexpr int PER3 = (NCH3 + PT - 1) / PT;             // 4
+  constexpr int NWF = (HIST - 1) * 2 * 3 * 64;           // 1152 16-byte fragment rows
+  constexpr int PERW = NWF / PT;                         // 3
+  static_assert(NWF % PT == 0 && NWF * 16 <= HIST * PLANE, "old-plane conv1 weights in the x8 region");
+  static_assert((HIST - 1) * PLANE * 2 <= 51 * 1024, "old planes as bf16 in the screen scratch");
+  static_assert(PLANE * 2 <= HIST * PLANE, "new plane as bf16 in the x8 region");
   const int pt = (int)threadIdx.x - 128;
-  uint4 pv[PER3];
+  uint4 pv[PER3], wv[PERW];
   if (pt >= 0) {
 #pragma unroll
     for (int k = 0; k < PER3; ++k) {
@@ -672,25 +757,60 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
       const int c = i / (PLANE / 16), j = i - c * (PLANE / 16);
       pv[k] = ((const uint4*)state_plane(nx.sa, b, c, tau0))[j];
     }
+#pragma unroll
+    for (int k = 0; k < PERW; ++k) wv[k] = ((const uint4*)nx.w1s)[pt + PT * k];
+#ifdef HS_TIMES
+    if (dbg && pt == 0) dbg[16] = __builtin_readcyclecounter() + (pv[0].x & 0) + (wv[PERW - 1].x & 0);
+#endif
   }
   const int32_t frame = head_act_env(h3, Wp, bp, Wv, bv, A, zs, z, sel, b, tau, dbg);
+  uint16_t* xold = (uint16_t*)smem;                      // planes 0..2, bf16
+  uint4* wlds = (uint4*)x8;
   if (pt >= 0) {
 #pragma unroll
     for (int k = 0; k < PER3; ++k) {
-      const int i = pt + PT * k;
-      if (i < NCH3) ((uint4*)x8)[i] = pv[k];
+      const int i = pt + PT * k;                         // chunk i = pixels 16 i .. 16 i + 15
+      if (i < NCH3) {
+        uint4* d = (uint4*)(xold + 16 * i);
+        const uint2 a0 = atari::u8x4_to_bf16x4(pv[k].x), a1 = atari::u8x4_to_bf16x4(pv[k].y);
+        const uint2 a2 = atari::u8x4_to_bf16x4(pv[k].z), a3 = atari::u8x4_to_bf16x4(pv[k].w);
+        d[0] = make_uint4(a0.x, a0.y, a1.x, a1.y);
+        d[1] = make_uint4(a2.x, a2.y, a3.x, a3.y);
+      }
     }
+#pragma unroll
+    for (int k = 0; k < PERW; ++k) wlds[pt + PT * k] = wv[k];
   }
-  // plane 3 = the new screen: to the ring slot (tau + 1) % R and to x8
-  atari::screen_frame<512>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3),
-                           sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE, smem, dbg,
-                           x8 + (HIST - 1) * PLANE);
-  if (dbg && threadIdx.x == 0) dbg[9] = __builtin_readcyclecounter();
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // conv1 over the 3 older planes while the new frame streams in from HBM (LDS operands only:
+  // nothing here waits on the frame loads); the newest plane's K-steps follow the screen
+  f32x4 acc[C1_TILES];
+#pragma unroll
+  for (int i = 0; i < C1_TILES; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto conv1_old = [&]() {
+    lds_only_barrier();                                  // planes 0..2 and their weights staged
+    conv1_accum<false, 0, HIST - 1, false>(nullptr, xold, acc,   // (no pipelining: the frame holds 51 VGPRs)
+                                           [&](int f) { return __builtin_bit_cast(bf16x8, wlds[f * 64 + lane]); });
+    lds_only_barrier();                                  // operands read: scratch and x8 are the screen's
+  };
+  // plane 3 = the new screen: to the ring slot (tau + 1) % R and, as bf16, to the x8 region
+  uint16_t* xnew = (uint16_t*)x8;
+  atari::screen_frame<512>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3),
+                           sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE, smem, dbg, xnew,
+                           conv1_old);
+  if (dbg && threadIdx.x == 0) dbg[9] = __builtin_readcyclecounter();
+  uint4 wn[6];
+#pragma unroll
+  for (int f = 0; f < 6; ++f) wn[f] = ((const uint4*)nx.w1s)[((HIST - 1) * 6 + f) * 64 + lane];
   float w2r[64];
   const float bias2 = nx.b2[16 * (wid & 1) + (lane & 15)];
-  conv12_core<SAVE_L1, false, true>(x8, nullptr, (float*)smem, b, nx.w1s, nx.b1, nx.W2,
-                                    SAVE_L1 ? nx.act_l1 : nullptr, nx.act_l2, w2r, bias2);
+  __syncthreads();                                       // plane 3 complete in x8
+  if (dbg && threadIdx.x == 0) dbg[11] = __builtin_readcyclecounter();
+  conv1_accum<false, HIST - 1, HIST>(nullptr, xnew - (HIST - 1) * PLANE, acc, [&](int f) {
+    return __builtin_bit_cast(bf16x8, wn[f - (HIST - 1) * 6]);
+  });
+  conv12_finish<SAVE_L1, false>(acc, (float*)smem, b, nx.w1s, nx.b1, nx.W2, SAVE_L1 ? nx.act_l1 : nullptr,
+                                nx.act_l2, w2r, bias2, dbg);
   span_end(srec);
   if (dbg) {
     __syncthreads();

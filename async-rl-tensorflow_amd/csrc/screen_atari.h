@@ -182,9 +182,24 @@ __device__ inline void hpass_seg(const uint8_t* __restrict__ grow, uint8_t* __re
 // of 3 output rows x 21 column quads, lane = (row, quad), taps read from the LDS table.
 #define SCREEN_KV_BYTES (84 * 8 * 4)
 #define SCREEN_FRAME_SMEM (210 * 160 + 210 * 84 + 96 + SCREEN_KV_BYTES)
-template <int NT>
+// 4 u8 pixels (one dword, little-endian) -> 4 bf16 (exact: integers 0..255 are the upper half of
+// their f32)
+__device__ inline uint2 u8x4_to_bf16x4(uint32_t d) {
+  const float f0 = (float)(d & 255u), f1 = (float)((d >> 8) & 255u);
+  const float f2 = (float)((d >> 16) & 255u), f3 = (float)(d >> 24);
+  return make_uint2(__builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u),
+                    __builtin_amdgcn_perm(__float_as_uint(f3), __float_as_uint(f2), 0x07060302u));
+}
+
+struct NoScreenMid {
+  __device__ void operator()() const {}
+};
+
+// mid(): work run by every thread while its frame loads are in flight, before the luminance
+// pass writes the scratch (it may use the first 51 KB of smem; it must not wait on vector memory)
+template <int NT, typename Mid = NoScreenMid>
 __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __restrict__ out, uint8_t* smem,
-                                    uint64_t* dbg = nullptr, uint8_t* lds_copy = nullptr) {
+                                    uint64_t* dbg = nullptr, uint16_t* lds_bf16 = nullptr, Mid mid = Mid()) {
   uint8_t* gray = smem;
   uint8_t* tmp = smem + IH * IW;
   int* kvs = (int*)(tmp + IH * OW + 96);              // [yy][8]: 7 taps, xmin
@@ -193,13 +208,27 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
   constexpr int NWV = NT / 64;
   constexpr int NUNIT = IH * IW / 4;                   // 8400 units of 4 pixels (12 bytes)
   constexpr int PER = (NUNIT + NT - 1) / NT;
+  // the vertical-tap table's loads are issued first and written after mid(): loads retire in
+  // order (vmcnt), so waiting for one issued behind the frame would wait for the whole frame
+  constexpr int NKV = OH * 8, PKV = (NKV + NT - 1) / NT;
+  int kv[PKV];
+#pragma unroll
+  for (int j = 0; j < PKV; ++j) {
+    const int i = min(tid + NT * j, NKV - 1);
+    kv[j] = (i & 7) < KV ? cV.k[i >> 3][i & 7] : cV.xmin[i >> 3];
+  }
   uint3 r[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const uint32_t* s = (const uint32_t*)(rgb + 12 * min(tid + NT * j, NUNIT - 1));
     r[j] = make_uint3(s[0], s[1], s[2]);
   }
-  for (int i = tid; i < OH * 8; i += NT) kvs[i] = (i & 7) < KV ? cV.k[i >> 3][i & 7] : cV.xmin[i >> 3];
+  if (dbg && tid == 0) dbg[14] = __builtin_readcyclecounter();
+  mid();
+  if (dbg && tid == 0) dbg[15] = __builtin_readcyclecounter();
+#pragma unroll
+  for (int j = 0; j < PKV; ++j)
+    if (tid + NT * j < NKV) kvs[tid + NT * j] = kv[j];
   if (dbg && tid == 0) dbg[4] = __builtin_readcyclecounter() + (r[0].x & 0);   // first unit landed
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -243,7 +272,7 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
 #pragma unroll
       for (int c = 0; c < 4; ++c) packed |= (uint32_t)(acc[c] >> A3C_PRECISION_BITS) << (8 * c);
       st_act((uint32_t*)(out + yy * OW + 4 * cq), packed);
-      if (lds_copy) *(uint32_t*)(lds_copy + yy * OW + 4 * cq) = packed;   // (fused conv12: x8 plane 3)
+      if (lds_bf16) *(uint2*)(lds_bf16 + yy * OW + 4 * cq) = u8x4_to_bf16x4(packed);   // (fused conv12)
     }
   }
   if (dbg) {

@@ -20,7 +20,7 @@ torch.cuda.synchronize()
 KER = int(os.environ.get('HS_KER', _lib.KER_HEAD_SCREEN))   # 5: the fused head+screen+conv kernel
 names = ['start', 'head_row', 'head_act', 'barrier1', 'first_load', 'lum_done', 'barrier2', 'hpass', 'vpass']
 if KER == _lib.KER_HEAD_SCREEN_CONV12:
-    names += ['(screen end)', 'conv_done', 'c1_start', 'c1_done', 'c2_start']
+    names += ['(screen end)', 'conv_done', 'c1_start', 'c1_w0_done', 'c1_all_done', 'mid_start', 'mid_end', 'w2_loads_done', 'w1_env_done']
 for rep in range(3):
     eng.time_kernel(KER, 1)
     torch.cuda.synchronize()
