@@ -109,14 +109,27 @@ __device__ inline uint32_t lum4(uint32_t d0, uint32_t d1, uint32_t d2) {
   constexpr uint32_t WLO = 78u | (240u << 8) | (210u << 16);
   constexpr uint32_t WHI = 8u | (27u << 8) | (2u << 16);
   const uint32_t px[4] = {d0, __builtin_amdgcn_alignbyte(d1, d0, 3), __builtin_amdgcn_alignbyte(d2, d1, 2), d2 >> 8};
-  uint32_t out = 0;
+  // stage by stage over the 4 pixels (independent chains interleave instead of each pixel's
+  // dependent dot4 -> shift -> dot4 -> multiply sequence waiting on its own latency)
+  uint32_t y[4], q[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) y[i] = __builtin_amdgcn_udot4(px[i], WHI, 0u, false) << 8;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) y[i] = __builtin_amdgcn_udot4(px[i], WLO, y[i], false) & 0x3FFFFFu;
+  // y <= 2,550,000 < 2^22, so floor(y / 10^4) = (y * 13743896) >> 37 (exhaustively checked over
+  // [0, 2550000]) on the full-rate 24-bit multiplier (v_mul_hi_u32_u24), not the quarter-rate
+  // 32-bit v_mul_hi_u32; the mask only tells the compiler the operand width
+  // y is a multiple of 10^4 iff the product's low 37 bits are below 2^22 (multiples leave
+  // q * 6528 <= 1,664,640 there, the others at least 13,743,896; exhaustively checked)
   bool mult = false;
+  uint32_t out = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const uint32_t y = __builtin_amdgcn_udot4(px[i], WLO, __builtin_amdgcn_udot4(px[i], WHI, 0u, false) << 8, false);
-    const uint32_t q = __umulhi(y, 3518437209u) >> 13;
-    mult |= q * 10000u == y;
-    out |= q << (8 * i);
+    const uint32_t hi = (uint32_t)(((uint64_t)y[i] * 13743896ull) >> 32);   // v_mul_hi_u32_u24
+    const uint32_t lo = y[i] * 13743896u;                                   // v_mul_u32_u24
+    q[i] = hi >> 5;
+    mult |= (hi & 31u) == 0u && lo < (1u << 22);
+    out |= q[i] << (8 * i);
   }
   if (mult) {
     out = 0;
