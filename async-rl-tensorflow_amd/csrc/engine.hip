@@ -74,6 +74,8 @@ struct a3c_engine {
   float* eps;              // q: per env epsilon
   float* ep_end;           // q: per env final epsilon
   float* ws;               // backward workspace
+  float* fcpart;           // fused overlap rollout: the fc as FC_NS K-slice partials [FC_NS][E][FC]
+  int fc_split;            // 1: the fused rollout's fc runs as k_fc_part + the head's fold
   float* lws;              // LSTM BPTT workspace (a3c_lstm_ws_floats)
   float* ldh;              // LSTM: dL/dh_t from the heads [nE][U]
   double* opt_part;
@@ -193,6 +195,8 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   // (1024-thread screen, early-W2 conv12) with the GPU to themselves
   e->fuse_conv = e->overlap;
   if (const char* v = getenv("A3C_FUSE_CONV")) e->fuse_conv = atoi(v) != 0;
+  e->fc_split = 1;
+  if (const char* v = getenv("A3C_FC_SPLIT")) e->fc_split = atoi(v) != 0;
   e->nslot = e->overlap ? 2 : 1;
   // ring: the states of one rollout (frames tau-3 .. tau+n); overlap keeps two rollouts' frames
   e->R = (e->overlap ? 2 * e->n : e->n) + HIST + (cfg->net.algo == A3C_ALGO_Q ? 1 : 0);
@@ -265,6 +269,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   ALLOC(e->ep_end, E * 4);
   BwdPlan bp = a3c_bwd_plan(L, nE);
   ALLOC(e->ws, bp.total * 4);
+  ALLOC(e->fcpart, (int64_t)FC_NS * E * FC * 4);
   ALLOC(e->opt_part, (int64_t)SS_MAX_BLOCKS * 8);
   ALLOC(e->sched, 64);
 #undef ALLOC
@@ -359,6 +364,8 @@ static bool spans_on() {
 }
 // conv fusion (k_head_screen_conv12) runs with the device envs and the fused screen
 static bool conv_fused(const a3c_engine* e) { return e->fuse_conv && !e->ext && e->fused_screen; }
+// the fused rollout's fc as K-slice partials folded by the head (feed-forward head only)
+static bool fc_split(const a3c_engine* e) { return conv_fused(e) && e->fc_split && !e->L.lstm; }
 
 __global__ void k_advance_tau(int64_t* counters, int n) { counters[0] += n; }
 
@@ -473,7 +480,8 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
   }
   int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
                               sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s,
-                              L.lstm ? &ls : nullptr, fuse && t > 0, has_next ? &nx : nullptr);
+                              L.lstm ? &ls : nullptr, fuse && t > 0, has_next ? &nx : nullptr,
+                              fc_split(e) ? e->fcpart : nullptr);
   if (rc) return rc;
   if (dev_env && !e->fused_screen) {
     rc = a3c_env_screen_launch(E, sl.frames + o, e->pool, e->ring, e->R, e->counters, t, s);
@@ -513,10 +521,40 @@ static int enqueue_rollout_end(a3c_engine* e, const Slot& sl, hipStream_t s) {
   return 0;
 }
 
+// Debug builds only (-DA3C_MARKERS, tools/markers.py): one-lane marker kernels captured at the
+// edges of the rollout and backward graphs record (id, s_memrealtime) in a device log, so the
+// unprofiled timeline of the two streams (and the cross-stream hops between them) can be read.
+#ifdef A3C_MARKERS
+#define MARK_CAP 8192
+__device__ unsigned long long g_marks[2 + 2 * MARK_CAP];
+__global__ void k_mark(int id) {
+  const unsigned long long i = atomicAdd(&g_marks[0], 1ull);
+  if (i < MARK_CAP) {
+    g_marks[2 + 2 * i] = (unsigned long long)id;
+    g_marks[3 + 2 * i] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+static void mark(int id, hipStream_t s) { hipLaunchKernelGGL(k_mark, dim3(1), dim3(1), 0, s, id); }
+extern "C" int a3c_debug_marks(unsigned long long* host, int reset) {
+  A3C_CHECK(hipDeviceSynchronize());
+  A3C_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_marks), sizeof(g_marks)));
+  if (reset) {
+    unsigned long long z = 0;
+    A3C_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_marks), &z, sizeof(z)));
+  }
+  return MARK_CAP;
+}
+#else
+static void mark(int, hipStream_t) {}
+#endif
+
 static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
+  mark(0, s);
   int rc = enqueue_rollout_begin(e, sl, s);
   for (int t = 0; t < e->n && !rc; ++t) rc = enqueue_step(e, sl, t, s);
-  return rc ? rc : enqueue_rollout_end(e, sl, s);
+  rc = rc ? rc : enqueue_rollout_end(e, sl, s);
+  mark(1, s);
+  return rc;
 }
 
 // returns / TD target, loss + backward over the slot's n*E samples, per-tensor norms (+ the
@@ -525,6 +563,7 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s);
 static int enqueue_grad(a3c_engine* e, const Slot& sl, hipStream_t s) {
   // overlap: the backward shares CUs with the next rollout -> small-footprint kernel variants
   a3c_set_shared_gpu(e->overlap != 0);
+  mark(2, s);
   int rc = enqueue_grad_impl(e, sl, s);
   a3c_set_shared_gpu(false);
   return rc;
@@ -595,8 +634,12 @@ static int enqueue_apply(a3c_engine* e, int snap, hipStream_t s) {
   op.mode = e->cfg.world_size > 1 ? OPT_APPLY : (OPT_CLIP | OPT_APPLY);
   int rc = a3c_apply_launch(e->params, e->ms, e->mom, e->grads, e->tt, op, e->opt_part,
                             e->cfg.world_size > 1 ? nullptr : e->sumsq, s);
-  if (rc || !e->overlap) return rc;
+  if (rc || !e->overlap) {
+    mark(3, s);
+    return rc;
+  }
   A3C_CHECK(hipMemcpyAsync(e->slot[snap].P, e->params, e->L.total * 4, hipMemcpyDeviceToDevice, s));
+  mark(3, s);
   return 0;
 }
 
@@ -712,6 +755,13 @@ static int rollout_grad(a3c_engine* e, hipStream_t s, bool fused) {
   if (rc) return rc;
   A3C_CHECK(hipEventRecord(e->ev_roll[p], e->rs));
   e->grad_ready = false;
+#ifdef A3C_MARKERS
+  static const bool abl_bwd = getenv("A3C_ABL_BWD") != nullptr;   // measurement only: rollouts alone
+  if (abl_bwd && e->iter >= 4) {
+    e->iter += 1;
+    return 0;
+  }
+#endif
   if (e->iter >= 1) {
     A3C_CHECK(hipStreamWaitEvent(s, e->ev_roll[p ^ 1], 0));
     rc = fused ? run_graph(e, 6 + (p ^ 1), 3, p ^ 1, s) : run_graph(e, 3 + (p ^ 1), 2, p ^ 1, s);
@@ -929,6 +979,8 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
       case A3C_KER_FC_FWD:
         return a3c_fc_fwd_launch(sl.act_l2, (const float*)(sl.prep + PREP_W1S_BYTES), e->params + L.off[T_FCB],
                                  sl.act_l3, E, s, e->params + L.off[T_FCW]);
+      case A3C_KER_FC_PART:
+        return a3c_fc_part_launch(sl.act_l2, (const float*)(sl.prep + PREP_W1S_BYTES), e->fcpart, E, s);
       case A3C_KER_ENV_STEP:
         return a3c_env_screen_launch(E, sl.frames, e->pool, e->ring, e->R, e->counters, 0, s);
       case A3C_KER_HEAD_SCREEN:
@@ -957,6 +1009,11 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
         nx.b1 = e->params + L.off[T_L1B]; nx.W2 = e->params + L.off[T_L2W]; nx.b2 = e->params + L.off[T_L2B];
         nx.act_l1 = sl.act_l1 + (int64_t)E * C1_P * C1_N;
         nx.act_l2 = sl.act_l2 + (int64_t)E * FLAT;
+        if (fc_split(e)) {       // the head folds the fc partials, as in the rollout
+          sel.fc_part = e->fcpart;
+          sel.fc_bias = e->params + L.off[T_FCB];
+          sel.l3_out = sl.act_l3;
+        }
         return a3c_head_screen_conv12_launch(L, e->params, L.lstm ? sl.lh : sl.act_l3, E, sl.z, sel, nx, s);
       }
       case A3C_KER_CONV_BWD: {

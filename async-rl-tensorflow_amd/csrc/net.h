@@ -121,7 +121,14 @@ struct HeadSelect {
   // once the launch's heads are written (the rollout's tau advance, no kernel of its own)
   int64_t* adv_ptr;
   int64_t adv_n;
+  // k_head_screen_conv12 only (fused overlap rollout): the fc layer arrives as FC_NS K-slice
+  // partials fc_part[x][b][FC] (k_fc_part); the head folds them in slice order, + fc_bias, ReLU,
+  // and writes the layer output row to l3_out[b] (the backward's activation)
+  const float* fc_part;
+  const float* fc_bias;
+  float* l3_out;
 };
+#define FC_NS 8                 // K-slices of the partial fc (= waves of k_head_screen_conv12)
 
 // forward of B states; returns 0 or error
 // prep: the forward's prepared weights of `params` (a3c_prep_fwd_launch, PREP_BYTES):
@@ -149,7 +156,9 @@ struct Conv12Next {
 int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* prep, const StateAddr& sa,
                        int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
                        hipStream_t s, const LstmStep* ls = nullptr, bool skip_conv12 = false,
-                       const Conv12Next* next = nullptr);
+                       const Conv12Next* next = nullptr, float* fc_part = nullptr);
+// fc layer as FC_NS K-slice partials part[x][M][FC] (folded by k_head_screen_conv12's head)
+int a3c_fc_part_launch(const float* A, const float* Wp, float* part, int64_t M, hipStream_t s);
 // tau_src / tau_dst (nullable): *tau_dst = *tau_src as well (the overlap rollout's tau snapshot)
 int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s,
                         const int64_t* tau_src = nullptr, int64_t* tau_dst = nullptr);

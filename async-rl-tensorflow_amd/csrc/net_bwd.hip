@@ -729,6 +729,10 @@ void a3c_set_shared_gpu(bool v) { t_shared_gpu = v; }
 int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,
                         const float* dl2, float* ws, hipStream_t s) {
   const BwdPlan p = a3c_bwd_plan(L, B);
+#ifdef A3C_MARKERS
+  static const bool ablate = getenv("A3C_ABL_CBWD") != nullptr;   // measurement only: no conv backward
+  if (ablate) return 0;
+#endif
   // sync: the DMA-prefetching kernel at 8 waves (2 per SIMD) owns the GPU; overlap: the compact
   // 4-wave kernel leaves registers and LDS for the concurrent rollout (measured, tools/ab.sh)
   static const int env_nw = getenv("A3C_CB_WAVES") ? atoi(getenv("A3C_CB_WAVES")) : 0;

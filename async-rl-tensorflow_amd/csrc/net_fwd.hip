@@ -622,7 +622,8 @@ __global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, 
 __device__ inline int32_t head_act_env(const float* __restrict__ h3, const float* __restrict__ Wp,
                                        const float* __restrict__ bp, const float* __restrict__ Wv,
                                        const float* __restrict__ bv, int A, int zs, float* __restrict__ z,
-                                       const HeadSelect& sel, int64_t b, int64_t tau, uint64_t* dbg) {
+                                       const HeadSelect& sel, int64_t b, int64_t tau, uint64_t* dbg,
+                                       const float* hrow = nullptr) {
   __shared__ int32_t s_act;
   __shared__ uint32_t s_draw, s_term;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -632,7 +633,9 @@ __device__ inline int32_t head_act_env(const float* __restrict__ h3, const float
     const float eps = sel.mode != 0 && sel.eps ? sel.eps[e] : 0.f;
     u32x4 x;
     // the action draw does not depend on the head: computed under its load latency
-    const float myz = head_row(h3, b, Wp, bp, Wv, bv, A, lane, [&]() { x = action_draw(sel, b, tau); });
+    // (hrow: the layer-output row, already folded into LDS by the caller)
+    const float myz = hrow ? head_row(hrow, 0, Wp, bp, Wv, bv, A, lane, [&]() { x = action_draw(sel, b, tau); })
+                           : head_row(h3, b, Wp, bp, Wv, bv, A, lane, [&]() { x = action_draw(sel, b, tau); });
     if (dbg) {
       if (lane == 0) dbg[1] = __builtin_readcyclecounter() + (uint64_t)(myz * 0.f);
     } else if (lane < zs) {
@@ -665,6 +668,9 @@ __device__ inline int32_t head_act_env(const float* __restrict__ h3, const float
   int32_t frame;
   if (sel.env_on) {
     frame = env_frame_of(s_draw + sel.frame_salt, (uint32_t)s_act, sel.envp);
+#ifdef A3C_ABL_FRAME
+    frame = e & 63;   // measurement only: every step reads from 64 L2-resident frames
+#endif
     if (threadIdx.x == 0) {
       sel.frames_out[e] = frame;
       if (!s_term) sel.envb.frame[nxt] = frame;
@@ -748,6 +754,16 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   static_assert(NWF % PT == 0 && NWF * 16 <= HIST * PLANE, "old-plane conv1 weights in the x8 region");
   static_assert((HIST - 1) * PLANE * 2 <= 51 * 1024, "old planes as bf16 in the screen scratch");
   static_assert(PLANE * 2 <= HIST * PLANE, "new plane as bf16 in the x8 region");
+  // fc as K-slice partials (sel.fc_part): wave w's first load is slice w's partial row of env b,
+  // ahead of everything else it loads (vmcnt retires in order)
+  static_assert(FC_NS * 64 == 512, "one partial slice per wave");
+  const int fwid = threadIdx.x >> 6, flane = threadIdx.x & 63;
+  const bool fold = sel.fc_part != nullptr;
+  f32x4 fpart = {0.f, 0.f, 0.f, 0.f}, fbias = {0.f, 0.f, 0.f, 0.f};
+  if (fold) {
+    fpart = *(const f32x4*)(sel.fc_part + ((int64_t)fwid * gridDim.x + b) * FC + 4 * flane);
+    if (fwid == 0) fbias = *(const f32x4*)(sel.fc_bias + 4 * flane);
+  }
   const int pt = (int)threadIdx.x - 128;
   uint4 pv[PER3], wv[PERW];
   if (pt >= 0) {
@@ -763,7 +779,25 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
     if (dbg && pt == 0) dbg[16] = __builtin_readcyclecounter() + (pv[0].x & 0) + (wv[PERW - 1].x & 0);
 #endif
   }
-  const int32_t frame = head_act_env(h3, Wp, bp, Wv, bv, A, zs, z, sel, b, tau, dbg);
+  const float* hrow = nullptr;
+  if (fold) {
+    // fold the FC_NS slices in slice order, + bias, ReLU (wave 0; LDS [0, 9 KB) is free until
+    // head_act_env's barrier); the row also goes to l3_out for the backward
+    f32x4* fl = (f32x4*)smem;
+    fl[fwid * 64 + flane] = fpart;
+    lds_only_barrier();
+    if (fwid == 0) {
+      f32x4 v = fl[flane];
+#pragma unroll
+      for (int w = 1; w < FC_NS; ++w) v += fl[w * 64 + flane];
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) v[c4] = fmaxf(v[c4] + fbias[c4], 0.f);
+      fl[FC_NS * 64 + flane] = v;
+      *(f32x4*)(sel.l3_out + b * FC + 4 * flane) = v;
+    }
+    hrow = (const float*)(fl + FC_NS * 64);
+  }
+  const int32_t frame = head_act_env(h3, Wp, bp, Wv, bv, A, zs, z, sel, b, tau, dbg, hrow);
   uint16_t* xold = (uint16_t*)smem;                      // planes 0..2, bf16
   uint4* wlds = (uint4*)x8;
   if (pt >= 0) {
@@ -838,7 +872,8 @@ int a3c_head_screen_conv12_launch(const NetLayout& L, const float* P, const floa
                                   const HeadSelect& sel, const Conv12Next& nx, hipStream_t s);
 int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* prep, const StateAddr& sa,
                        int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
-                       hipStream_t s, const LstmStep* ls, bool skip_conv12, const Conv12Next* next) {
+                       hipStream_t s, const LstmStep* ls, bool skip_conv12, const Conv12Next* next,
+                       float* fc_part) {
   if (B <= 0) return 0;
   if (L.lstm != (ls != nullptr))
     return a3c_set_error(A3C_ERR_INVALID, "a3c_forward", "the LSTM head needs its recurrent state");
@@ -847,8 +882,11 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
     int rc0 = a3c_conv12_launch(L, P, prep, sa, B, act_l1, act_l2, s);
     if (rc0) return rc0;
   }
-  int rc = a3c_fc_fwd_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), P + L.off[T_FCB], act_l3, B, s,
-                             P + L.off[T_FCW]);
+  // fused overlap rollout: the fc as K-slice partials, folded by the head of k_head_screen_conv12
+  const bool part = fc_part && next && !ls && sel.mode >= 0 && sel.env_on && sel.ring;
+  int rc = part ? a3c_fc_part_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), fc_part, B, s)
+                : a3c_fc_fwd_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), P + L.off[T_FCB], act_l3, B, s,
+                                    P + L.off[T_FCW]);
   if (rc) return rc;
   const float* head_in = act_l3;
   if (ls) {   // C5: LSTM cell on the fc output, heads on its h
@@ -858,8 +896,15 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
   }
   const float* Wv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VW] : nullptr;
   const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
-  if (sel.mode >= 0 && sel.env_on && sel.ring && next)
-    return a3c_head_screen_conv12_launch(L, P, head_in, B, z, sel, *next, s);
+  if (sel.mode >= 0 && sel.env_on && sel.ring && next) {
+    HeadSelect hs = sel;
+    if (part) {
+      hs.fc_part = fc_part;
+      hs.fc_bias = P + L.off[T_FCB];
+      hs.l3_out = act_l3;
+    }
+    return a3c_head_screen_conv12_launch(L, P, head_in, B, z, hs, *next, s);
+  }
   if (next) return a3c_set_error(A3C_ERR_INVALID, "a3c_forward", "conv fusion needs the fused env screen");
   if (sel.mode >= 0 && sel.env_on && sel.ring)
     return a3c_head_screen_launch(L, P, head_in, B, z, sel, s);
@@ -975,14 +1020,26 @@ __global__ void __launch_bounds__(64 * NW) k_fc_fwd(const float* __restrict__ A,
   // xcd_rows: 1-D grid, workgroup id -> XCD id % 8 gets a contiguous band of row tiles (all 16
   // column tiles each), so an XCD reads 1/8 of A and all of W (which is the same every step)
   int ct = blockIdx.x, mt = blockIdx.y;
-  if (xcd_rows) {
-    const int ntiles = gridDim.x, id = blockIdx.x;
-    const int t = (id & 7) * (ntiles >> 3) + (id >> 3);
-    ct = t % (FC / 16);
-    mt = t / (FC / 16);
+  int m0, rstride = 1;                 // tile row i is row m0 + rstride * i
+  if (xcd_rows == 2) {
+    // rows of one XCD's envs: workgroup id -> XCD id % 8 = x takes rows x, x + 8, ... (the l2 rows
+    // the rollout kernel's workgroups x + 8 k wrote on that XCD, and the l3 rows its next launch
+    // reads there), all 16 column tiles; speed only, any placement is correct
+    const int id = blockIdx.x, k = id >> 3;
+    ct = k % (FC / 16);
+    m0 = 128 * (k / (FC / 16)) + (id & 7);
+    rstride = 8;
+  } else {
+    if (xcd_rows) {
+      const int ntiles = gridDim.x, id = blockIdx.x;
+      const int t = (id & 7) * (ntiles >> 3) + (id >> 3);
+      ct = t % (FC / 16);
+      mt = t / (FC / 16);
+    }
+    m0 = mt * 16;
   }
-  const int m0 = mt * 16, n0 = ct * 16;
-  const int m = min(m0 + i16, M - 1);
+  const int n0 = ct * 16;
+  const int m = min(m0 + rstride * i16, M - 1);
   WG_T0();
   // the waves' partial tiles meet in LDS (fixed order), bias + relu, store
   auto fc_epilogue = [&](f32x4 acc) {
@@ -995,7 +1052,7 @@ __global__ void __launch_bounds__(64 * NW) k_fc_fwd(const float* __restrict__ A,
       const float bb = bias[n];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + 4 * j4 + r;
+        const int row = m0 + rstride * (4 * j4 + r);
         if (row < M) st_act(C + (int64_t)row * FC + n, fmaxf(acc[r] + bb, 0.f));
       }
     }
@@ -1080,6 +1137,102 @@ __global__ void __launch_bounds__(64 * NW) k_fc_fwd(const float* __restrict__ A,
   fc_epilogue(acc + acc1);
 }
 
+// ---------------------------------------------------------------------------------------
+// fc layer of the fused overlap rollout as K-slice partials (the consumer folds them): the
+// k_fc_fwd tile above moves 332 KB per workgroup (a 16-row A strip and a 16-column W strip over
+// all of K), which is what bounds it.  Here workgroup (x, rb, cb) multiplies the 32 rows of
+// row block rb by the 64 columns of column block cb over K-slice x only (20-21 of the 162
+// chunks of 16): 43 KB of A staged once in LDS and shared by the 4 waves (one 16-column tile
+// each, both 16-row tiles), 21 KB of packed W per wave -- 129 KB per workgroup.  The partial
+// sums go to part[x][row][256]; the head of the rollout kernel folds the FC_NS slices in a
+// fixed order (+ bias, ReLU), so the layer output is deterministic.  blockIdx.x & 7 is the
+// K-slice: under round-robin placement each XCD streams only its slice of W (332 KB), which
+// stays L2-resident across the rollout's steps (speed only, any placement is correct).
+// ---------------------------------------------------------------------------------------
+#define FCP_RB 32                               // rows per row block
+#define FCP_CB 64                               // columns per column block (4 waves x 16)
+#define FCP_MAXCH ((FC_CH + FC_NS - 1) / FC_NS + 1)   // 21 chunks per slice at most
+#define FCP_LD (FCP_MAXCH * 16 + 4)             // A row stride in LDS (floats), padded
+#define FCP_SMEM (FCP_RB * FCP_LD * 4)          // 43520
+__device__ inline int fcp_c0(int x) { return (FC_CH * x) / FC_NS; }
+
+__global__ void __launch_bounds__(256) k_fc_part(const float* __restrict__ A, const float* __restrict__ Wp,
+                                                 float* __restrict__ part, int M) {
+  __shared__ __attribute__((aligned(16))) float as[FCP_RB * FCP_LD];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i16 = lane & 15, j4 = lane >> 4;
+  const int id = blockIdx.x;
+  const int x = id % FC_NS, k = id / FC_NS;
+  const int rb = k / (FC / FCP_CB), cb = k % (FC / FCP_CB);
+  const int c0 = fcp_c0(x), c1 = fcp_c0(x + 1), nch = c1 - c0;
+  const int m0 = rb * FCP_RB, ct = cb * (FCP_CB / 16) + wid;
+  // this wave's packed-W chunks (16-byte fragments, 4 MFMAs each), the first D in flight before
+  // the A tile is staged.  D = 8 keeps the kernel at 96 VGPRs: all 21 in flight (152 VGPRs) is
+  // faster alone (6.8 vs 7.4 us) and loses overlapped (3.83M vs 4.09M env-steps/s)
+#ifndef FCP_D
+#define FCP_D 8
+#endif
+  constexpr int D = FCP_D;
+  const f32x4* bp = (const f32x4*)Wp + ((int64_t)ct * FC_CH + c0) * 64 + lane;
+  f32x4 rb4[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) rb4[d] = bp[(int64_t)min(d, nch - 1) * 64];
+  // A tile: 32 rows x nch chunks of 16 floats, f32x4 per thread-iteration, all loads issued first
+  constexpr int NA = (FCP_RB * FCP_MAXCH * 4 + 255) / 256;   // 11
+  f32x4 ra[NA];
+  const int q4 = nch * 4;                                    // f32x4 per row
+#pragma unroll
+  for (int u = 0; u < NA; ++u) {
+    const int i = min((int)threadIdx.x + 256 * u, FCP_RB * q4 - 1);
+    const int r = i / q4, q = i - r * q4;
+    ra[u] = *(const f32x4*)(A + (int64_t)min(m0 + r, M - 1) * FLAT + 16 * c0 + 4 * q);
+  }
+#pragma unroll
+  for (int u = 0; u < NA; ++u) {
+    const int i = (int)threadIdx.x + 256 * u;
+    if (i < FCP_RB * q4) {
+      const int r = i / q4, q = i - r * q4;
+      *(f32x4*)(as + r * FCP_LD + 4 * q) = ra[u];
+    }
+  }
+  __syncthreads();
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};   // row tiles 0 / 1
+  const float* a0 = as + i16 * FCP_LD + 4 * j4;
+  const float* a1 = a0 + 16 * FCP_LD;
+  for (int c = 0; c < nch; c += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (c + d < nch) {
+        const f32x4 x0 = *(const f32x4*)(a0 + 16 * (c + d));
+        const f32x4 x1 = *(const f32x4*)(a1 + 16 * (c + d));
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[c4], rb4[d][c4], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[c4], rb4[d][c4], acc1, 0, 0, 0);
+        }
+        const int cn = c + d + D;
+        if (cn < nch) rb4[d] = bp[(int64_t)cn * 64];
+      }
+    }
+  }
+  // partial tile rows m0 + 16 rt + 4 j4 + r, column 16 ct + i16
+  float* out = part + ((int64_t)x * M) * FC + 16 * ct + i16;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row0 = m0 + 4 * j4 + r, row1 = row0 + 16;
+    if (row0 < M) out[(int64_t)row0 * FC] = acc0[r];
+    if (row1 < M) out[(int64_t)row1 * FC] = acc1[r];
+  }
+}
+
+int a3c_fc_part_launch(const float* A, const float* Wp, float* part, int64_t M, hipStream_t s) {
+  if (M <= 0) return 0;
+  const int nrb = (int)((M + FCP_RB - 1) / FCP_RB);
+  hipLaunchKernelGGL(k_fc_part, dim3((unsigned)(FC_NS * nrb * (FC / FCP_CB))), dim3(256), 0, s, A, Wp, part, (int)M);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
 // row-major-weight variant (4 scalar B loads per chunk), kept for A/B measurement
 __global__ void __launch_bounds__(256) k_fc_fwd_rows(const float* __restrict__ A, const float* __restrict__ W,
                                                 const float* __restrict__ bias, float* __restrict__ C, int M) {
@@ -1145,6 +1298,10 @@ __global__ void __launch_bounds__(256) k_fc_fwd_rows(const float* __restrict__ A
 int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s,
                       const float* Wrows) {
   if (M <= 0) return 0;
+#ifdef A3C_MARKERS
+  static const bool ablate = getenv("A3C_ABL_FC") != nullptr;   // measurement only: no fc
+  if (ablate) return 0;
+#endif
   static const int env_nw = getenv("A3C_FC_WAVES") ? atoi(getenv("A3C_FC_WAVES")) : -1;
   const int nw = env_nw >= 0 ? env_nw : (a3c_shared_gpu() ? 4 : 8);
   if (nw == 0 && Wrows)
@@ -1153,7 +1310,7 @@ int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* 
   else {
     static const int env_x = getenv("A3C_FC_XCD") ? atoi(getenv("A3C_FC_XCD")) : 0;
     const int mt = (int)((M + 15) / 16), ntiles = mt * (FC / 16);
-    const int xr = env_x && ntiles % 8 == 0;
+    const int xr = env_x == 2 ? (M % 128 == 0 ? 2 : 0) : (env_x && ntiles % 8 == 0);
     const dim3 grid = xr ? dim3((unsigned)ntiles) : dim3(FC / 16, (unsigned)mt);
     if (nw == 4)
       hipLaunchKernelGGL(k_fc_fwd<4>, grid, dim3(256), 0, s, A, W, bias, C, (int)M, xr);

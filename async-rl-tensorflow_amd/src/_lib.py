@@ -133,7 +133,7 @@ SIGNATURES = {
     'a3c_engine_time_kernel': (c_int, [c_void_p, c_int, c_int, c_void_p, ctypes.POINTER(c_float)]),
 }
 
-KER_CONV12_FWD, KER_FC_FWD, KER_ENV_STEP, KER_CONV_BWD, KER_HEAD_SCREEN, KER_HEAD_SCREEN_CONV12 = 0, 1, 2, 3, 4, 5
+KER_CONV12_FWD, KER_FC_FWD, KER_ENV_STEP, KER_CONV_BWD, KER_HEAD_SCREEN, KER_HEAD_SCREEN_CONV12, KER_FC_PART = 0, 1, 2, 3, 4, 5, 6
 
 _lib = None
 

@@ -401,6 +401,7 @@ int a3c_engine_slot_buffers(a3c_engine* eng, int slot, a3c_engine_buffers* out);
 #define A3C_KER_CONV_BWD 3     /* fused conv backward over B = n*E                       */
 #define A3C_KER_HEAD_SCREEN 4  /* fused head + action draw + Environment.screen, B = E    */
 #define A3C_KER_HEAD_SCREEN_CONV12 5  /* ... + conv1+conv2 of the next states (overlap mode) */
+#define A3C_KER_FC_PART 6      /* fc as K-slice partials (overlap mode; the head folds them)  */
 /* Live launch spans, recorded by the kernels themselves inside the engine's graphs (which 0:
  * k_conv_bwd, 1: k_head_screen_conv12): per launch, last workgroup end - first workgroup start
  * (s_memrealtime).  reset = 1 clears the records (before a timed region); otherwise returns the

@@ -165,6 +165,7 @@ def test_conv_fusion_is_bit_exact(overlap, monkeypatch):
     """k_head_screen_conv12 (step t+1's conv1 + conv2 inside step t's head + screen kernel) gives
     the same rollouts, activations and updates as the separate kernels, bit for bit."""
     engs = []
+    monkeypatch.setenv('A3C_FC_SPLIT', '0')     # the same fc kernel in both (see the next test)
     for fuse in ('0', '1'):
         monkeypatch.setenv('A3C_FUSE_CONV', fuse)
         engs.append(build('a3c', 6, 16, 5, 0, seed=13, overlap=overlap)[0])
@@ -175,6 +176,28 @@ def test_conv_fusion_is_bit_exact(overlap, monkeypatch):
     torch.cuda.synchronize()
     for name in ('params', 'ms', 'mom', 'frame_ring', 'loss', 'counters', 'actions', 'act_l1', 'act_l2', 'z'):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
+
+
+@pytest.mark.parametrize('E', [16, 256])
+def test_fc_split_matches_monolithic_fc(E, monkeypatch):
+    """Fused overlap rollout: the fc as K-slice partials (k_fc_part) folded by the head of
+    k_head_screen_conv12 equals the single-pass fc kernel up to fp32 summation order -- same
+    rollouts (actions, frames, rewards), layer outputs and updates to 1e-5."""
+    engs = []
+    for split in ('0', '1'):
+        monkeypatch.setenv('A3C_FC_SPLIT', split)
+        engs.append(build('a3c', 6, E, 5, 0, seed=21, overlap=True, frames=512)[0])
+    a, b = engs
+    for _ in range(4):
+        a.iterate()
+        b.iterate()
+    torch.cuda.synchronize()
+    for name in ('actions', 'frame_ring', 'counters'):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    for name in ('act_l3', 'z', 'params', 'ms', 'mom', 'loss'):
+        x, y = getattr(a, name).double(), getattr(b, name).double()
+        err = (x - y).norm() / max(y.norm().item(), 1e-30)
+        assert err < 1e-5, (name, float(err))
 
 
 def test_engine_bench_shape_runs():
