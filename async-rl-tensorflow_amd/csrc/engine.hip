@@ -511,7 +511,8 @@ static int enqueue_rollout_end(a3c_engine* e, const Slot& sl, hipStream_t s) {
     }
     int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, n, e->counters), E, nullptr, sl.scr_l2,
                                 sl.scr_l3, sl.z + e->nE * L.zs, none, s, L.lstm ? &ls : nullptr,
-                                conv_fused(e));   // s_n's convs ran in the last step's kernel
+                                conv_fused(e),   // s_n's convs ran in the last step's kernel
+                                nullptr, fc_split(e) ? e->fcpart : nullptr);
     return rc;
   }
   if (e->overlap) {

@@ -607,10 +607,29 @@ __global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, 
                                                   const float* __restrict__ Wp, const float* __restrict__ bp,
                                                   const float* __restrict__ Wv, const float* __restrict__ bv,
                                                   int A, int zs, float* __restrict__ z, HeadSelect sel) {
+  __shared__ __attribute__((aligned(16))) f32x4 l3s[4][64];
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
-  const float myz = head_row(h3, b, Wp, bp, Wv, bv, A, lane);
+  float myz;
+  if (sel.fc_part) {
+    // the fc as K-slice partials (k_fc_part): fold in slice order, + bias, ReLU, as the rollout
+    // kernel's head does, then the head reads the row from LDS
+    f32x4 fp[FC_NS];
+#pragma unroll
+    for (int w = 0; w < FC_NS; ++w) fp[w] = *(const f32x4*)(sel.fc_part + ((int64_t)w * B + b) * FC + 4 * lane);
+    const f32x4 fb = *(const f32x4*)(sel.fc_bias + 4 * lane);
+    f32x4 v = fp[0];
+#pragma unroll
+    for (int w = 1; w < FC_NS; ++w) v += fp[w];
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) v[c4] = fmaxf(v[c4] + fb[c4], 0.f);
+    l3s[threadIdx.x >> 6][lane] = v;
+    if (sel.l3_out) *(f32x4*)(sel.l3_out + b * FC + 4 * lane) = v;
+    myz = head_row((const float*)l3s[threadIdx.x >> 6], 0, Wp, bp, Wv, bv, A, lane);
+  } else {
+    myz = head_row(h3, b, Wp, bp, Wv, bv, A, lane);
+  }
   if (lane < zs) z[b * zs + lane] = myz;   // padding columns are 0
   if (sel.mode >= 0) (void)head_act(myz, lane, A, sel, b);
   if (sel.adv_ptr && blockIdx.x == 0 && threadIdx.x == 0) *sel.adv_ptr += sel.adv_n;   // (reads no tau)
@@ -754,15 +773,18 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   static_assert(NWF % PT == 0 && NWF * 16 <= HIST * PLANE, "old-plane conv1 weights in the x8 region");
   static_assert((HIST - 1) * PLANE * 2 <= 51 * 1024, "old planes as bf16 in the screen scratch");
   static_assert(PLANE * 2 <= HIST * PLANE, "new plane as bf16 in the x8 region");
-  // fc as K-slice partials (sel.fc_part): wave w's first load is slice w's partial row of env b,
-  // ahead of everything else it loads (vmcnt retires in order)
-  static_assert(FC_NS * 64 == 512, "one partial slice per wave");
+  // fc as K-slice partials (sel.fc_part), folded by wave 0 ahead of the head
   const int fwid = threadIdx.x >> 6, flane = threadIdx.x & 63;
   const bool fold = sel.fc_part != nullptr;
-  f32x4 fpart = {0.f, 0.f, 0.f, 0.f}, fbias = {0.f, 0.f, 0.f, 0.f};
-  if (fold) {
-    fpart = *(const f32x4*)(sel.fc_part + ((int64_t)fwid * gridDim.x + b) * FC + 4 * flane);
-    if (fwid == 0) fbias = *(const f32x4*)(sel.fc_bias + 4 * flane);
+  f32x4 fbias = {0.f, 0.f, 0.f, 0.f};
+  // wave 0 loads all FC_NS partial rows itself: no workgroup barrier before the head (each wave
+  // loading one slice and meeting in LDS measured 4.10M vs 4.23M env-steps/s)
+  f32x4 fpart[FC_NS];
+  if (fold && fwid == 0) {
+#pragma unroll
+    for (int w = 0; w < FC_NS; ++w)
+      fpart[w] = *(const f32x4*)(sel.fc_part + ((int64_t)w * gridDim.x + b) * FC + 4 * flane);
+    fbias = *(const f32x4*)(sel.fc_bias + 4 * flane);
   }
   const int pt = (int)threadIdx.x - 128;
   uint4 pv[PER3], wv[PERW];
@@ -781,21 +803,19 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   }
   const float* hrow = nullptr;
   if (fold) {
-    // fold the FC_NS slices in slice order, + bias, ReLU (wave 0; LDS [0, 9 KB) is free until
-    // head_act_env's barrier); the row also goes to l3_out for the backward
+    // fold the FC_NS slices in slice order, + bias, ReLU; the row goes to LDS [0, 1 KB) (free
+    // until head_act_env's barrier) for the head, and to l3_out for the backward
     f32x4* fl = (f32x4*)smem;
-    fl[fwid * 64 + flane] = fpart;
-    lds_only_barrier();
     if (fwid == 0) {
-      f32x4 v = fl[flane];
+      f32x4 v = fpart[0];
 #pragma unroll
-      for (int w = 1; w < FC_NS; ++w) v += fl[w * 64 + flane];
+      for (int w = 1; w < FC_NS; ++w) v += fpart[w];
 #pragma unroll
       for (int c4 = 0; c4 < 4; ++c4) v[c4] = fmaxf(v[c4] + fbias[c4], 0.f);
-      fl[FC_NS * 64 + flane] = v;
+      fl[flane] = v;
       *(f32x4*)(sel.l3_out + b * FC + 4 * flane) = v;
     }
-    hrow = (const float*)(fl + FC_NS * 64);
+    hrow = (const float*)fl;
   }
   const int32_t frame = head_act_env(h3, Wp, bp, Wv, bv, A, zs, z, sel, b, tau, dbg, hrow);
   uint16_t* xold = (uint16_t*)smem;                      // planes 0..2, bf16
@@ -883,7 +903,8 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
     if (rc0) return rc0;
   }
   // fused overlap rollout: the fc as K-slice partials, folded by the head of k_head_screen_conv12
-  const bool part = fc_part && next && !ls && sel.mode >= 0 && sel.env_on && sel.ring;
+  // (and the bootstrap state's, folded by k_head_fwd)
+  const bool part = fc_part && !ls && (next ? sel.mode >= 0 && sel.env_on && sel.ring : sel.mode < 0);
   int rc = part ? a3c_fc_part_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), fc_part, B, s)
                 : a3c_fc_fwd_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), P + L.off[T_FCB], act_l3, B, s,
                                     P + L.off[T_FCW]);
@@ -908,9 +929,16 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
   if (next) return a3c_set_error(A3C_ERR_INVALID, "a3c_forward", "conv fusion needs the fused env screen");
   if (sel.mode >= 0 && sel.env_on && sel.ring)
     return a3c_head_screen_launch(L, P, head_in, B, z, sel, s);
-  else
+  else {
+    HeadSelect hs = sel;
+    if (part) {
+      hs.fc_part = fc_part;
+      hs.fc_bias = P + L.off[T_FCB];
+      hs.l3_out = act_l3;
+    }
     hipLaunchKernelGGL(k_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, head_in, B,
-                       P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel);
+                       P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, hs);
+  }
   A3C_CHECK(hipGetLastError());
   return 0;
 }
