@@ -141,3 +141,19 @@ __device__ inline void st_act(T* p, T v) {
   *p = v;
 #endif
 }
+
+// sum_{s < n} p[s * stride], accumulated in s order (bit-identical to the plain loop) with 8 loads in
+// flight: the deterministic slab folds would otherwise wait one full load latency per term
+__device__ inline float sum_strided(const float* __restrict__ p, int n, int64_t stride) {
+  float v = 0.f;
+  int s = 0;
+  for (; s + 8 <= n; s += 8) {
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = p[(int64_t)(s + j) * stride];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v += t[j];
+  }
+  for (; s < n; ++s) v += p[(int64_t)s * stride];
+  return v;
+}

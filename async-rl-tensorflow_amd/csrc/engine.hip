@@ -633,15 +633,12 @@ static int enqueue_rollout_grad(a3c_engine* e, hipStream_t s) {
 static int enqueue_apply(a3c_engine* e, int snap, hipStream_t s) {
   OptParams op = opt_params(e);
   op.mode = e->cfg.world_size > 1 ? OPT_APPLY : (OPT_CLIP | OPT_APPLY);
+  // overlap: the same pass writes the parameter snapshot of the rollout that will use slot `snap`
+  if (e->overlap) op.snap = e->slot[snap].P;
   int rc = a3c_apply_launch(e->params, e->ms, e->mom, e->grads, e->tt, op, e->opt_part,
                             e->cfg.world_size > 1 ? nullptr : e->sumsq, s);
-  if (rc || !e->overlap) {
-    mark(3, s);
-    return rc;
-  }
-  A3C_CHECK(hipMemcpyAsync(e->slot[snap].P, e->params, e->L.total * 4, hipMemcpyDeviceToDevice, s));
   mark(3, s);
-  return 0;
+  return rc;
 }
 
 // Graph gi (see NGRAPH) is captured on first use (what: 0 rollout+grad, 1 rollout, 2 grad,

@@ -117,8 +117,7 @@ __global__ void k_reduce_slabs(const float* __restrict__ slab, int nsplit, int M
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t total = (int64_t)M * N;
   if (i >= total) return;
-  float v = 0.f;
-  for (int s = 0; s < nsplit; ++s) v += slab[(int64_t)s * total + i];
+  float v = sum_strided(slab + i, nsplit, total);
   int row = (int)(i / N), col = (int)(i - (int64_t)row * N);
   if (epi == EPI_BIAS_RELU) v = fmaxf(v + bias[col], 0.f);
   else if (epi == EPI_BIAS) v = v + bias[col];

@@ -526,9 +526,7 @@ __global__ void __launch_bounds__(256) k_slab_group(const float* __restrict__ sr
   if (i >= len) return;
   const int g = blockIdx.y;
   const int s0 = g * per, s1 = min(nsplit, s0 + per);
-  float v = 0.f;
-  for (int s = s0; s < s1; ++s) v += src[(int64_t)s * len + i];
-  dst[(int64_t)g * len + i] = v;
+  dst[(int64_t)g * len + i] = sum_strided(src + (int64_t)s0 * len + i, s1 - s0, len);
 }
 
 __device__ void loss_reduce_block(const float* __restrict__ terms, int64_t B, float* __restrict__ out) {
@@ -561,9 +559,7 @@ __global__ void __launch_bounds__(256) k_finalize(FinalizeSegs fs, const float* 
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int r = (int)(i / sg.ncols), c = (int)(i - (int64_t)r * sg.ncols);
     const float* src = sg.src + (int64_t)r * sg.src_ld + sg.col0 + c;
-    float v = 0.f;
-    for (int s = 0; s < sg.nsplit; ++s) v += src[(int64_t)s * sg.split_stride];
-    fs.dst[sg.dst_off + (int64_t)r * sg.dst_ld + c] = v * sg.scale;
+    fs.dst[sg.dst_off + (int64_t)r * sg.dst_ld + c] = sum_strided(src, sg.nsplit, sg.split_stride) * sg.scale;
   }
 }
 

@@ -30,6 +30,7 @@ struct OptParams {
   int64_t max_step;
   int64_t target_period;  // 0: no target network
   float* target;          // apply: params also written here when sched[1] != 0
+  float* snap;            // apply (nullable): the new params also written here (overlap snapshot)
   int64_t* counters;      // apply: block 0 advances counters[0] += dtau, counters[1] += step_add
   int64_t dtau;
   float rho, momentum, eps;

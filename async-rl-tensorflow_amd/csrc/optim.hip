@@ -137,6 +137,7 @@ __global__ void __launch_bounds__(256) k_apply(float* __restrict__ w, float* __r
       *(f32x4*)(mom + i) = mo;
       *(f32x4*)(w + i) = wv;
       if (copy) *(f32x4*)(op.target + i) = wv;
+      if (op.snap) *(f32x4*)(op.snap + i) = wv;
     } else {
       *(f32x4*)(grads + i) = g;
     }
