@@ -575,10 +575,11 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   // of the CUs, so that each CU keeps LDS for a concurrent rollout workgroup (conv12's 60 KB u8
   // variant, head_screen's 54 KB).  Measured on MI355X (Pong, 256 envs): 3.70M env-steps/s vs
   // 3.45M with 448 two-per-CU workgroups (those alone are faster, 92 vs 132 us, but leave no LDS
-  // for the rollout).  The slab workspace is sized for the larger count, so the plan's offsets
-  // do not depend on the mode.
+  // for the rollout).  Round 2, with the partial fc: 192 (-> 183 workgroups of 7 samples at
+  // n*E = 1280) 4.37M env-steps/s vs 4.29M for 224 (214 x 6), 4.14M for 160 (160 x 8), 4.00M for 256.
+  // The slab workspace is sized for the larger count, so the plan's offsets do not depend on the mode.
   static const int env_nwg = getenv("A3C_CB_NWG") ? atoi(getenv("A3C_CB_NWG")) : 0;
-  const int nwg_shared = env_nwg ? env_nwg : 224, nwg_own = env_nwg ? env_nwg : 256;
+  const int nwg_shared = env_nwg ? env_nwg : 192, nwg_own = env_nwg ? env_nwg : 256;
   auto count = [&](int nwg_max, int& per) {
     int nwg = (int)(B < nwg_max ? B : nwg_max);
     if (nwg < 1) nwg = 1;
