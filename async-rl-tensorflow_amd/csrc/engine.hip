@@ -90,6 +90,12 @@ struct a3c_engine {
   hipStream_t gs;          // backward side stream (weight-gradient GEMMs beside the conv backward)
   hipEvent_t ev_gfork, ev_gjoin;
   hipEvent_t ev_start, ev_roll[2];
+  // cross-stream ordering by stream memory operations (hipStreamWriteValue32 / WaitValue32 on
+  // monotonic counters in device memory) instead of events: measured 3.6 us per hop against
+  // 12-40 us for hipEventRecord + hipStreamWaitEvent (tools/waitvalue_probe.py)
+  int wait_value;
+  uint32_t* xflags;        // [0]: caller-stream sequence, [1]: rollout-stream sequence
+  uint32_t s_seq, r_seq, roll_seq[2];
   // external (host) envs: the host steps the envs between ext_act and ext_observe
   int ext;                 // cfg.external_env
   int ext_t;               // next rollout step (0..n; n: ready for rollout_grad)
@@ -216,6 +222,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   ALLOC(e->pool, (int64_t)e->cfg.num_frames * SCREEN_H * SCREEN_W * 3);
   ALLOC(e->ext_idx, E * 4);
   ALLOC(e->counters, 64);
+  ALLOC(e->xflags, 64);
   ALLOC(e->env.episode, 2 * E * 4);
   ALLOC(e->env.ep_step, 2 * E * 4);
   ALLOC(e->env.ep_len, 2 * E * 4);
@@ -297,6 +304,8 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
               hipEventCreateWithFlags(&e->ev_start, hipEventDisableTiming) == hipSuccess;
     for (int k = 0; k < 2 && ok; ++k)
       ok = hipEventCreateWithFlags(&e->ev_roll[k], hipEventDisableTiming) == hipSuccess;
+    e->wait_value = 1;
+    if (const char* v = getenv("A3C_WAIT_VALUE")) e->wait_value = atoi(v) != 0;
     if (!ok) {
       a3c_engine_destroy(e);
       return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "stream/event creation failed");
@@ -712,6 +721,10 @@ extern "C" int a3c_engine_reset(a3c_engine* e, const float* host_params, void* s
       A3C_CHECK(hipMemsetAsync(e->slot[k].lc, 0, (size_t)e->nE * LSTM_U * 4, s));
       A3C_CHECK(hipMemsetAsync(e->slot[k].terms, 0, (size_t)e->nE, s));
     }
+  A3C_CHECK(hipMemsetAsync(e->xflags, 0, 64, s));
+  A3C_CHECK(hipStreamSynchronize(s));
+  e->s_seq = e->r_seq = 0;
+  e->roll_seq[0] = e->roll_seq[1] = 0;
   e->iter = 0;
   e->grad_ready = false;
   e->grad_applied = false;
@@ -747,11 +760,21 @@ static int rollout_grad(a3c_engine* e, hipStream_t s, bool fused) {
   // the caller's stream once that rollout is complete.
   const int p = (int)(e->iter & 1);
   const Slot& sl = e->slot[p];
-  A3C_CHECK(hipEventRecord(e->ev_start, s));
-  A3C_CHECK(hipStreamWaitEvent(e->rs, e->ev_start, 0));
+  if (e->wait_value) {
+    A3C_CHECK(hipStreamWriteValue32(s, e->xflags, ++e->s_seq, 0));
+    A3C_CHECK(hipStreamWaitValue32(e->rs, e->xflags, e->s_seq, hipStreamWaitValueGte, 0xffffffffu));
+  } else {
+    A3C_CHECK(hipEventRecord(e->ev_start, s));
+    A3C_CHECK(hipStreamWaitEvent(e->rs, e->ev_start, 0));
+  }
   int rc = run_graph(e, 1 + p, 1, p, e->rs);   // (its prep kernel snapshots tau into sl.tau)
   if (rc) return rc;
-  A3C_CHECK(hipEventRecord(e->ev_roll[p], e->rs));
+  if (e->wait_value) {
+    A3C_CHECK(hipStreamWriteValue32(e->rs, e->xflags + 1, ++e->r_seq, 0));
+    e->roll_seq[p] = e->r_seq;
+  } else {
+    A3C_CHECK(hipEventRecord(e->ev_roll[p], e->rs));
+  }
   e->grad_ready = false;
 #ifdef A3C_MARKERS
   static const bool abl_bwd = getenv("A3C_ABL_BWD") != nullptr;   // measurement only: rollouts alone
@@ -761,7 +784,10 @@ static int rollout_grad(a3c_engine* e, hipStream_t s, bool fused) {
   }
 #endif
   if (e->iter >= 1) {
-    A3C_CHECK(hipStreamWaitEvent(s, e->ev_roll[p ^ 1], 0));
+    if (e->wait_value)
+      A3C_CHECK(hipStreamWaitValue32(s, e->xflags + 1, e->roll_seq[p ^ 1], hipStreamWaitValueGte, 0xffffffffu));
+    else
+      A3C_CHECK(hipStreamWaitEvent(s, e->ev_roll[p ^ 1], 0));
     rc = fused ? run_graph(e, 6 + (p ^ 1), 3, p ^ 1, s) : run_graph(e, 3 + (p ^ 1), 2, p ^ 1, s);
     if (rc) return rc;
     e->grad_ready = true;
