@@ -21,9 +21,15 @@ struct GemmArgs {
   int nsplit;                 // requested split (effective split may be smaller)
   int kchunk;                 // set by a3c_gemm
   float* colsum;              // optional [nsplit_eff][N] column sums of B over each K-chunk
+  int defer_reduce;           // a3c_gemm: leave the split-K fold to the caller (a3c_gemm_reduce)
 };
 
 int a3c_gemm(bool a_kcontig, bool b_ncontig, GemmArgs g, hipStream_t s);
+// three independent GEMMs in one launch: g0, g1 with (A k-strided, B n-contiguous), g2 with (A
+// k-contiguous, B k-contiguous).  The split-K folds are left to the caller (a3c_gemm_reduce, with
+// the arguments as updated here: effective split, K chunk)
+int a3c_gemm3(GemmArgs& g0, GemmArgs& g1, GemmArgs& g2, hipStream_t s);
+int a3c_gemm_reduce(const GemmArgs& g, hipStream_t s);
 int a3c_gemm_plan_split(int M, int N, int K, int target_blocks);
 
 inline int a3c_gemm_effective_split(int K, int nsplit) {

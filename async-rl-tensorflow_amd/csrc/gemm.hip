@@ -13,17 +13,17 @@
 #define BK 16
 #define PAD 4
 
+// one 64x64 output tile (bx, by) over K-chunk bz of C = A B (the block body of k_gemm_f32)
 template <bool A_KC, bool B_NC>
-__global__ void __launch_bounds__(256) k_gemm_f32(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) float As[BK][BM + PAD];
-  __shared__ __attribute__((aligned(16))) float Bs[BK][BN + PAD];
+__device__ inline void gemm_tile(const GemmArgs& g, int bx, int by, int bz, float (&As)[BK][BM + PAD],
+                                 float (&Bs)[BK][BN + PAD]) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int ks = blockIdx.z;
+  const int m0 = by * BM, n0 = bx * BN;
+  const int ks = bz;
   const int kbeg = ks * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
-  const bool do_colsum = g.colsum != nullptr && blockIdx.y == 0;
+  const bool do_colsum = g.colsum != nullptr && by == 0;
 
   // per-thread load coordinates
   int a_r, a_c, b_r, b_c;
@@ -109,6 +109,35 @@ __global__ void __launch_bounds__(256) k_gemm_f32(GemmArgs g) {
   if (do_colsum && tid < BN && n0 + tid < g.N) g.colsum[(int64_t)ks * g.N + n0 + tid] = csum;
 }
 
+// tile number id of g's (N tiles, M tiles, K-chunks) grid, N fastest (as k_gemm_f32's blockIdx)
+template <bool A_KC, bool B_NC>
+__device__ inline void gemm_tile_id(const GemmArgs& g, int id, float (&As)[BK][BM + PAD], float (&Bs)[BK][BN + PAD]) {
+  const int gx = (g.N + BN - 1) / BN, gy = (g.M + BM - 1) / BM;
+  gemm_tile<A_KC, B_NC>(g, id % gx, (id / gx) % gy, id / (gx * gy), As, Bs);
+}
+
+template <bool A_KC, bool B_NC>
+__global__ void __launch_bounds__(256) k_gemm_f32(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) float As[BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[BK][BN + PAD];
+  gemm_tile<A_KC, B_NC>(g, blockIdx.x, blockIdx.y, blockIdx.z, As, Bs);
+}
+
+// Several independent GEMMs in one launch (the backward's dW_head, dW_fc and dl2 all need only
+// dz / dl3): workgroup ids [0, nb[0]) are GEMM 0's tiles, then GEMM 1's, then GEMM 2's -- one
+// kernel boundary instead of three and one fill/drain tail.  Flavours: (A k-contiguous, B
+// n-contiguous) = (false, true), (false, true), (true, false).
+__global__ void __launch_bounds__(256) k_gemm_multi(GemmArgs g0, GemmArgs g1, GemmArgs g2, int nb0, int nb1) {
+  __shared__ __attribute__((aligned(16))) float As[BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[BK][BN + PAD];
+  // (each branch names its own kernel argument: selecting a pointer to one would copy all three
+  // to scratch)
+  const int id = blockIdx.x;
+  if (id < nb0) gemm_tile_id<false, true>(g0, id, As, Bs);
+  else if (id < nb0 + nb1) gemm_tile_id<false, true>(g1, id - nb0, As, Bs);
+  else gemm_tile_id<true, false>(g2, id - nb0 - nb1, As, Bs);
+}
+
 // dst[row*ldc + col] = epi(scale * sum_s slab[s][row][col])
 __global__ void k_reduce_slabs(const float* __restrict__ slab, int nsplit, int M, int N,
                                float* __restrict__ C, int64_t ldc, int epi,
@@ -135,28 +164,59 @@ int a3c_gemm_plan_split(int M, int N, int K, int target_blocks) {
   return split;
 }
 
-int a3c_gemm(bool a_kc, bool b_nc, GemmArgs g, hipStream_t s) {
-  if (g.M <= 0 || g.N <= 0) return 0;
+// shared by a3c_gemm and a3c_gemm3: alignment checks, effective split, K-chunk
+static int gemm_setup(bool a_kc, bool b_nc, GemmArgs& g) {
   if (((a_kc || !b_nc) && (g.K & 3)) || (g.lda & 3) || (g.ldb & 3) ||
       (((uintptr_t)g.A | (uintptr_t)g.B) & 15) || (a_kc ? 0 : (g.M & 3)) || (b_nc ? (g.N & 3) : 0))
     return a3c_set_error(A3C_ERR_INVALID, "a3c_gemm", "unaligned operands (need 16-B alignment, dims %4)");
   if (g.nsplit < 1) g.nsplit = 1;
-  int ktiles = (g.K + BK - 1) / BK;
-  int per = (ktiles + g.nsplit - 1) / g.nsplit;
+  const int ktiles = (g.K + BK - 1) / BK;
+  const int per = (ktiles + g.nsplit - 1) / g.nsplit;
   g.kchunk = per * BK;
   g.nsplit = (ktiles + per - 1) / per;
   if (g.nsplit > 1 && !g.slab) return a3c_set_error(A3C_ERR_INVALID, "a3c_gemm", "split-K needs a slab");
+  return 0;
+}
+
+static void gemm_reduce(const GemmArgs& g, hipStream_t s) {
+  const int64_t total = (int64_t)g.M * g.N;
+  hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                     g.slab, g.nsplit, g.M, g.N, g.C, g.ldc, g.epi, g.bias, g.mask, g.ldm);
+}
+
+int a3c_gemm3(GemmArgs& g0, GemmArgs& g1, GemmArgs& g2, hipStream_t s) {
+  if (g0.M <= 0 || g0.N <= 0 || g1.M <= 0 || g1.N <= 0 || g2.M <= 0 || g2.N <= 0)
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_gemm3", "empty GEMM");
+  int rc = gemm_setup(false, true, g0);
+  if (!rc) rc = gemm_setup(false, true, g1);
+  if (!rc) rc = gemm_setup(true, false, g2);
+  if (rc) return rc;
+  auto blocks = [](const GemmArgs& g) {
+    return ((g.N + BN - 1) / BN) * ((g.M + BM - 1) / BM) * g.nsplit;
+  };
+  const int nb0 = blocks(g0), nb1 = blocks(g1), nb2 = blocks(g2);
+  hipLaunchKernelGGL(k_gemm_multi, dim3((unsigned)(nb0 + nb1 + nb2)), dim3(256), 0, s, g0, g1, g2, nb0, nb1);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+int a3c_gemm_reduce(const GemmArgs& g, hipStream_t s) {
+  if (g.nsplit > 1) {
+    gemm_reduce(g, s);
+    A3C_CHECK(hipGetLastError());
+  }
+  return 0;
+}
+
+int a3c_gemm(bool a_kc, bool b_nc, GemmArgs g, hipStream_t s) {
+  if (g.M <= 0 || g.N <= 0) return 0;
+  int rc = gemm_setup(a_kc, b_nc, g);
+  if (rc) return rc;
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, g.nsplit);
   if (a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32<true, true>), grid, dim3(256), 0, s, g);
   else if (a_kc && !b_nc) hipLaunchKernelGGL((k_gemm_f32<true, false>), grid, dim3(256), 0, s, g);
   else if (!a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32<false, true>), grid, dim3(256), 0, s, g);
   else hipLaunchKernelGGL((k_gemm_f32<false, false>), grid, dim3(256), 0, s, g);
   A3C_CHECK(hipGetLastError());
-  if (g.nsplit > 1) {
-    int64_t total = (int64_t)g.M * g.N;
-    hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                       g.slab, g.nsplit, g.M, g.N, g.C, g.ldc, g.epi, g.bias, g.mask, g.ldm);
-    A3C_CHECK(hipGetLastError());
-  }
-  return 0;
+  return g.defer_reduce ? 0 : a3c_gemm_reduce(g, s);
 }

@@ -650,39 +650,62 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     A3C_CHECK(hipStreamWaitEvent(side, ev_fork, 0));
   }
   // head weights: dWh[256][zs] = l3^T dz ; dbh = colsum(dz)
-  GemmArgs g = {};
-  g.A = head_in; g.lda = FC;         // A(m=feature, k=b) = l3[b][m]  (m contiguous)
-  g.B = dz; g.ldb = L.zs;            // B(k=b, n=j) = dz[b][j]
-  g.C = ws + p.hgrad; g.ldc = L.zs;
-  g.M = FC; g.N = L.zs; g.K = (int)B;
-  g.epi = EPI_STORE; g.slab = ws + p.hslab; g.nsplit = p.head_split; g.colsum = ws + p.hcol;
-  int rc = a3c_gemm(false, true, g, ws_s);
-  if (rc) return rc;
-
+  GemmArgs gh = {};
+  gh.A = head_in; gh.lda = FC;       // A(m=feature, k=b) = l3[b][m]  (m contiguous)
+  gh.B = dz; gh.ldb = L.zs;          // B(k=b, n=j) = dz[b][j]
+  gh.C = ws + p.hgrad; gh.ldc = L.zs;
+  gh.M = FC; gh.N = L.zs; gh.K = (int)B;
+  gh.epi = EPI_STORE; gh.slab = ws + p.hslab; gh.nsplit = p.head_split; gh.colsum = ws + p.hcol;
   // fc weights: dW[2592][256] = l2^T dl3 -> grads directly ; db = colsum(dl3)
-  g = GemmArgs{};
-  g.A = act_l2; g.lda = FLAT;
-  g.B = dh3; g.ldb = FC;
-  g.C = grads + L.off[T_FCW]; g.ldc = FC;
-  g.M = FLAT; g.N = FC; g.K = (int)B;
-  g.epi = EPI_STORE; g.slab = ws + p.fcslab; g.nsplit = p.fc_split; g.colsum = ws + p.fccol;
-  rc = a3c_gemm(false, true, g, ws_s);
-  if (rc) return rc;
-
-  if (fork) A3C_CHECK(hipEventRecord(ev_join, side));
-
+  GemmArgs gf = {};
+  gf.A = act_l2; gf.lda = FLAT;
+  gf.B = dh3; gf.ldb = FC;
+  gf.C = grads + L.off[T_FCW]; gf.ldc = FC;
+  gf.M = FLAT; gf.N = FC; gf.K = (int)B;
+  gf.epi = EPI_STORE; gf.slab = ws + p.fcslab; gf.nsplit = p.fc_split; gf.colsum = ws + p.fccol;
   // dl2[B][2592] = (dl3 W^T) * (l2 > 0)
-  g = GemmArgs{};
-  g.A = dh3; g.lda = FC;                 // A(m=b, k) = dl3[b][k]
-  g.B = P + L.off[T_FCW]; g.ldb = FC;    // B(k, n) = W[n][k]
-  g.C = dl2; g.ldc = FLAT;
-  g.M = (int)B; g.N = FLAT; g.K = FC;
-  g.epi = EPI_MASK; g.mask = act_l2; g.ldm = FLAT; g.nsplit = 1;
-  rc = a3c_gemm(true, false, g, s);
-  if (rc) return rc;
-
-  rc = a3c_conv_bwd_launch(L, P, sa, B, act_l1, dl2, ws, s);
-  if (rc) return rc;
+  GemmArgs gd = {};
+  gd.A = dh3; gd.lda = FC;               // A(m=b, k) = dl3[b][k]
+  gd.B = P + L.off[T_FCW]; gd.ldb = FC;  // B(k, n) = W[n][k]
+  gd.C = dl2; gd.ldc = FLAT;
+  gd.M = (int)B; gd.N = FLAT; gd.K = FC;
+  gd.epi = EPI_MASK; gd.mask = act_l2; gd.ldm = FLAT; gd.nsplit = 1;
+  int rc;
+  // sync mode: the three GEMMs in one launch (3.32M -> 3.41M env-steps/s); overlapped with the
+  // next rollout the 1,420-workgroup launch slows it more than it gains (4.40M -> 4.30M), and so
+  // do the folds moved behind the conv backward alone (A3C_FOLD_LATE: 4.36M -> 3.73M)
+  static const int env_multi = getenv("A3C_GEMM_MULTI") ? atoi(getenv("A3C_GEMM_MULTI")) : -1;
+  static const int env_late = getenv("A3C_FOLD_LATE") ? atoi(getenv("A3C_FOLD_LATE")) : -1;
+  const bool multi = env_multi >= 0 ? env_multi != 0 : !a3c_shared_gpu();
+  const bool late = env_late >= 0 ? env_late != 0 : multi;
+  if (!fork && (multi || late)) {
+    // the weight-gradient split-K folds go after the conv backward (only the clip / apply read
+    // them), so nothing but dl2 stands between the head and the conv
+    if (multi) {
+      rc = a3c_gemm3(gh, gf, gd, s);
+    } else {
+      gh.defer_reduce = gf.defer_reduce = 1;
+      rc = a3c_gemm(false, true, gh, s);
+      if (!rc) rc = a3c_gemm(false, true, gf, s);
+      if (!rc) rc = a3c_gemm(true, false, gd, s);
+    }
+    if (rc) return rc;
+    rc = a3c_conv_bwd_launch(L, P, sa, B, act_l1, dl2, ws, s);
+    if (rc) return rc;
+    rc = a3c_gemm_reduce(gh, s);
+    if (!rc) rc = a3c_gemm_reduce(gf, s);
+    if (rc) return rc;
+  } else {
+    rc = a3c_gemm(false, true, gh, ws_s);
+    if (rc) return rc;
+    rc = a3c_gemm(false, true, gf, ws_s);
+    if (rc) return rc;
+    if (fork) A3C_CHECK(hipEventRecord(ev_join, side));
+    rc = a3c_gemm(true, false, gd, s);
+    if (rc) return rc;
+    rc = a3c_conv_bwd_launch(L, P, sa, B, act_l1, dl2, ws, s);
+    if (rc) return rc;
+  }
 
   FinalizeSegs fs = {};
   fs.dst = grads;
