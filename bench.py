@@ -222,11 +222,12 @@ def main():
             'k_fc_fwd': ('mfma', FC_FWD_FLOP * E),
         }
         if fused and os.environ.get('A3C_FC_SPLIT', '1') != '0' and not args.lstm:
-            # the rollout steps' fc runs as K-slice partials folded by the next head (k_fc_part);
-            # the bootstrap state's keeps the single-pass k_fc_fwd
+            # every fc of the rollout (n steps + the bootstrap state) runs as K-slice partials
+            # folded by the consuming head (k_fc_part): the single-pass k_fc_fwd is not launched
             ms['k_fc_part'] = eng.time_kernel(_lib.KER_FC_PART, 20)
-            count['k_fc_part'], count['k_fc_fwd'] = n, 1
+            count['k_fc_part'] = n + 1
             work['k_fc_part'] = ('mfma', FC_FWD_FLOP * E)
+            del ms['k_fc_fwd']
         if fused:
             ms['k_head_screen_conv12'] = eng.time_kernel(_lib.KER_HEAD_SCREEN_CONV12, 20)
             count['k_head_screen_conv12'] = n
