@@ -295,3 +295,18 @@ def test_overlap_stale_semantics_match_oracle():
             d = np.abs(P[name] - ref.params[name]).max()
             assert d <= 1e-5 * max(1.0, np.abs(ref.params[name]).max()), (k, name, d)
         assert int(eng.counters[1].item()) == ref.global_step
+
+def test_stream_ordering_modes_are_bit_identical(monkeypatch):
+    """Overlap pipeline: ordering the rollout and backward streams by stream wait-value operations
+    on device counters (default) or by HIP events gives the same training, bit for bit."""
+    engs = []
+    for wv in ('0', '1'):
+        monkeypatch.setenv('A3C_WAIT_VALUE', wv)
+        engs.append(build('a3c', 6, 32, 5, 0, seed=17, overlap=True, frames=256)[0])
+    a, b = engs
+    for _ in range(6):
+        a.iterate()
+        b.iterate()
+    torch.cuda.synchronize()
+    for name in ('params', 'ms', 'mom', 'frame_ring', 'loss', 'counters', 'actions', 'z'):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
