@@ -304,7 +304,9 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
               hipEventCreateWithFlags(&e->ev_start, hipEventDisableTiming) == hipSuccess;
     for (int k = 0; k < 2 && ok; ++k)
       ok = hipEventCreateWithFlags(&e->ev_roll[k], hipEventDisableTiming) == hipSuccess;
-    e->wait_value = 1;
+    // (one GPU: with an exchange the collectives' own stream synchronisation sits between the
+    // graphs, a combination the pool has not run on several GPUs -- events there)
+    e->wait_value = e->cfg.world_size == 1;
     if (const char* v = getenv("A3C_WAIT_VALUE")) e->wait_value = atoi(v) != 0;
     if (!ok) {
       a3c_engine_destroy(e);
