@@ -310,3 +310,18 @@ def test_stream_ordering_modes_are_bit_identical(monkeypatch):
     torch.cuda.synchronize()
     for name in ('params', 'ms', 'mom', 'frame_ring', 'loss', 'counters', 'actions', 'z'):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
+
+
+@pytest.mark.parametrize('overlap', [False, True])
+def test_bench_shape_is_deterministic(overlap):
+    """At the bench configuration (Pong, 256 envs, n=5) two engines from the same seed train bit for
+    bit alike: every reduction is fixed-order (slab folds, sum of squares), no atomics."""
+    engs = [build('a3c', 6, 256, 5, 0, seed=29, frames=512, scale=1.0, overlap=overlap)[0] for _ in range(2)]
+    for _ in range(4):
+        for e in engs:
+            e.iterate()
+    torch.cuda.synchronize()
+    a, b = engs
+    for name in ('params', 'ms', 'mom', 'frame_ring', 'loss', 'counters', 'actions', 'z', 'act_l3'):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert torch.isfinite(a.params).all() and torch.isfinite(a.loss).all()
