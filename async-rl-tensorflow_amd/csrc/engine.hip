@@ -64,6 +64,7 @@ struct a3c_engine {
   EnvParams envp;
   int overlap, nslot;
   int fused_screen;        // 1: screen kernel fused into the head (k_head_screen)
+  int frame84;             // cfg.frame84: pre-sized 84x84 pool frames (measurement mode M2)
   int fuse_conv;           // 1: step t+1's conv1 + conv2 fused into step t's head + screen
   unsigned long long* spans;  // [2][SPAN_RECS][2]: live launch spans of k_conv_bwd, k_head_screen_conv12
   Slot slot[2];
@@ -173,6 +174,8 @@ extern "C" int a3c_engine_destroy(a3c_engine* e) {
   return 0;
 }
 
+static int frame_bytes(const a3c_engine* e) { return e->frame84 ? PLANE : SCREEN_H * SCREEN_W * 3; }
+
 extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out) {
   if (!cfg || !out) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "null");
   *out = nullptr;
@@ -203,6 +206,11 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   if (const char* v = getenv("A3C_FUSE_CONV")) e->fuse_conv = atoi(v) != 0;
   e->fc_split = 1;
   if (const char* v = getenv("A3C_FC_SPLIT")) e->fc_split = atoi(v) != 0;
+  e->frame84 = cfg->frame84 ? 1 : 0;
+  if (e->frame84 && (e->ext || !e->fused_screen)) {   // the copy lives in the fused head kernels
+    delete e;
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "frame84 needs device envs and the fused screen");
+  }
   e->nslot = e->overlap ? 2 : 1;
   // ring: the states of one rollout (frames tau-3 .. tau+n); overlap keeps two rollouts' frames
   e->R = (e->overlap ? 2 * e->n : e->n) + HIST + (cfg->net.algo == A3C_ALGO_Q ? 1 : 0);
@@ -219,7 +227,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   ALLOC(e->mom, L.total * 4);
   ALLOC(e->grads, L.total * 4);
   ALLOC(e->ring, (int64_t)E * e->R * PLANE);
-  ALLOC(e->pool, (int64_t)e->cfg.num_frames * SCREEN_H * SCREEN_W * 3);
+  ALLOC(e->pool, (int64_t)e->cfg.num_frames * frame_bytes(e));
   ALLOC(e->ext_idx, E * 4);
   ALLOC(e->counters, 64);
   ALLOC(e->xflags, 64);
@@ -463,6 +471,7 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
       sel.pool = e->pool;
       sel.ring = e->ring;
       sel.R = e->R;
+      sel.frame84 = e->frame84;
     }
   }
   LstmStep ls = {};
@@ -709,9 +718,9 @@ extern "C" int a3c_engine_reset(a3c_engine* e, const float* host_params, void* s
   A3C_CHECK(hipMemsetAsync(e->loss, 0, 64, s));
   A3C_CHECK(hipMemsetAsync(e->ring, 0, (size_t)e->E * e->R * PLANE, s));
   if (!e->ext) {
-    rc = a3c_pool_fill_launch(e->pool, e->cfg.num_frames, e->k0, e->k1, s);
+    rc = a3c_pool_fill_launch(e->pool, e->cfg.num_frames, e->k0, e->k1, s, frame_bytes(e));
     if (rc) return rc;
-    rc = a3c_env_init_launch(e->envp, e->env, e->E, e->pool, e->ring, e->R, e->counters, s);
+    rc = a3c_env_init_launch(e->envp, e->env, e->E, e->pool, e->ring, e->R, e->counters, s, e->frame84);
     if (rc) return rc;
   }
   if (e->overlap)
@@ -1008,6 +1017,7 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
       case A3C_KER_FC_PART:
         return a3c_fc_part_launch(sl.act_l2, (const float*)(sl.prep + PREP_W1S_BYTES), e->fcpart, E, s);
       case A3C_KER_ENV_STEP:
+        if (e->frame84) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_time_kernel", "no screen kernel in frame84 mode");
         return a3c_env_screen_launch(E, sl.frames, e->pool, e->ring, e->R, e->counters, 0, s);
       case A3C_KER_HEAD_SCREEN:
       case A3C_KER_HEAD_SCREEN_CONV12: {
@@ -1025,6 +1035,7 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
         sel.rewards = sl.rewards; sel.terms = sl.terms;
         sel.frames_out = sl.frames;
         sel.pool = e->pool; sel.ring = e->ring; sel.R = e->R;
+        sel.frame84 = e->frame84;
         sel.frame_salt = salt;
         if (kernel == A3C_KER_HEAD_SCREEN)
           return a3c_head_screen_launch(L, e->params, L.lstm ? sl.lh : sl.act_l3, E, sl.z, sel, s);

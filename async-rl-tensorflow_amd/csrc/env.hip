@@ -62,8 +62,23 @@ __global__ void __launch_bounds__(256) k_env_screen(int E, const int32_t* __rest
                            ring + (int64_t)e * R * PLANE + ((tau + 1) % R) * PLANE, blockIdx.x, smem);
 }
 
-int a3c_pool_fill_launch(uint8_t* pool, int P, uint32_t k0, uint32_t k1, hipStream_t s) {
-  const int64_t cpf = (int64_t)SCREEN_H * SCREEN_W * 3 / 16;
+// mode M2 (pre-sized frames): frame f of the pool copied into all HIST ring slots of env e (grid E)
+__global__ void __launch_bounds__(256) k_env_init_copy84(EnvBufs b, int E, const uint8_t* __restrict__ pool,
+                                                         uint8_t* __restrict__ ring, int R) {
+  const int e = blockIdx.x;
+  const int32_t f = b.frame[(int64_t)((HIST - 1) & 1) * E + e];
+  const uint4* src = (const uint4*)(pool + (int64_t)f * PLANE);
+  uint8_t* base = ring + (int64_t)e * R * PLANE;
+  for (int i = threadIdx.x; i < PLANE / 16; i += blockDim.x) {
+    const uint4 v = src[i];
+    for (int c = 0; c < HIST; ++c) ((uint4*)(base + (int64_t)(c % R) * PLANE))[i] = v;
+  }
+}
+
+// frame f, 16-byte chunk j = philox(j, f, P_POOL, 0): frame_bytes = 210*160*3 (RGB frames) or
+// 84*84 (mode M2 -- the first 441 chunks of the same hash)
+int a3c_pool_fill_launch(uint8_t* pool, int P, uint32_t k0, uint32_t k1, hipStream_t s, int frame_bytes) {
+  const int64_t cpf = frame_bytes / 16;
   const int64_t total = cpf * P;
   hipLaunchKernelGGL(k_pool_fill, dim3(4096), dim3(256), 0, s, pool, cpf, total, k0, k1);
   A3C_CHECK(hipGetLastError());
@@ -71,10 +86,15 @@ int a3c_pool_fill_launch(uint8_t* pool, int P, uint32_t k0, uint32_t k1, hipStre
 }
 
 int a3c_env_init_launch(const EnvParams& p, const EnvBufs& b, int E, const uint8_t* pool, uint8_t* ring,
-                        int R, int64_t* counters, hipStream_t s) {
+                        int R, int64_t* counters, hipStream_t s, int frame84) {
   PreGeom g = a3c_make_geom(SCREEN_H, SCREEN_W, IMG_OUT, IMG_OUT);
   hipLaunchKernelGGL(k_env_init_state, dim3((E + 63) / 64), dim3(64), 0, s, p, b, E, counters);
   A3C_CHECK(hipGetLastError());
+  if (frame84) {
+    hipLaunchKernelGGL(k_env_init_copy84, dim3(E), dim3(256), 0, s, b, E, pool, ring, R);
+    A3C_CHECK(hipGetLastError());
+    return 0;
+  }
   hipLaunchKernelGGL(k_env_init_screens, dim3(g.parts, E), dim3(256), a3c_pre_smem_bytes(g), s, b, E, pool, ring, R, g);
   A3C_CHECK(hipGetLastError());
   return 0;

@@ -113,6 +113,7 @@ struct HeadSelect {
   const uint8_t* pool;
   uint8_t* ring;
   int R;
+  int frame84;              // 1: pool frames are pre-sized 84x84 screens (mode M2): a copy
   // measurement only (a3c_engine_time_kernel): offsets the post-act frame index so that every
   // timed launch streams a different set of frames from HBM, as the live rollout does; 0 in
   // every product launch

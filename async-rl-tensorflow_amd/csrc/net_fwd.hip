@@ -721,8 +721,11 @@ __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restr
   if (dbg && threadIdx.x == 0) dbg[0] = __builtin_readcyclecounter();
 #endif
   const int32_t frame = head_act_env(h3, Wp, bp, Wv, bv, A, zs, z, sel, b, tau, dbg);
-  atari::screen_frame<HS_THREADS>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3),
-                                  sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE, smem, dbg);
+  uint8_t* slot = sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE;
+  if (sel.frame84)
+    atari::copy_frame84<HS_THREADS>(sel.pool + (int64_t)frame * PLANE, slot);
+  else
+    atari::screen_frame<HS_THREADS>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3), slot, smem, dbg);
   WG_T1(z + b * zs);
 }
 
@@ -849,9 +852,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   };
   // plane 3 = the new screen: to the ring slot (tau + 1) % R and, as bf16, to the x8 region
   uint16_t* xnew = (uint16_t*)x8;
-  atari::screen_frame<512>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3),
-                           sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE, smem, dbg, xnew,
-                           conv1_old);
+  uint8_t* slot = sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE;
+  if (sel.frame84)
+    atari::copy_frame84<512>(sel.pool + (int64_t)frame * PLANE, slot, xnew, conv1_old);
+  else
+    atari::screen_frame<512>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3), slot, smem, dbg, xnew,
+                             conv1_old);
   if (dbg && threadIdx.x == 0) dbg[9] = __builtin_readcyclecounter();
   uint4 wn[6];
 #pragma unroll

@@ -294,6 +294,35 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
   }
 }
 
+// Measurement mode M2 (a3c_engine_config.frame84): the pool frame is already an 84x84 u8 screen,
+// so the "screen" is a copy into the ring slot (and, for the fused conv, the bf16 plane in LDS).
+// mid() runs while the loads are in flight, as in screen_frame.
+template <int NT, typename Mid = NoScreenMid>
+__device__ inline void copy_frame84(const uint8_t* __restrict__ src, uint8_t* __restrict__ out,
+                                    uint16_t* lds_bf16 = nullptr, Mid mid = Mid()) {
+  constexpr int NCH = OH * OW / 16;                     // 441 chunks of 16 pixels
+  constexpr int PER = (NCH + NT - 1) / NT;
+  const int tid = threadIdx.x;
+  uint4 v[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) v[j] = ((const uint4*)src)[min(tid + NT * j, NCH - 1)];
+  mid();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = tid + NT * j;
+    if (i < NCH) {
+      ((uint4*)out)[i] = v[j];
+      if (lds_bf16) {
+        uint4* d = (uint4*)(lds_bf16 + 16 * i);
+        const uint2 a0 = u8x4_to_bf16x4(v[j].x), a1 = u8x4_to_bf16x4(v[j].y);
+        const uint2 a2 = u8x4_to_bf16x4(v[j].z), a3 = u8x4_to_bf16x4(v[j].w);
+        d[0] = make_uint4(a0.x, a0.y, a1.x, a1.y);
+        d[1] = make_uint4(a2.x, a2.y, a3.x, a3.y);
+      }
+    }
+  }
+}
+
 template <int ROWS>
 struct Smem {
   static constexpr int SR = max_src_rows<ROWS>();

@@ -5,7 +5,7 @@
 #include <new>
 #include "env_dev.h"
 
-int a3c_pool_fill_launch(uint8_t* pool, int P, uint32_t k0, uint32_t k1, hipStream_t s);
+int a3c_pool_fill_launch(uint8_t* pool, int P, uint32_t k0, uint32_t k1, hipStream_t s, int frame_bytes);
 int a3c_launch_screen_atari(const uint8_t* rgb, const int32_t* idx, int64_t n, uint8_t* out, int64_t stride,
                             hipStream_t s);
 
@@ -87,7 +87,7 @@ extern "C" int a3c_env_create(int num_envs, int action_size, int start_lives, in
   v->p.random_start = random_start;
   v->p.action_repeat = action_repeat;
   v->p.env_id_base = env_id_base;
-  int rc = a3c_pool_fill_launch(v->pool, num_frames, v->p.k0, v->p.k1, nullptr);
+  int rc = a3c_pool_fill_launch(v->pool, num_frames, v->p.k0, v->p.k1, nullptr, SCREEN_H * SCREEN_W * 3);
   if (!rc) {
     hipLaunchKernelGGL(k_venv_zero, dim3((num_envs + 63) / 64), dim3(64), 0, nullptr, v->b, num_envs);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)

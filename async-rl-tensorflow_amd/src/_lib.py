@@ -39,7 +39,7 @@ class EngineConfig(ctypes.Structure):
                 ('clip_norm', c_float), ('literal_adv', c_int), ('ep_start', c_float),
                 ('ep_end', c_float), ('ep_end_t', c_i64), ('learn_start', c_i64),
                 ('target_q_update_step', c_i64), ('discount', c_double), ('overlap', c_int),
-                ('external_env', c_int)]
+                ('external_env', c_int), ('frame84', c_int)]
 
 
 class EngineBuffers(ctypes.Structure):

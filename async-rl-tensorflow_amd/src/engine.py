@@ -96,7 +96,9 @@ class Engine:
         self._slots = [self._slot_views(k) for k in range(2 if self.overlap else 1)]
         for k, v in self._slots[0].items():
             setattr(self, k, v)
-        self.frame_pool = _view(b.frame_pool, (int(cfg.num_frames), 210, 160, 3), torch.uint8)
+        self.frame84 = bool(cfg.frame84)
+        self.frame_pool = _view(b.frame_pool, (int(cfg.num_frames),) + ((84, 84) if self.frame84 else (210, 160, 3)),
+                                torch.uint8)
         # env state is double-buffered by step parity: the current state lives at tau & 1
         self._env = {'frame': _view(b.env_frame, (2, E), torch.int32),
                      'lives': _view(b.env_lives, (2, E), torch.int32),

@@ -32,6 +32,7 @@ CONV12_FWD_FLOP = 2 * 400 * 16 * 256 + 2 * 81 * 32 * 256            # 4,603,904
 CONV_BWD_FLOP = 2 * 81 * 32 * 256 * 2 + 2 * 400 * 16 * 256          # 5,931,008
 FC_FWD_FLOP = 2 * 2592 * 256                                        # 1,327,104
 ENV_STEP_BYTES = 210 * 160 * 3 + 84 * 84                            # 107,856
+ENV_STEP_BYTES_84 = 84 * 84 + 84 * 84                               # 14,112 (--frames84: copy)
 PEAK_FP32_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix peak (spec)
 PEAK_HBM_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 
@@ -53,6 +54,9 @@ def parse():
     ap.add_argument('--lstm', action='store_true',
                     help='C5 LSTM policy head (BASELINE config 5: SpaceInvaders-v0, 256-cell LSTM after the fc)')
     ap.add_argument('--frames', type=int, default=16384, help='HBM frame pool (16384 = 1.65 GB > L3)')
+    ap.add_argument('--frames84', action='store_true',
+                    help='measurement mode M2 (SURVEY 8(d)): the pool holds pre-sized 84x84 grey frames, the env '
+                         'step copies one into the history ring (no Environment.screen); default M1: raw RGB')
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--update', default='overlap', choices=['overlap', 'sync', 'hogwild'],
                     help='overlap: rollout k overlaps backward+apply of rollout k-1 (stale-1 async A3C); '
@@ -75,7 +79,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(seconds, game, algo):
+def cpu_baseline(seconds, game, algo, frame84=False):
     """The reference's ps/worker algorithm restated on the CPU (oracle/ps_worker.py: shared-memory
     PS, W worker processes with Hogwild RMSProp, one numpy thread each) on the same synthetic
     env: 1 ps / 1 worker (BASELINE config 1) and W = min(nproc - 1, 15) workers.  Runs before
@@ -85,13 +89,13 @@ def cpu_baseline(seconds, game, algo):
     n = 5 if algo == 'a3c' else 32
     W = max(1, min((os.cpu_count() or 2) - 1, 15))
     one = ps_worker.run(seconds=seconds / 2, workers=1, envs_per_worker=8, n_step=n, action_size=A, algo=algo,
-                        start_lives=lives)
+                        start_lives=lives, frame84=frame84)
     many = ps_worker.run(seconds=seconds / 2, workers=W, envs_per_worker=8, n_step=n, action_size=A, algo=algo,
-                         start_lives=lives) if W > 1 else one
+                         start_lives=lives, frame84=frame84) if W > 1 else one
     return dict(value=round(many['value'], 2), unit='env-steps/s', cores=W, kind='port',
                 one_worker=round(one['value'], 2),
                 sample=f'oracle/ps_worker.py ({algo} ps/worker, shared-memory PS, unlocked RMSProp, numpy fp32, '
-                       f'8 envs x n={n} per worker): {W} workers x {many["seconds"]:.1f} s = '
+                       f'8 envs x n={n} per worker{", pre-sized 84x84 frames" if frame84 else ""}): {W} workers x {many["seconds"]:.1f} s = '
                        f'{many["iterations"]} iterations; 1 ps/1 worker: {one["value"]:.1f} env-steps/s')
 
 
@@ -109,7 +113,7 @@ def main():
             raise SystemExit('--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)')
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds, args.game, args.algo)    # before any HIP initialisation
+        cpu = cpu_baseline(args.cpu_seconds, args.game, args.algo, args.frames84)    # before any HIP initialisation
     ndev = torch.cuda.device_count()
     torch.cuda.set_device(local % max(ndev, 1))
     if world > 1:
@@ -132,9 +136,11 @@ def main():
     host = args.env == 'host'
     if host and args.update != 'sync':
         args.update = 'sync'              # host-stepped envs drive a synchronous engine
+    if host and args.frames84:
+        raise SystemExit('--frames84 is a device-env pool mode')
     eng = Engine(num_envs=E, n_step=n, action_size=A, algo=args.algo, start_lives=lives, num_frames=args.frames,
                  seed=123, env_id_base=rank * E, world_size=world, use_graph=not args.no_graph,
-                 overlap=args.update == 'overlap', lstm=args.lstm, external_env=host)
+                 overlap=args.update == 'overlap', lstm=args.lstm, external_env=host, frame84=int(args.frames84))
     hpool = None
     if host:
         from src.host_env import SyntheticHostEnvPool
@@ -210,6 +216,7 @@ def main():
         # overlap mode fuses step t+1's conv1+conv2 into step t's head+screen kernel
         # (k_head_screen_conv12, engine.hip conv_fused): conv12 then runs once per rollout
         fused = args.update == 'overlap' and os.environ.get('A3C_FUSE_CONV', '1') != '0'
+        step_bytes = ENV_STEP_BYTES_84 if args.frames84 else ENV_STEP_BYTES
         ms = {
             'k_conv12_fwd': eng.time_kernel(_lib.KER_CONV12_FWD, 20),
             'k_conv_bwd': eng.time_kernel(_lib.KER_CONV_BWD, 10),
@@ -233,11 +240,11 @@ def main():
             count['k_head_screen_conv12'] = n
             # two serial phases per workgroup: Environment.screen (HBM) then conv1+conv2 (MFMA);
             # roofline time = bytes / HBM peak + FLOP / FP32 MFMA peak
-            work['k_head_screen_conv12'] = ('hbm+mfma', (ENV_STEP_BYTES * E, CONV12_FWD_FLOP * E))
+            work['k_head_screen_conv12'] = ('hbm+mfma', (step_bytes * E, CONV12_FWD_FLOP * E))
         else:
             ms['k_head_screen'] = eng.time_kernel(_lib.KER_HEAD_SCREEN, 20)
             count['k_head_screen'] = n
-            work['k_head_screen'] = ('hbm', ENV_STEP_BYTES * E)
+            work['k_head_screen'] = ('hbm', step_bytes * E)
         iter_ms = el / args.steps * 1e3
         # live = the average in-graph launch span over the timed region (contended in overlap
         # mode); avg_ms = the same kernel alone, back-to-back on the engine's buffers
@@ -274,7 +281,7 @@ def main():
         # (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 FETCH_SIZE correction per MI355X_MICROARCH.md
         traffic = None
         pmc = os.path.join(ROOT, 'profiles', 'pmc_hbm_bytes.json')
-        if os.path.exists(pmc):
+        if os.path.exists(pmc) and not args.frames84:    # (the committed passes profile mode M1)
             try:
                 t = json.load(open(pmc))['hbm_bytes_per_launch'].get(dom)
                 traffic = None if t is None else int(round(t))
@@ -299,14 +306,16 @@ def main():
             'metric': METRIC, 'value': round(steps_total / el, 1), 'unit': 'env-steps/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 4),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
-            'data': (f'synthetic: HBM-resident hashed RGB 210x160x3 frame pool ({args.frames} frames) stepped by '
-                     f'the on-device synthetic Atari env; random-init NIPS A3C conv net' if not host else
+            'data': (f'synthetic: HBM-resident hashed {"pre-sized 84x84 grey" if args.frames84 else "RGB 210x160x3"} '
+                     f'frame pool ({args.frames} frames) stepped by the on-device synthetic Atari env; random-init '
+                     f'NIPS A3C conv net' if not host else
                      f'synthetic: host-stepped emulator ({args.host_threads} threads, a3c_hostenv) writing raw RGB '
                      f'210x160x3 frames into pinned buffers, PCIe H2D every step (PCIe-inclusive); random-init '
                      f'NIPS A3C conv net'),
             'config': {'workload': f'{args.game}, {E} envs batched per MI355X, n-step={n}, '
                                    f'{"A3C" if args.algo == "a3c" else "one-step Q"} conv net (nips trunk'
                                    f'{" + 256-cell LSTM head" if args.lstm else ""})',
+                       'frames': 'M2: pre-sized 84x84 (copy)' if args.frames84 else 'M1: raw RGB 210x160x3 + screen',
                        'game': args.game, 'head': 'lstm' if args.lstm else 'feed-forward', 'env': args.env, 'envs_per_gpu': E, 'n_step': n, 'action_size': A, 'algo': args.algo,
                        'env_steps_per_step': world * E * n,
                        'parallelism': (f'dp{world} hogwild: unlocked RMSProp pushes into {world} IPC-mapped HBM '

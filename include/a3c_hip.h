@@ -285,6 +285,10 @@ typedef struct a3c_engine_config {
                         SURVEY §8(f)1): a3c_engine_ext_* below feed their RGB frames,
                         rewards and terminals each step; no synthetic env, no frame pool
                         (num_frames ignored).  Synchronous engines only.                 */
+  int frame84;        /* 1: measurement mode M2: the pool holds pre-sized 84x84
+                        grey frames (the north star's synthetic 84x84x4 states), so the env
+                        step's Environment.screen becomes a 7 KB copy into the history ring.
+                        0 (default, M1): raw 210x160x3 RGB frames, screen computed on device. */
 } a3c_engine_config;
 
 void a3c_engine_config_default(a3c_engine_config* cfg);

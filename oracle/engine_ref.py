@@ -13,7 +13,7 @@ import numpy as np
 
 from . import philox as px
 from . import ref_cpu as R
-from .synthetic_env import SyntheticAtari, pool_frame
+from .synthetic_env import SyntheticAtari, pool_frame, pool_frame84
 
 EP_END_CHOICES = np.array([0.1, 0.01, 0.5], np.float32)   # main.py:68
 
@@ -24,7 +24,7 @@ class EngineRef:
                  gamma=0.99, beta=0.01, learning_rate=0.0007, max_step=80_000_000, decay=0.99,
                  momentum=0.0, epsilon=0.1, clip_norm=40.0, literal_adv=False, ep_start=1.0,
                  ep_end_t=4_000_000, learn_start=32, target_q_update_step=40_000, discount=0.99,
-                 dtype=np.float64, lstm=False):
+                 dtype=np.float64, lstm=False, frame84=False):
         self.algo, self.A, self.E, self.n = algo, int(action_size), int(num_envs), int(n_step)
         self.seed = int(seed)
         self.k0, self.k1 = px.seed_key(seed)
@@ -54,15 +54,20 @@ class EngineRef:
         x0 = px.philox4x32(self.ids, 0, 0, 11, self.k0, self.k1)[0]
         self.ep_end = EP_END_CHOICES[x0 % 3]
         self._screens = {}
+        # measurement mode M2 (a3c_engine_config.frame84): pool frames are pre-sized 84x84 screens
+        self.frame84 = bool(frame84)
         self.cache_screens = True      # the fixed pool makes screens cacheable; bench turns it off
 
     # ---- screens of pool frames (cached: the pool is a fixed set) --------------------
+    def _screen(self, f):
+        return pool_frame84(self.seed, f) if self.frame84 else R.screen(pool_frame(self.seed, f))
+
     def screen_of(self, f):
         f = int(f)
         if not self.cache_screens:
-            return R.screen(pool_frame(self.seed, f))
+            return self._screen(f)
         if f not in self._screens:
-            self._screens[f] = R.screen(pool_frame(self.seed, f))
+            self._screens[f] = self._screen(f)
         return self._screens[f]
 
     def reset(self):

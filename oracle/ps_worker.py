@@ -28,7 +28,7 @@ def _names_shapes(A, algo):
     return R.param_shapes(A, algo)
 
 
-def _worker(wid, E, n, A, algo, lives, seed, seconds, shm_name, layout, start_evt, out_q):
+def _worker(wid, E, n, A, algo, lives, seed, seconds, shm_name, layout, start_evt, out_q, frame84=False):
     os.environ['OMP_NUM_THREADS'] = '1'
     os.environ['OPENBLAS_NUM_THREADS'] = '1'
     os.environ['MKL_NUM_THREADS'] = '1'
@@ -50,7 +50,7 @@ def _worker(wid, E, n, A, algo, lives, seed, seconds, shm_name, layout, start_ev
 
     shared_p, shared_ms, shared_mom = views(P), views(MS), views(MOM)
     ref = EngineRef({k: v.copy() for k, v in shared_p.items()}, E, n, A, algo, lives, num_frames=16384,
-                    seed=seed, env_id_base=wid * E, dtype=np.float32)
+                    seed=seed, env_id_base=wid * E, dtype=np.float32, frame84=frame84)
     ref.cache_screens = False
     ref.reset()
     start_evt.wait()
@@ -74,7 +74,7 @@ def _worker(wid, E, n, A, algo, lives, seed, seconds, shm_name, layout, start_ev
 
 
 def run(seconds=12.0, workers=1, envs_per_worker=8, n_step=5, action_size=6, algo='a3c', start_lives=0,
-        seed=123):
+        seed=123, frame84=False):
     """Returns dict(value=env-steps/s over all workers, cores, iterations)."""
     from multiprocessing import shared_memory
     from . import ref_cpu as R
@@ -99,7 +99,7 @@ def run(seconds=12.0, workers=1, envs_per_worker=8, n_step=5, action_size=6, alg
         start_evt = ctx.Event()
         out_q = ctx.Queue()
         procs = [ctx.Process(target=_worker, args=(w, envs_per_worker, n_step, action_size, algo, start_lives,
-                                                   seed, seconds, shm.name, layout, start_evt, out_q))
+                                                   seed, seconds, shm.name, layout, start_evt, out_q, frame84))
                  for w in range(workers)]
         for p in procs:
             p.start()

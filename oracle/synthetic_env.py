@@ -45,6 +45,15 @@ def pool_frame(seed, f):
     return words.view(np.uint8).reshape(SCREEN_H, SCREEN_W, 3)
 
 
+def pool_frame84(seed, f):
+    """Frame ``f`` of the pre-sized pool (measurement mode M2): the same hash as
+    pool_frame over the 441 chunks of one 84x84 u8 plane.  Returns u8 [84, 84]."""
+    k0, k1 = px.seed_key(seed)
+    j = np.arange(84 * 84 // 16, dtype=np.uint32)
+    w = px.philox4x32(j, np.uint32(f), px.P_POOL, 0, k0, k1)
+    return np.stack(w, axis=1).astype('<u4').view(np.uint8).reshape(84, 84)
+
+
 class SyntheticAtari:
     """Vectorised over E envs with global ids ``env_ids``."""
 

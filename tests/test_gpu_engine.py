@@ -29,7 +29,7 @@ def build(algo, A, E, n, lives, seed, frames=48, use_graph=True, scale=4.0, **kw
     p = init_params(ns, seed=seed, stddev=0.02 * scale)
     eng.reset(flatten_host(ns, eng.offsets, eng.params.numel(), p))
     ref = EngineRef(p, E, n, A, algo, lives, frames, seed, **{k: v for k, v in kw.items() if k in
-                                                              ('target_q_update_step', 'learning_rate')})
+                                                              ('target_q_update_step', 'learning_rate', 'frame84')})
     ref.reset()
     return eng, ref, ns
 
@@ -64,7 +64,18 @@ def unflat(eng, ns, flat):
 
 @pytest.mark.parametrize('algo,A,E,n,lives', [('a3c', 6, 8, 5, 0), ('a3c', 4, 6, 3, 5), ('q', 6, 4, 8, 3)])
 def test_engine_matches_oracle(algo, A, E, n, lives):
-    eng, ref, ns = build(algo, A, E, n, lives, seed=123 + E, target_q_update_step=40)
+    check_engine_vs_oracle(algo, A, E, n, lives)
+
+
+@pytest.mark.parametrize('algo,A,E,n,lives', [('a3c', 6, 8, 5, 0), ('q', 6, 4, 8, 3)])
+def test_frame84_mode_matches_oracle(algo, A, E, n, lives):
+    """Measurement mode M2: pre-sized 84x84 pool frames copied into the history
+    ring instead of Environment.screen of RGB frames; the same parity bar as the RGB mode."""
+    check_engine_vs_oracle(algo, A, E, n, lives, frame84=1)
+
+
+def check_engine_vs_oracle(algo, A, E, n, lives, **kw):
+    eng, ref, ns = build(algo, A, E, n, lives, seed=123 + E, target_q_update_step=40, **kw)
     torch.cuda.synchronize()
     # initial env state and history ring
     assert np.array_equal(eng.env_frame.cpu().numpy(), ref.env.frame.astype(np.int32))
@@ -259,11 +270,13 @@ def test_overlap_with_zero_lr_equals_sync():
     assert int(o.counters[1].item()) == int(s.counters[1].item())
 
 
-def test_overlap_stale_semantics_match_oracle():
+@pytest.mark.parametrize('frame84', [0, 1])
+def test_overlap_stale_semantics_match_oracle(frame84):
     """Rollout k uses the parameters after update k-2 (staleness 1): replay that order on the
-    oracle with the engine's own actions and activations; parameters agree at 1e-5."""
+    oracle with the engine's own actions and activations; parameters agree at 1e-5 (RGB frames,
+    and the pre-sized 84x84 frames of measurement mode M2)."""
     A, E, n = 6, 8, 5
-    eng, ref, ns = build('a3c', A, E, n, 0, seed=77, overlap=True, learning_rate=3e-3)
+    eng, ref, ns = build('a3c', A, E, n, 0, seed=77, overlap=True, learning_rate=3e-3, frame84=frame84)
     hist = []                  # per rollout: (oracle params used, planes, oracle out)
     for k in range(5):
         eng.iterate()
@@ -275,6 +288,10 @@ def test_overlap_stale_semantics_match_oracle():
         ref.tau += n                                    # the rollout owns tau in overlap mode
         assert np.array_equal(sl['rewards'].cpu().numpy(), out['rewards']), k
         assert np.array_equal(sl['terminals'].cpu().numpy(), out['terminals']), k
+        ring = eng.frame_ring.cpu().numpy()            # the rollout's new screens, bit-exact
+        for t in range(n):
+            tt = ref.tau - n + t + 1
+            assert np.array_equal(ring[:, tt % eng.ring_slots], ref.ring[:, tt % ref.R]), (k, t)
         agree = (sl['actions'].cpu().numpy() == out['sampled']).mean()
         assert agree >= 0.98, (k, agree)
         hist.append((Pk, planes, out))
@@ -312,11 +329,12 @@ def test_stream_ordering_modes_are_bit_identical(monkeypatch):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
 
 
-@pytest.mark.parametrize('overlap', [False, True])
-def test_bench_shape_is_deterministic(overlap):
+@pytest.mark.parametrize('overlap,frame84', [(False, 0), (True, 0), (True, 1)])
+def test_bench_shape_is_deterministic(overlap, frame84):
     """At the bench configuration (Pong, 256 envs, n=5) two engines from the same seed train bit for
     bit alike: every reduction is fixed-order (slab folds, sum of squares), no atomics."""
-    engs = [build('a3c', 6, 256, 5, 0, seed=29, frames=512, scale=1.0, overlap=overlap)[0] for _ in range(2)]
+    engs = [build('a3c', 6, 256, 5, 0, seed=29, frames=512, scale=1.0, overlap=overlap, frame84=frame84)[0]
+            for _ in range(2)]
     for _ in range(4):
         for e in engs:
             e.iterate()
