@@ -142,6 +142,13 @@ __device__ inline void st_act(T* p, T v) {
 #endif
 }
 
+// one 16-byte-per-lane global -> LDS DMA wave-instruction: lane l's 16 bytes land at
+// lds_base + 16 l (lds_base wave-uniform), no VGPR destination
+__device__ inline void glds16(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
 // sum_{s < n} p[s * stride], accumulated in s order (bit-identical to the plain loop) with 8 loads in
 // flight: the deterministic slab folds would otherwise wait one full load latency per term
 __device__ inline float sum_strided(const float* __restrict__ p, int n, int64_t stride) {

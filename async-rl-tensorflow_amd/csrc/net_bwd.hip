@@ -160,13 +160,6 @@ __device__ inline int dlb_slot(int G, int n) { return 4 * (G >> 2) + ((G + ((n >
 // the backward overlaps the next rollout (engine overlap mode)
 #define CB_SMEM_COMPACT (CB_X8 + CB_TAIL)                                               // 74304
 
-// one 16-byte-per-lane global -> LDS DMA wave-instruction: lane l's 16 bytes land at
-// lds_base + 16 l (lds_base wave-uniform), no VGPR destination
-__device__ inline void glds16(const void* g, void* lds_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
-}
-
 // the nw waves DMA `nbytes` (multiple of 16) from g to LDS dst in 1 KiB wave-instructions
 __device__ inline void glds_copy(const uint8_t* g, uint8_t* dst, int nbytes, int wid, int lane, int nw) {
   for (int c = wid; c * 1024 < nbytes; c += nw) {

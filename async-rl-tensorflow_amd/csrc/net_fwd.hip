@@ -790,7 +790,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
     fbias = *(const f32x4*)(sel.fc_bias + 4 * flane);
   }
   const int pt = (int)threadIdx.x - 128;
-  uint4 pv[PER3], wv[PERW];
+  uint4 pv[PER3];
   if (pt >= 0) {
 #pragma unroll
     for (int k = 0; k < PER3; ++k) {
@@ -798,10 +798,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
       const int c = i / (PLANE / 16), j = i - c * (PLANE / 16);
       pv[k] = ((const uint4*)state_plane(nx.sa, b, c, tau0))[j];
     }
+    // the weight fragments go global -> LDS (x8 region, free until the screen) by DMA: no VGPRs
+    // (held in registers they spilled 48 B per lane to scratch); landed by the vmcnt(0) below
+    const int wbase = (fwid - 2) * 64;
 #pragma unroll
-    for (int k = 0; k < PERW; ++k) wv[k] = ((const uint4*)nx.w1s)[pt + PT * k];
+    for (int k = 0; k < PERW; ++k)
+      glds16((const uint4*)nx.w1s + wbase + PT * k + flane, (uint4*)x8 + wbase + PT * k);
 #ifdef HS_TIMES
-    if (dbg && pt == 0) dbg[16] = __builtin_readcyclecounter() + (pv[0].x & 0) + (wv[PERW - 1].x & 0);
+    if (dbg && pt == 0) dbg[16] = __builtin_readcyclecounter() + (pv[0].x & 0);
 #endif
   }
   const float* hrow = nullptr;
@@ -824,6 +828,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   uint16_t* xold = (uint16_t*)smem;                      // planes 0..2, bf16
   uint4* wlds = (uint4*)x8;
   if (pt >= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the planes and the weight DMA landed
 #pragma unroll
     for (int k = 0; k < PER3; ++k) {
       const int i = pt + PT * k;                         // chunk i = pixels 16 i .. 16 i + 15
@@ -835,8 +840,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
         d[1] = make_uint4(a2.x, a2.y, a3.x, a3.y);
       }
     }
-#pragma unroll
-    for (int k = 0; k < PERW; ++k) wlds[pt + PT * k] = wv[k];
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   // conv1 over the 3 older planes while the new frame streams in from HBM (LDS operands only:
