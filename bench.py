@@ -280,8 +280,9 @@ def main():
         # HBM bytes per launch from the committed PMC passes (tools/profile_round.sh):
         # (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 FETCH_SIZE correction per MI355X_MICROARCH.md
         traffic = None
-        pmc = os.path.join(ROOT, 'profiles', 'pmc_hbm_bytes.json')
-        if os.path.exists(pmc) and not args.frames84:    # (the committed passes profile mode M1)
+        # (per frame mode: the committed passes of mode M1 and of mode M2)
+        pmc = os.path.join(ROOT, 'profiles', 'pmc_hbm_bytes_m2.json' if args.frames84 else 'pmc_hbm_bytes.json')
+        if os.path.exists(pmc):
             try:
                 t = json.load(open(pmc))['hbm_bytes_per_launch'].get(dom)
                 traffic = None if t is None else int(round(t))
