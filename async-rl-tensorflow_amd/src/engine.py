@@ -43,7 +43,7 @@ def _view(ptr, shape, dtype):
 
 class Engine:
     def __init__(self, num_envs=256, n_step=5, action_size=6, algo='a3c', start_lives=0, num_frames=1024,
-                 seed=123, env_id_base=0, world_size=1, use_graph=True, overlap=False, lstm=False,
+                 seed=123, env_id_base=0, world_size=1, use_graph=False, overlap=False, lstm=False,
                  external_env=False, **overrides):
         _lib.require_device()
         if lstm and algo != 'a3c':

@@ -57,7 +57,10 @@ def parse():
     ap.add_argument('--frames84', action='store_true',
                     help='measurement mode M2 (SURVEY 8(d)): the pool holds pre-sized 84x84 grey frames, the env '
                          'step copies one into the history ring (no Environment.screen); default M1: raw RGB')
-    ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--graph', action='store_true',
+                    help='capture each iteration into hipGraphs (default: eager launches, faster on MI355X: '
+                         'a graph end costs ~13 us before the next packet on its stream)')
+    ap.add_argument('--no-graph', action='store_true', help='(the default; kept for older command lines)')
     ap.add_argument('--update', default='overlap', choices=['overlap', 'sync', 'hogwild'],
                     help='overlap: rollout k overlaps backward+apply of rollout k-1 (stale-1 async A3C); '
                          'sync: rollout -> backward -> all-reduce -> apply; hogwild: unlocked pushes into a '
@@ -139,7 +142,7 @@ def main():
     if host and args.frames84:
         raise SystemExit('--frames84 is a device-env pool mode')
     eng = Engine(num_envs=E, n_step=n, action_size=A, algo=args.algo, start_lives=lives, num_frames=args.frames,
-                 seed=123, env_id_base=rank * E, world_size=world, use_graph=not args.no_graph,
+                 seed=123, env_id_base=rank * E, world_size=world, use_graph=args.graph and not args.no_graph,
                  overlap=args.update == 'overlap', lstm=args.lstm, external_env=host, frame84=int(args.frames84))
     hpool = None
     if host:
@@ -326,7 +329,7 @@ def main():
                                        f'{world} sequential RMSProp steps per owned shard, RCCL all-gather'
                                        if args.exchange == 'sequential' else
                                        f'dp{world} all-reduce (RCCL) of per-worker-clipped grads, one summed step')
-                       if world > 1 else 'dp1', 'hipgraph': not args.no_graph,
+                       if world > 1 else 'dp1', 'hipgraph': args.graph and not args.no_graph,
                        'update': {'overlap': 'overlap: rollout k uses params after update k-2 (A3C stale-1 async), '
                                              'backward+apply of k-1 concurrent with rollout k',
                                   'sync': 'synchronous: rollout -> backward -> apply',

@@ -264,7 +264,8 @@ typedef struct a3c_engine_config {
   int random_start;      /* config.py:7 (30)                                          */
   int action_repeat;     /* config.py:50 (1)                                          */
   int num_frames;        /* synthetic frame pool size (HBM resident RGB frames)       */
-  int use_graph;         /* capture the rollout+backward into a hipGraph              */
+  int use_graph;         /* 1: capture the rollout / backward into hipGraphs; default 0
+                            (eager launches: faster on MI355X)          */
   uint64_t seed;         /* main.py:35 random_seed (123)                             */
   double gamma;          /* config.py:9 discount 0.99                                 */
   float beta;            /* config.py:16 entropy weight 0.01                          */

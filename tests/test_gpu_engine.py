@@ -19,7 +19,7 @@ def rel_l2(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
 
 
-def build(algo, A, E, n, lives, seed, frames=48, use_graph=True, scale=4.0, **kw):
+def build(algo, A, E, n, lives, seed, frames=48, use_graph=False, scale=4.0, **kw):
     from src.engine import Engine
     from src.initializers import init_params, flatten_host
     from src.kernels import param_names_shapes
@@ -141,9 +141,10 @@ def check_engine_vs_oracle(algo, A, E, n, lives, **kw):
                 np.testing.assert_allclose(T[name], ref.tparams[name], rtol=1e-5, atol=1e-6)
 
 
-def test_engine_deterministic_and_graph_equals_eager():
-    a, _, ns = build('a3c', 6, 16, 5, 0, seed=7)
-    b, _, _ = build('a3c', 6, 16, 5, 0, seed=7, use_graph=False)
+@pytest.mark.parametrize('overlap', [False, True])
+def test_engine_deterministic_and_graph_equals_eager(overlap):
+    a, _, ns = build('a3c', 6, 16, 5, 0, seed=7, use_graph=True, overlap=overlap)
+    b, _, _ = build('a3c', 6, 16, 5, 0, seed=7, use_graph=False, overlap=overlap)
     for _ in range(4):
         a.iterate()
         b.iterate()

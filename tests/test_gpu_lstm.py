@@ -183,7 +183,7 @@ def test_engine_lstm_overlap_zero_lr_equals_sync():
 def test_engine_lstm_bench_shape_runs():
     """BASELINE config 5 per GPU (SpaceInvaders, 256 envs, n=5, LSTM head): runs, finite, graph
     replay equals eager."""
-    a, _, _ = build(6, 256, 5, 3, seed=5, frames=256, scale=1.0, overlap=True)
+    a, _, _ = build(6, 256, 5, 3, seed=5, frames=256, scale=1.0, overlap=True, use_graph=True)
     b, _, _ = build(6, 256, 5, 3, seed=5, frames=256, scale=1.0, overlap=True, use_graph=False)
     for _ in range(3):
         a.iterate()

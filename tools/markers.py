@@ -1,7 +1,7 @@
 """Unprofiled iteration timeline from the marker build (-DA3C_MARKERS): rollout start (0) / end (1),
 backward start (2), apply end (3), s_memrealtime (100 MHz).  Per iteration (anchored at each
 rollout start) prints the mean offsets of the other marks and the rollout / backward spans.
-A3C_LIB=<marker build> python3 tools/markers.py [overlap|sync]"""
+A3C_LIB=<marker build> python3 tools/markers.py [overlap|sync] [m2] [eager]"""
 import ctypes
 import os
 import sys
@@ -17,7 +17,8 @@ mode = sys.argv[1] if len(sys.argv) > 1 else 'overlap'
 L = _lib.lib()
 L.a3c_debug_marks.argtypes = [ctypes.c_void_p, ctypes.c_int]
 buf = np.zeros(2 + 2 * 8192, dtype=np.uint64)
-eng = Engine(num_envs=256, n_step=5, action_size=6, num_frames=16384, seed=123, overlap=mode == 'overlap')
+eng = Engine(num_envs=256, n_step=5, action_size=6, num_frames=16384, seed=123, overlap=mode == 'overlap',
+             frame84=int('m2' in sys.argv[2:]), use_graph='eager' not in sys.argv[2:])
 ns = param_names_shapes(6, 'a3c')
 eng.reset(flatten_host(ns, eng.offsets, eng.params.numel(), init_params(ns, seed=123)))
 for _ in range(20):
