@@ -11,6 +11,11 @@ parameter-server apply of main.py:60-66.
 parameters after update k-2 while the backward, exchange and apply of rollout k-1 run on the
 caller's stream (A3C's stale-parameter asynchrony at a fixed staleness of one update).  Rollout
 k's buffers are ``slot(k & 1)``.
+
+Kernels are launched eagerly by default; ``use_graph=True`` captures each engine call into
+hipGraphs and replays them (bit-identical, measured slower on MI355X: DESIGN.md §6).
+``frame84=1`` (an engine option) feeds pre-sized 84x84 frames instead of raw RGB (measurement
+mode M2).
 """
 import ctypes
 
@@ -186,8 +191,8 @@ class Engine:
 
     def iterate(self, exchange=None):
         """One iteration: rollout + gradient, [exchange(grads)], apply.  Single-GPU device-env
-        engines without an exchange take the fused path (a3c_engine_iterate: the apply captured
-        into the same hipGraphs, bit-identical to rollout_grad() + apply()).  An exchange with
+        engines without an exchange take the fused path (a3c_engine_iterate: the apply enqueued with
+        the backward, bit-identical to rollout_grad() + apply()).  An exchange with
         ``owns_apply`` (src.distributed.PartitionedPS) performs the apply itself."""
         if exchange is None and self.cfg.world_size == 1 and not self.external_env:
             check(lib().a3c_engine_iterate(self._h, _lib.stream_handle()), 'a3c_engine_iterate')
@@ -275,7 +280,7 @@ class Engine:
         self.apply()
 
     def span_stats(self, which, reset=False):
-        """Live launch spans recorded inside the graphs (which 0: k_conv_bwd, 1:
+        """Live launch spans recorded by the kernels themselves (which 0: k_conv_bwd, 1:
         k_head_screen_conv12): reset=True clears; else (avg_us, max_us, launches)."""
         avg, mx, cnt = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
         check(lib().a3c_engine_span_stats(self._h, int(which), 1 if reset else 0, ctypes.byref(avg),
