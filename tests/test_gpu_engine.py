@@ -62,7 +62,8 @@ def unflat(eng, ns, flat):
     return out
 
 
-@pytest.mark.parametrize('algo,A,E,n,lives', [('a3c', 6, 8, 5, 0), ('a3c', 4, 6, 3, 5), ('q', 6, 4, 8, 3)])
+@pytest.mark.parametrize('algo,A,E,n,lives', [('a3c', 6, 8, 5, 0), ('a3c', 4, 6, 3, 5), ('q', 6, 4, 8, 3),
+                                               ('a3c', 6, 1, 5, 0), ('a3c', 6, 37, 2, 3)])
 def test_engine_matches_oracle(algo, A, E, n, lives):
     check_engine_vs_oracle(algo, A, E, n, lives)
 
@@ -271,12 +272,13 @@ def test_overlap_with_zero_lr_equals_sync():
     assert int(o.counters[1].item()) == int(s.counters[1].item())
 
 
-@pytest.mark.parametrize('frame84', [0, 1])
-def test_overlap_stale_semantics_match_oracle(frame84):
+@pytest.mark.parametrize('E,frame84', [(8, 0), (8, 1), (1, 0), (37, 0)])
+def test_overlap_stale_semantics_match_oracle(E, frame84):
     """Rollout k uses the parameters after update k-2 (staleness 1): replay that order on the
     oracle with the engine's own actions and activations; parameters agree at 1e-5 (RGB frames,
-    and the pre-sized 84x84 frames of measurement mode M2)."""
-    A, E, n = 6, 8, 5
+    and the pre-sized 84x84 frames of measurement mode M2; one env, and a ragged 37 that leaves
+    partial row blocks in the partial fc, the bootstrap head and the conv backward's groups)."""
+    A, n = 6, 5
     eng, ref, ns = build('a3c', A, E, n, 0, seed=77, overlap=True, learning_rate=3e-3, frame84=frame84)
     hist = []                  # per rollout: (oracle params used, planes, oracle out)
     for k in range(5):
