@@ -312,10 +312,16 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
     int prio = hi_prio;
     if (const char* v = getenv("A3C_ROLLOUT_PRIO")) prio = atoi(v) ? hi_prio : lo_prio;
+    // the cross-stream events order two streams of this device and the host never inspects
+    // them: no system-scope fence (measured: 4.54M vs 4.47M env-steps/s with events, on par with
+    // the wait-value hop; A3C_DEVICE_EVENTS=0 restores the default events)
+    unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;
+    if (const char* v = getenv("A3C_DEVICE_EVENTS"))
+      if (!atoi(v)) evf = hipEventDisableTiming;
     bool ok = hipStreamCreateWithPriority(&e->rs, hipStreamNonBlocking, prio) == hipSuccess &&
-              hipEventCreateWithFlags(&e->ev_start, hipEventDisableTiming) == hipSuccess;
+              hipEventCreateWithFlags(&e->ev_start, evf) == hipSuccess;
     for (int k = 0; k < 2 && ok; ++k)
-      ok = hipEventCreateWithFlags(&e->ev_roll[k], hipEventDisableTiming) == hipSuccess;
+      ok = hipEventCreateWithFlags(&e->ev_roll[k], evf) == hipSuccess;
     // (one GPU: with an exchange the collectives' own stream synchronisation sits between the
     // graphs, a combination the pool has not run on several GPUs -- events there)
     e->wait_value = e->cfg.world_size == 1;
