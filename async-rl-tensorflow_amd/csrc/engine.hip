@@ -932,19 +932,36 @@ extern "C" int a3c_engine_ext_act(a3c_engine* e, int32_t* actions, void* stream)
   return 0;
 }
 
+// part of observe: the post-act frames of envs [env_lo, env_hi) (rgb indexed by env, full
+// [E][210][160][3] buffer) -> device, so the H2D copy of one range overlaps the host stepping of
+// the next; a3c_engine_ext_observe(rgb = NULL, ...) then completes the step
+extern "C" int a3c_engine_ext_upload(a3c_engine* e, const uint8_t* rgb, int env_lo, int env_hi, void* stream) {
+  if (int rc = ext_check(e, "a3c_engine_ext_upload")) return rc;
+  if (!e->ext_begun || e->ext_t >= e->n || !rgb)
+    return a3c_set_error(A3C_ERR_STATE, "a3c_engine_ext_upload", "ext_act of this step first");
+  if (env_lo < 0 || env_hi > e->E || env_lo > env_hi)
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_ext_upload", "env range outside [0, num_envs]");
+  const int64_t fb = (int64_t)SCREEN_H * SCREEN_W * 3;
+  if (env_hi > env_lo)
+    A3C_CHECK(hipMemcpyAsync(e->pool + env_lo * fb, rgb + env_lo * fb, (size_t)(env_hi - env_lo) * fb,
+                             hipMemcpyDefault, (hipStream_t)stream));
+  return 0;
+}
+
 // observe of rollout step t: the post-act RGB frames [E][210][160][3] u8, rewards [E] f32 and
 // terminals [E] u8 of every env (GymEnvironment.act, environment.py:78-96, done on the host) ->
 // reward clip (agent.py:154), Environment.screen + History.add into the frame ring
+// rgb == NULL: the frames of every env were already sent by a3c_engine_ext_upload this step.
 extern "C" int a3c_engine_ext_observe(a3c_engine* e, const uint8_t* rgb, const float* rewards,
                                       const uint8_t* terminals, void* stream) {
   if (int rc = ext_check(e, "a3c_engine_ext_observe")) return rc;
-  if (!e->ext_begun || e->ext_t >= e->n || !rgb || !rewards || !terminals)
+  if (!e->ext_begun || e->ext_t >= e->n || !rewards || !terminals)
     return a3c_set_error(A3C_ERR_STATE, "a3c_engine_ext_observe", "ext_act of this step first");
   hipStream_t s = (hipStream_t)stream;
   const Slot& sl = e->slot[0];
   const int E = e->E, t = e->ext_t;
   const int64_t o = (int64_t)t * E;
-  A3C_CHECK(hipMemcpyAsync(e->pool, rgb, (size_t)E * SCREEN_H * SCREEN_W * 3, hipMemcpyDefault, s));
+  if (rgb) A3C_CHECK(hipMemcpyAsync(e->pool, rgb, (size_t)E * SCREEN_H * SCREEN_W * 3, hipMemcpyDefault, s));
   A3C_CHECK(hipMemcpyAsync(sl.rewards + o, rewards, (size_t)E * 4, hipMemcpyDefault, s));
   A3C_CHECK(hipMemcpyAsync(sl.terms + o, terminals, (size_t)E, hipMemcpyDefault, s));
   hipLaunchKernelGGL(k_ext_clip, dim3((E + 255) / 256), dim3(256), 0, s, sl.rewards + o, E);

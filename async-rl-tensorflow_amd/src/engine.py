@@ -241,9 +241,18 @@ class Engine:
         self._ext_check(actions_out, torch.int32, (self.E,), 'actions_out')
         check(lib().a3c_engine_ext_act(self._h, _lib.ptr(actions_out), _lib.stream_handle()), 'a3c_engine_ext_act')
 
-    def ext_observe(self, rgb, rewards, terminals):
-        """external_env: the step's post-act frames, rewards and terminals of every env."""
+    def ext_upload(self, rgb, env_lo, env_hi):
+        """external_env: the post-act frames of envs [env_lo, env_hi) only (rgb stays the full
+        [E,210,160,3] buffer); finish the step with ext_observe(None, rewards, terminals)."""
         self._ext_check(rgb, torch.uint8, (self.E, 210, 160, 3), 'rgb')
+        check(lib().a3c_engine_ext_upload(self._h, _lib.ptr(rgb), int(env_lo), int(env_hi), _lib.stream_handle()),
+              'a3c_engine_ext_upload')
+
+    def ext_observe(self, rgb, rewards, terminals):
+        """external_env: the step's post-act frames (None: sent by ext_upload), rewards and
+        terminals of every env."""
+        if rgb is not None:
+            self._ext_check(rgb, torch.uint8, (self.E, 210, 160, 3), 'rgb')
         self._ext_check(rewards, torch.float32, (self.E,), 'rewards')
         self._ext_check(terminals, torch.uint8, (self.E,), 'terminals')
         check(lib().a3c_engine_ext_observe(self._h, _lib.ptr(rgb), _lib.ptr(rewards), _lib.ptr(terminals),
@@ -266,11 +275,22 @@ class Engine:
             self._ext_began = True
             self._ext_actions = torch.zeros(self.E, dtype=torch.int32).pin_memory()
         stream = torch.cuda.current_stream()
+        # pools that step env ranges (SyntheticHostEnvPool) are stepped in `upload_chunks` ranges:
+        # the H2D copy of one range runs while the host steps the next
+        chunks = max(1, min(int(getattr(pool, 'upload_chunks', 1)), self.E)) if hasattr(pool, 'step_range') else 1
+        bounds = [self.E * c // chunks for c in range(chunks + 1)]
         for _ in range(self.n):
             self.ext_act(self._ext_actions)
             stream.synchronize()            # actions on the host; the previous H2D copies are done
-            pool.step(self._ext_actions.numpy())
-            self.ext_observe(pool.rgb, pool.rewards, pool.terminals)
+            acts = self._ext_actions.numpy()
+            if chunks == 1:
+                pool.step(acts)
+                self.ext_observe(pool.rgb, pool.rewards, pool.terminals)
+                continue
+            for lo, hi in zip(bounds[:-1], bounds[1:]):
+                pool.step_range(acts, lo, hi)
+                self.ext_upload(pool.rgb, lo, hi)
+            self.ext_observe(None, pool.rewards, pool.terminals)
         self.rollout_grad()
         if getattr(exchange, 'owns_apply', False):
             exchange.apply(self)

@@ -146,7 +146,7 @@ class SyntheticHostEnvPool(object):
   driving or measuring the external-env path (PCIe-inclusive).  Buffers are pinned."""
 
   def __init__(self, num_envs, action_size, start_lives=0, num_frames=1024, seed=123, env_id_base=0,
-               random_start=30, action_repeat=1, threads=8, is_training=True):
+               random_start=30, action_repeat=1, threads=8, is_training=True, upload_chunks=2):
     import ctypes
     from . import _lib
     self._lib = _lib
@@ -163,6 +163,7 @@ class SyntheticHostEnvPool(object):
     self.terminals = mk((self.E,), torch.uint8)
     self._acts = mk((self.E,), torch.int32)
     self.is_training = is_training
+    self.upload_chunks = int(upload_chunks)   # Engine.iterate_host: ranges per step (H2D overlap)
 
   def begin(self):
     self._lib.check(self._lib.lib().a3c_hostenv_begin(self._h, self._lib.ptr(self.rgb)), 'a3c_hostenv_begin')
@@ -175,6 +176,14 @@ class SyntheticHostEnvPool(object):
     self._lib.check(L.a3c_hostenv_step(self._h, p(self._acts), 1 if self.is_training else 0, p(self.rgb),
                                        p(self.rewards), p(self.terminals)), 'a3c_hostenv_step')
     return self.rgb, self.rewards, self.terminals
+
+  def step_range(self, actions, env_lo, env_hi):
+    """step of envs [env_lo, env_hi) only; actions is the full [E] array."""
+    self._acts.copy_(torch.as_tensor(np.asarray(actions, np.int32)))
+    L, p = self._lib.lib(), self._lib.ptr
+    self._lib.check(L.a3c_hostenv_step_range(self._h, p(self._acts), 1 if self.is_training else 0, p(self.rgb),
+                                             p(self.rewards), p(self.terminals), int(env_lo), int(env_hi)),
+                    'a3c_hostenv_step_range')
 
   def close(self):
     if getattr(self, '_h', None):

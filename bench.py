@@ -51,6 +51,8 @@ def parse():
                          'inputs); host: it runs on host threads (a3c_hostenv, stand-in for real ALE workers) '
                          'and every step moves the raw RGB frames over PCIe (PCIe-inclusive rate)')
     ap.add_argument('--host-threads', type=int, default=16)
+    ap.add_argument('--host-chunks', type=int, default=2,
+                    help='--env host: env ranges per rollout step; the H2D copy of one overlaps stepping the next')
     ap.add_argument('--lstm', action='store_true',
                     help='C5 LSTM policy head (BASELINE config 5: SpaceInvaders-v0, 256-cell LSTM after the fc)')
     ap.add_argument('--frames', type=int, default=16384, help='HBM frame pool (16384 = 1.65 GB > L3)')
@@ -148,7 +150,7 @@ def main():
     if host:
         from src.host_env import SyntheticHostEnvPool
         hpool = SyntheticHostEnvPool(E, A, lives, num_frames=min(args.frames, 2048), seed=123, env_id_base=rank * E,
-                                     threads=args.host_threads)
+                                     threads=args.host_threads, upload_chunks=args.host_chunks)
     ns = param_names_shapes(A, args.algo, lstm=args.lstm)
     params = flatten_host(ns, eng.offsets, eng.params.numel(), init_params(ns, seed=123))
     eng.reset(params)     # every rank starts from the same parameters

@@ -350,6 +350,9 @@ int a3c_engine_ext_begin(a3c_engine* eng, const uint8_t* rgb, void* stream);
 int a3c_engine_ext_act(a3c_engine* eng, int32_t* actions, void* stream);
 int a3c_engine_ext_observe(a3c_engine* eng, const uint8_t* rgb, const float* rewards, const uint8_t* terminals,
                            void* stream);
+/* part of observe (same step, before it): frames of envs [env_lo, env_hi) only, so the copy of
+ * one range overlaps the host stepping of the next; observe is then called with rgb = NULL */
+int a3c_engine_ext_upload(a3c_engine* eng, const uint8_t* rgb, int env_lo, int env_hi, void* stream);
 
 /* Host-side batched synthetic env (the device env's emulator, bit-identical dynamics, stepped by
  * `threads` CPU threads): raw RGB frames into caller host buffers -- a stand-in for real ALE
@@ -365,6 +368,9 @@ int a3c_hostenv_destroy(a3c_hostenv* env);
 int a3c_hostenv_begin(a3c_hostenv* env, uint8_t* rgb);
 int a3c_hostenv_step(a3c_hostenv* env, const int32_t* actions, int is_training, uint8_t* rgb, float* rewards,
                      uint8_t* terminals);
+/* step of envs [env_lo, env_hi) only (buffers stay full-size, indexed by env) */
+int a3c_hostenv_step_range(a3c_hostenv* env, const int32_t* actions, int is_training, uint8_t* rgb,
+                           float* rewards, uint8_t* terminals, int env_lo, int env_hi);
 
 /* device pointers owned by the engine (valid until destroy) */
 typedef struct a3c_engine_buffers {

@@ -81,3 +81,39 @@ def test_external_env_call_order_enforced():
         ext.ext_act(torch.zeros(2, dtype=torch.int32))     # pageable host buffer
     with pytest.raises(RuntimeError):
         Engine(num_envs=2, n_step=2, action_size=6, external_env=True, overlap=True)
+
+
+@pytest.mark.parametrize('chunks,E', [(1, 8), (3, 8), (4, 13), (13, 13)])
+def test_chunked_uploads_equal_device_envs(chunks, E):
+    """The C++ host env stepped in env ranges, each range's frames sent by a3c_engine_ext_upload
+    while the next is stepped (Engine.iterate_host), equals the device-env engine bit for bit."""
+    from src.host_env import SyntheticHostEnvPool
+    seed, P, A, n, lives = 321, 40, 6, 5, 3
+    dev, ext = _pair('a3c', A, E, n, lives, seed, P)
+    pool = SyntheticHostEnvPool(E, A, lives, num_frames=P, seed=seed, threads=3, upload_chunks=chunks)
+    for it in range(4):
+        dev.iterate()
+        ext.iterate_host(pool)
+        torch.cuda.synchronize()
+        assert torch.equal(dev.actions, ext.actions), it
+        assert torch.equal(dev.rewards, ext.rewards), it
+        assert torch.equal(dev.terminals, ext.terminals), it
+        assert torch.equal(dev.frame_ring, ext.frame_ring), it
+        torch.testing.assert_close(ext.loss, dev.loss, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(ext.params, dev.params, rtol=1e-6, atol=1e-7)
+    pool.close()
+
+
+def test_ext_upload_checks():
+    from src.engine import Engine
+    ext = Engine(num_envs=3, n_step=2, action_size=6, external_env=True, num_frames=1)
+    ext.reset()
+    rgb = torch.zeros(3, 210, 160, 3, dtype=torch.uint8).pin_memory()
+    with pytest.raises(RuntimeError):
+        ext.ext_upload(rgb, 0, 3)               # ext_begin / ext_act first
+    ext.ext_begin(rgb)
+    ext.ext_act(torch.zeros(3, dtype=torch.int32).pin_memory())
+    with pytest.raises(RuntimeError):
+        ext.ext_upload(rgb, 2, 4)               # range outside [0, E]
+    ext.ext_upload(rgb, 0, 3)
+    torch.cuda.synchronize()

@@ -3,6 +3,8 @@ Environment / GymEnvironment code (tests/golden/make_env_goldens.py, environment
 scripted emulator: same frames, rewards, terminals, lives, emulator step and reset counts."""
 import random
 
+import pytest
+
 import numpy as np
 
 from fake_ale import ScriptedALE
@@ -75,3 +77,30 @@ def test_cpp_host_env_matches_oracle():
             ref.new_random_game(t.astype(bool))
     assert terms > 0
     pool.close()
+
+
+def test_cpp_host_env_ranges_equal_full_step():
+    """a3c_hostenv_step_range over ragged env ranges (Engine.iterate_host's upload chunks) ==
+    a3c_hostenv_step of every env at once, and bad ranges raise."""
+    from src.host_env import SyntheticHostEnvPool
+    E, P, A, L = 11, 40, 6, 3
+    full = SyntheticHostEnvPool(E, A, L, num_frames=P, seed=5, threads=4)
+    part = SyntheticHostEnvPool(E, A, L, num_frames=P, seed=5, threads=3)
+    assert np.array_equal(full.begin().numpy(), part.begin().numpy())
+    rng = np.random.default_rng(1)
+    for it in range(120):
+        a = rng.integers(0, A, E).astype(np.int32)
+        full.step(a)
+        cuts = sorted(set([0, E] + list(rng.integers(0, E + 1, 3))))
+        for lo, hi in zip(cuts[:-1], cuts[1:]):
+            part.step_range(a, lo, hi)
+        part.step_range(a, 4, 4)            # empty range: no env steps
+        assert np.array_equal(full.rgb.numpy(), part.rgb.numpy()), it
+        assert np.array_equal(full.rewards.numpy(), part.rewards.numpy()), it
+        assert np.array_equal(full.terminals.numpy(), part.terminals.numpy()), it
+    with pytest.raises(RuntimeError):
+        part.step_range(a, 3, E + 1)
+    with pytest.raises(RuntimeError):
+        part.step_range(a, 5, 2)
+    full.close()
+    part.close()
