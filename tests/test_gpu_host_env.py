@@ -83,7 +83,7 @@ def test_external_env_call_order_enforced():
         Engine(num_envs=2, n_step=2, action_size=6, external_env=True, overlap=True)
 
 
-@pytest.mark.parametrize('chunks,E', [(1, 8), (3, 8), (4, 13), (13, 13)])
+@pytest.mark.parametrize('chunks,E', [(1, 8), (3, 8), (4, 13), (13, 13), (2, 256)])   # 256: BASELINE config 2
 def test_chunked_uploads_equal_device_envs(chunks, E):
     """The C++ host env stepped in env ranges, each range's frames sent by a3c_engine_ext_upload
     while the next is stepped (Engine.iterate_host), equals the device-env engine bit for bit."""
