@@ -147,7 +147,12 @@ extern "C" int a3c_hostenv_create(int num_envs, int action_size, int start_lives
         memcpy(pool + f * FRAME_BYTES + j * 16, w, 16);
       }
   });
-  h->workers.start(threads < num_envs ? threads : num_envs);
+  try {
+    h->workers.start(threads < num_envs ? threads : num_envs);
+  } catch (...) {       // no exception crosses the C ABI
+    delete h;
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_hostenv_create", "could not start worker threads");
+  }
   *out = h;
   return 0;
 }
