@@ -58,6 +58,10 @@ def parse_flags(argv=None):
   p.add_argument('--num_envs', type=int, default=256)
   p.add_argument('--num_frames', type=int, default=16384)
   p.add_argument('--iterations', type=int, default=1000)
+  p.add_argument('--envs_on', choices=['device', 'host', 'gym'], default='device',
+                 help='engine mode: envs stepped on the GPU (synthetic), on host threads (C++ synthetic '
+                      'emulator, frames over PCIe), or gym/ALE envs on the host (AtariEnv, needs gym)')
+  p.add_argument('--host_threads', type=int, default=16)
   p.add_argument('--max_step', type=int, default=None)
   p.add_argument('--log_every', type=int, default=100)
   p.add_argument('--update', choices=['overlap', 'sync', 'hogwild'], default='overlap',
@@ -80,6 +84,29 @@ def initial_params(eng, action_size, algo, seed):
   return flatten_host(ns, eng.offsets, eng.params.numel(), init_params(ns, seed=seed))
 
 
+def make_host_pool(config, flags, E, A, lives, rank):
+  """Host-stepped envs for the external-env engine: the C++ synthetic emulator
+  (`host`), or E gym envs wrapped with the reference's Environment rules (`gym`,
+  environment.py:14-96)."""
+  from src.host_env import AtariEnv, HostEnvPool, SyntheticHostEnvPool
+  if flags.envs_on == 'host':
+    return SyntheticHostEnvPool(E, A, lives, num_frames=min(flags.num_frames, 2048), seed=flags.random_seed,
+                                env_id_base=rank * E, random_start=config.random_start,
+                                action_repeat=config.action_repeat, threads=flags.host_threads)
+  try:
+    import gym
+  except ImportError as e:
+    raise RuntimeError('--envs_on gym needs the gym package (with the Atari ROMs)') from e
+  rng = random.Random(flags.random_seed + rank)
+  envs = []
+  for e in range(E):
+    g = gym.make(config.env_name)
+    if hasattr(g, 'seed'):
+      g.seed(flags.random_seed + rank * E + e)
+    envs.append(AtariEnv(g, action_repeat=config.action_repeat, random_start=config.random_start, rng=rng))
+  return HostEnvPool(envs, threads=flags.host_threads)
+
+
 def run_engine(config, flags):
   from src import distributed as D
   from src.engine import Engine
@@ -94,10 +121,14 @@ def run_engine(config, flags):
               ep_end=config.ep_end, ep_end_t=config.ep_end_t, learn_start=config.learn_start,
               target_q_update_step=config.target_q_update_step, random_start=config.random_start,
               action_repeat=config.action_repeat)
-  overlap = flags.update == 'overlap' and flags.algo == 'a3c'
+  host = flags.envs_on != 'device'
+  if host and flags.update == 'hogwild':
+    raise ValueError('--envs_on host/gym drives a synchronous engine; use --update sync or overlap')
+  overlap = flags.update == 'overlap' and flags.algo == 'a3c' and not host
+  pool = make_host_pool(config, flags, E, A, lives, rank) if host else None
   eng = Engine(num_envs=E, n_step=flags.n_step, action_size=A, algo=flags.algo, start_lives=lives,
-               num_frames=flags.num_frames, seed=flags.random_seed, env_id_base=rank * E, world_size=world,
-               overlap=overlap, **opts)
+               num_frames=1 if host else flags.num_frames, seed=flags.random_seed, env_id_base=rank * E,
+               world_size=world, overlap=overlap, external_env=host, **opts)
   eng.reset(initial_params(eng, A, flags.algo, flags.random_seed))
   D.broadcast_params(eng.params, src=0)
   if flags.algo == 'q':
@@ -124,6 +155,8 @@ def run_engine(config, flags):
   for it in range(iterations):
     if ps is not None:
       eng.iterate_hogwild(ps)
+    elif pool is not None:
+      eng.iterate_host(pool, exchange=xch)
     else:
       eng.iterate(exchange=xch)
     if rank == 0 and (it + 1) % flags.log_every == 0:
@@ -139,6 +172,8 @@ def run_engine(config, flags):
   torch.cuda.synchronize()
   if ps is not None:
     ps.close()
+  if pool is not None:
+    pool.close()
   if log:
     log.close()
   return eng

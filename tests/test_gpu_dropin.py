@@ -354,6 +354,29 @@ def test_main_engine_mode_runs(tmp_path, update):
     assert len(lines) == 2
 
 
+@pytest.mark.parametrize('update', ['sync', 'overlap'])
+def test_main_engine_mode_host_envs(tmp_path, update):
+    """main.py --mode engine --envs_on host: host-stepped envs feed the engine
+    (overlap falls back to the synchronous engine); hogwild and a missing gym are refused."""
+    import main
+    eng = main.main(['--mode', 'engine', '--env_name', 'Pong-v0', '--num_envs', '16', '--num_frames', '64',
+                     '--iterations', '4', '--log_every', '2', '--logdir', str(tmp_path), '--update', update,
+                     '--envs_on', 'host', '--host_threads', '4'])
+    torch.cuda.synchronize()
+    assert eng.external_env and torch.isfinite(eng.params).all()
+    assert int(eng.counters[1].item()) == 4 * 16 * 5
+    assert len(open(tmp_path / 'engine.jsonl').read().splitlines()) == 2
+    with pytest.raises(ValueError):
+        main.main(['--mode', 'engine', '--envs_on', 'host', '--update', 'hogwild', '--num_envs', '4',
+                   '--iterations', '1', '--logdir', str(tmp_path)])
+    try:
+        import gym  # noqa: F401
+    except ImportError:
+        with pytest.raises(RuntimeError):
+            main.main(['--mode', 'engine', '--envs_on', 'gym', '--num_envs', '4', '--iterations', '1',
+                       '--logdir', str(tmp_path)])
+
+
 def test_main_engine_mode_initialises_params_and_stops_at_max_step(tmp_path):
     """main.py --mode engine starts from the reference initialisers (conv truncated_normal(0,
     0.02) agent.py:214, linear normal(0.02) ops.py:36-37, zero biases), not from whatever
