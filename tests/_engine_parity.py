@@ -1,0 +1,227 @@
+"""Shared checks of the batched engine against the CPU replay oracle (oracle/engine_ref.py).
+
+Test infrastructure only (imported by tests/test_gpu_*.py).  Each check drives the HIP engine
+through src/engine.py (the C-ABI) and replays the same iteration on the oracle with the engine's
+own action draws, then asserts:
+  * env dynamics, rewards, terminals and the frame ring (Environment.screen + History) bit-exact;
+  * the engine's draws agree with the oracle's policy except at fp32 cdf boundaries;
+  * n-step returns / TD targets within 1e-5;
+  * losses within 1e-4 of max(1, |loss|) (north star: 1e-3);
+  * gradients within 1e-4 relative-L2 of the fp64 oracle backward on the engine's own saved
+    activations (same ReLU masks), and within 2e-2 of the fully independent fp64 forward+backward;
+  * parameters after clip + RMSProp within 1e-5 over the iterations.
+Reference: agent.py:141-207 (act / observe / batch_update), agent.py:306-321 (loss, clip, apply),
+network.py:60-94 + assets/a3c.png (A3C losses, n-step returns), main.py:63-65 (RMSProp)."""
+import numpy as np
+import torch
+
+from oracle import ref_cpu as Rc
+from oracle.engine_ref import EngineRef
+
+
+def rel_l2(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+REF_KEYS = ('target_q_update_step', 'learning_rate', 'frame84')
+
+
+def build(algo, A, E, n, lives, seed, frames=48, use_graph=False, scale=4.0, **kw):
+    """An engine and an oracle from the same seed and initial parameters (stddev 0.02*scale)."""
+    from src.engine import Engine
+    from src.initializers import init_params, flatten_host
+    from src.kernels import param_names_shapes
+    eng = Engine(num_envs=E, n_step=n, action_size=A, algo=algo, start_lives=lives, num_frames=frames, seed=seed,
+                 use_graph=use_graph, **kw)
+    ns = param_names_shapes(A, algo)
+    p = init_params(ns, seed=seed, stddev=0.02 * scale)
+    eng.reset(flatten_host(ns, eng.offsets, eng.params.numel(), p))
+    ref = EngineRef(p, E, n, A, algo, lives, frames, seed, **{k: v for k, v in kw.items() if k in REF_KEYS})
+    ref.reset()
+    return eng, ref, ns
+
+
+def unflat(eng, ns, flat):
+    f = flat.cpu().numpy()
+    return {name: f[off:off + sz].reshape(shp) for (name, shp), off, sz in zip(ns, eng.offsets, eng.sizes)}
+
+
+def same_act_grads(slot, planes, P, algo, A, n, E, tgt):
+    """oracle loss + backward of one rollout on the engine's saved activations of that rollout
+    (slot: Engine.slot(k), or the engine itself in sync mode)."""
+    g = (lambda k: slot[k]) if isinstance(slot, dict) else (lambda k: getattr(slot, k))
+    B = n * E
+    l1 = g('act_l1').cpu().numpy().astype(np.float64).reshape(B, 20, 20, 16)
+    l2 = g('act_l2').cpu().numpy().astype(np.float64)
+    zw = A + 1 if algo == 'a3c' else A
+    z = g('z').cpu().numpy()[:n].reshape(B, -1)[:, :zw].astype(np.float64)
+    fwd = dict(z=z, h3=g('act_l3').cpu().numpy().astype(np.float64), flat=l2,
+               acts=[Rc.states_nhwc(planes).astype(np.float64) / 255.0, l1, l2.reshape(B, 9, 9, 32)])
+    acts = g('actions').cpu().numpy().reshape(-1)
+    if algo == 'a3c':
+        losses, dz = Rc.a3c_loss_and_dz(z, acts, tgt.reshape(-1).astype(np.float64), 0.01)
+    else:
+        loss, dz = Rc.q_loss_and_dz(z, acts, tgt.reshape(-1).astype(np.float64))
+        losses = dict(loss=loss)
+    gr = Rc.backward(P, fwd, dz, algo)
+    return losses, {k: np.asarray(v, np.float32).reshape(P[k].shape) for k, v in gr.items()}
+
+
+def rollout_planes(ref, n):
+    """[n*E,4,84,84] u8 states of the oracle's current rollout (b = t*E + e); call after
+    ref.iterate() (the states hold the frames the rollout produced) and before tau advances."""
+    return np.concatenate([np.transpose(ref.states(ref.tau + t), (0, 3, 1, 2)) for t in range(n)])
+
+
+def assert_losses(loss, ref_losses, algo, tag):
+    keys = ('policy', 'value', 'entropy', 'total') if algo == 'a3c' else ('loss',)
+    for i, k in enumerate(keys):
+        # sums of +- per-sample terms: 1e-4 of max(1, |sum|) (north star 1e-3)
+        assert abs(loss[i] - ref_losses[k]) <= 1e-4 * max(1.0, abs(ref_losses[k])), (tag, k, loss[i], ref_losses[k])
+
+
+def assert_params(eng, ns, ref, tag):
+    P = unflat(eng, ns, eng.params)
+    for name, _ in ns:
+        d = np.abs(P[name] - ref.params[name]).max()
+        assert d <= 1e-5 * max(1.0, np.abs(ref.params[name]).max()), (tag, name, d)
+
+
+def assert_env_state(eng, ref, tag):
+    for f, ref_v in (('frame', ref.env.frame), ('lives', ref.env.lives), ('episode', ref.env.episode),
+                     ('ep_step', ref.env.ep_step), ('ep_len', ref.env.ep_len)):
+        assert np.array_equal(eng.env_field(f).cpu().numpy(), ref_v.astype(np.int32)), (tag, f)
+
+
+def check_sync_vs_oracle(algo, A, E, n, lives, iters=3, seed=None, frames=48, scale=4.0, independent=True, **kw):
+    """Synchronous engine (rollout_grad + apply): every iteration against the oracle."""
+    seed = 123 + E if seed is None else seed
+    kw.setdefault('target_q_update_step', 40)
+    eng, ref, ns = build(algo, A, E, n, lives, seed=seed, frames=frames, scale=scale, **kw)
+    torch.cuda.synchronize()
+    assert np.array_equal(eng.env_frame.cpu().numpy(), ref.env.frame.astype(np.int32))
+    R = eng.ring_slots
+    ring = eng.frame_ring.cpu().numpy()
+    for c in range(4):
+        assert np.array_equal(ring[:, c % R], ref.ring[:, c % R])
+    for it in range(iters):
+        Pk = unflat(eng, ns, eng.params)          # the parameters this rollout runs with
+        eng.rollout_grad()
+        torch.cuda.synchronize()
+        acts = eng.actions.cpu().numpy()
+        out = ref.iterate(forced_actions=acts)
+        planes = rollout_planes(ref, n)           # after: the rollout's own frames are in the ring
+        agree = (acts == out['sampled']).mean()
+        assert agree >= 0.98, (it, agree)
+        assert np.array_equal(eng.rewards.cpu().numpy(), out['rewards']), it
+        assert np.array_equal(eng.terminals.cpu().numpy(), out['terminals']), it
+        gr = eng.frame_ring.cpu().numpy()
+        bad = [(e, sl) for e in range(E) for sl in range(R) if not np.array_equal(gr[e, sl], ref.ring[e, sl])]
+        assert not bad, (it, ref.tau, bad[:8])
+        tgt = eng.returns.cpu().numpy()
+        np.testing.assert_allclose(tgt, out['target'], rtol=1e-5, atol=1e-5)
+        assert_losses(eng.loss.cpu().numpy(), out['losses'], algo, it)
+        G = unflat(eng, ns, eng.grads)
+        # single GPU: the per-tensor clip is fused into apply, so after rollout_grad the buffer
+        # holds the raw gradient
+        _, g_same = same_act_grads(eng, planes, Pk, algo, A, n, E, tgt)
+        for name, _ in ns:
+            assert rel_l2(G[name], g_same[name]) < 1e-4, (it, name, rel_l2(G[name], g_same[name]))
+            if independent:     # fully independent fp64 oracle: ReLU-mask flips allowed
+                assert rel_l2(G[name], out['grads'][name]) < 2e-2, (it, name)
+        eng.apply()
+        torch.cuda.synchronize()
+        ss = eng.sumsq.cpu().numpy()
+        for i, (name, _) in enumerate(ns):
+            assert np.isclose(ss[i], np.sum(G[name].astype(np.float64) ** 2), rtol=1e-5), (it, name)
+        # the oracle optimizer consumes the same-mask gradients so the two parameter
+        # trajectories stay comparable at 1e-5 over iterations
+        ref.apply({k: Rc.clip_by_norm(v, 40.0) for k, v in g_same.items()})
+        assert_params(eng, ns, ref, it)
+        cnt = eng.counters.cpu().numpy()
+        assert cnt[0] == ref.tau and cnt[1] == ref.global_step
+        assert_env_state(eng, ref, it)
+        if algo == 'q':
+            T = unflat(eng, ns, eng.target_params)
+            for name, _ in ns:
+                np.testing.assert_allclose(T[name], ref.tparams[name], rtol=1e-5, atol=1e-6)
+    return eng, ref
+
+
+def check_overlap_vs_oracle(A, E, n, lives, rollouts=5, seed=77, frames=48, scale=4.0, **kw):
+    """Overlap (stale-1) pipeline: rollout k uses the parameters after update k-2.  The oracle is
+    replayed in that order with the engine's own actions and activations."""
+    algo = 'a3c'
+    eng, ref, ns = build(algo, A, E, n, lives, seed=seed, frames=frames, scale=scale, overlap=True, **kw)
+    hist = []                  # per rollout: (oracle params used, planes, oracle out)
+    for k in range(rollouts):
+        eng.iterate()
+        torch.cuda.synchronize()
+        sl = eng.slot(k & 1)
+        Pk = {kk: v.copy() for kk, v in ref.params.items()}
+        out = ref.iterate(forced_actions=sl['actions'].cpu().numpy())
+        planes = rollout_planes(ref, n)
+        ref.tau += n                                    # the rollout owns tau in overlap mode
+        assert np.array_equal(sl['rewards'].cpu().numpy(), out['rewards']), k
+        assert np.array_equal(sl['terminals'].cpu().numpy(), out['terminals']), k
+        ring = eng.frame_ring.cpu().numpy()            # the rollout's new screens, bit-exact
+        for t in range(n):
+            tt = ref.tau - n + t + 1
+            assert np.array_equal(ring[:, tt % eng.ring_slots], ref.ring[:, tt % ref.R]), (k, t)
+        agree = (sl['actions'].cpu().numpy() == out['sampled']).mean()
+        assert agree >= 0.98, (k, agree)
+        hist.append((Pk, planes, out))
+        if k == 0:
+            assert not eng.grad_ready
+            continue
+        Pp, planes_p, out_p = hist[k - 1]
+        slp = eng.slot((k - 1) & 1)
+        tgt = slp['returns'].cpu().numpy()
+        np.testing.assert_allclose(tgt, out_p['target'], rtol=1e-5, atol=1e-5)
+        losses, g_same = same_act_grads(slp, planes_p, Pp, algo, A, n, E, tgt)
+        assert_losses(eng.loss.cpu().numpy(), losses, algo, k)
+        G = unflat(eng, ns, eng.grads)
+        for name, _ in ns:
+            assert rel_l2(G[name], g_same[name]) < 1e-4, (k, name, rel_l2(G[name], g_same[name]))
+            assert rel_l2(G[name], out_p['grads'][name]) < 2e-2, (k, name)
+        ref.apply({kk: Rc.clip_by_norm(v, 40.0) for kk, v in g_same.items()}, advance_tau=False)
+        assert_params(eng, ns, ref, k)
+        assert int(eng.counters[1].item()) == ref.global_step
+    return eng, ref
+
+
+def check_hogwild1_vs_oracle(A, E, n, lives, iters=3, seed=91, frames=48, scale=4.0, **kw):
+    """Hogwild with one worker (src/hogwild.py at world 1): rollout + gradient, per-worker clip,
+    unlocked RMSProp push into the sharded PS, pull.  With one worker the push order is fixed, so
+    it must equal the oracle's clip + RMSProp step for step."""
+    from src.hogwild import HogwildPS
+    algo = 'a3c'
+    eng, ref, ns = build(algo, A, E, n, lives, seed=seed, frames=frames, scale=scale, **kw)
+    ps = HogwildPS(eng.params)
+    try:
+        for it in range(iters):
+            Pk = unflat(eng, ns, eng.params)
+            eng.iterate_hogwild(ps)
+            torch.cuda.synchronize()
+            out = ref.iterate(forced_actions=eng.actions.cpu().numpy())
+            planes = rollout_planes(ref, n)
+            assert np.array_equal(eng.rewards.cpu().numpy(), out['rewards']), it
+            assert np.array_equal(eng.terminals.cpu().numpy(), out['terminals']), it
+            tgt = eng.returns.cpu().numpy()
+            np.testing.assert_allclose(tgt, out['target'], rtol=1e-5, atol=1e-5)
+            losses, g_same = same_act_grads(eng, planes, Pk, algo, A, n, E, tgt)
+            assert_losses(eng.loss.cpu().numpy(), losses, algo, it)
+            clipped = {k: Rc.clip_by_norm(v, 40.0) for k, v in g_same.items()}
+            G = unflat(eng, ns, eng.grads)        # the engine's buffer holds the clipped gradient
+            for name, _ in ns:
+                assert rel_l2(G[name], clipped[name]) < 1e-4, (it, name)
+            ref.apply(clipped)
+            assert_params(eng, ns, ref, it)
+            assert torch.equal(ps.gather(), eng.params)
+            cnt = eng.counters.cpu().numpy()
+            assert cnt[0] == ref.tau and cnt[1] == ref.global_step
+    finally:
+        ps.close()
+    return eng, ref
