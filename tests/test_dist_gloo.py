@@ -1,11 +1,11 @@
-"""World-size-2 CPU (gloo) tests of the multi-GPU update paths (src/distributed.py).
+"""CPU (gloo) tests at world sizes 2, 4 and 8 of the multi-GPU update paths (src/distributed.py).
 
 Each rank runs the oracle iteration on its own env shard (env ids rank*E..) and clips per tensor
 (agent.py:319).  Then:
 * PartitionedPS (the default exchange): the real all-to-all / all-gather protocol drives a
   CPU stand-in of the engine's shard apply (oracle RMSProp on flat arrays).  The replicas must
-  stay bit-identical and equal ONE process applying rank 0's then rank 1's clipped gradient as
-  two RMSProp steps (EngineRef.apply_sequence) -- the reference PS's rule (main.py:63-65,
+  stay bit-identical and equal ONE process applying every rank's clipped gradient, in rank order,
+  as W RMSProp steps (EngineRef.apply_sequence) -- the reference PS's rule (main.py:63-65,
   agent.py:321) in rank order.
 * GradExchange (``--exchange sum``): SUM all-reduce, one step of the sum, for comparison.
 And, without processes: the summed single step is NOT the reference's W steps."""
@@ -36,16 +36,33 @@ def _setup_paths():
             sys.path.insert(0, p)
 
 
+def aligned_layout(ns, align=64):
+    """The engine's flat layout (include/a3c_hip.h a3c_param_layout): TF variable order, every
+    tensor 64-float aligned, total rounded up to 64 -- so the shard ranges below are the ones the
+    real engine exchanges (678,144 floats for Pong, 677,632 for Breakout, 1,203,456 with LSTM)."""
+    offs, off = [], 0
+    for _, shp in ns:
+        offs.append(off)
+        off = -(-(off + int(np.prod(shp))) // align) * align
+    return offs, off
+
+
 class _CpuShardEngine:
     """The engine's partitioned-PS interface (apply_shard / apply_commit) over an EngineRef:
-    flat float32 params / ms / mom in the oracle's name order, RMSProp from oracle/ref_cpu."""
+    flat float32 params / ms / mom in the engine's aligned layout, RMSProp from oracle/ref_cpu."""
 
-    def __init__(self, ref, names):
-        self.ref, self.names = ref, names
-        self.sizes = [ref.params[n].size for n in names]
-        self.flat = lambda d: np.concatenate([d[n].reshape(-1) for n in names]).astype(np.float32)
-        self.ms, self.mom = self.flat(ref.ms), self.flat(ref.mom)
+    def __init__(self, ref, ns):
+        self.ref, self.ns = ref, ns
+        self.offs, self.total = aligned_layout(ns)
+        self.ms, self.mom = self.flat(ref.ms, 1.0), self.flat(ref.mom)
         self.grads = None
+
+    def flat(self, d, pad=0.0):
+        out = np.full(self.total, pad, np.float32)
+        for (name, _), off in zip(self.ns, self.offs):
+            v = np.asarray(d[name], np.float32).reshape(-1)
+            out[off:off + v.size] = v
+        return out
 
     def set_grads(self, clipped):
         self.grads = torch.as_tensor(self.flat(clipped))
@@ -62,10 +79,9 @@ class _CpuShardEngine:
         w_out[:n] = torch.as_tensor(w)
 
     def apply_commit(self, gathered):
-        flat = gathered.numpy()[:sum(self.sizes)]
-        parts = np.split(flat, np.cumsum(self.sizes)[:-1])
-        for name, part in zip(self.names, parts):
-            self.ref.params[name] = part.reshape(self.ref.params[name].shape).astype(np.float32).copy()
+        flat = gathered.numpy()[:self.total]
+        for (name, shp), off in zip(self.ns, self.offs):
+            self.ref.params[name] = flat[off:off + int(np.prod(shp))].reshape(shp).astype(np.float32).copy()
         self.ref.finish_update()
 
 
@@ -78,48 +94,55 @@ def _init(rank, world, port):
     assert (r, w) == (rank, world)
 
 
-def _shared_start(rank):
+def _shared_start(rank, A=6, lstm=False):
     """Every rank starts from rank 0's parameters (broadcast, as main.py / bench.py do)."""
     from src.distributed import broadcast_params
     from src.initializers import init_params
     from src.kernels import param_names_shapes
-    ns = param_names_shapes(6, 'a3c')
+    ns = param_names_shapes(A, 'a3c', lstm=lstm)
     p = init_params(ns, seed=5 + rank, stddev=0.08)       # different on purpose: broadcast fixes it
     names = [n for n, _ in ns]
     flat = torch.cat([torch.as_tensor(p[n]).reshape(-1) for n in names])
     broadcast_params(flat, src=0)
     sizes = [int(np.prod(s)) for _, s in ns]
     parts = torch.split(flat, sizes)
-    return {n: parts[i].reshape(s).numpy().copy() for i, (n, s) in enumerate(ns)}, names
+    return {n: parts[i].reshape(s).numpy().copy() for i, (n, s) in enumerate(ns)}, ns
 
 
-def _worker_partitioned(rank, world, port, out):
+def _ref(p, rank, world, cfg):
+    from oracle.engine_ref import EngineRef
+    E = cfg.get('E', 3)
+    ref = EngineRef(p, E, 2, cfg.get('A', 6), 'a3c', cfg.get('lives', 0), 16, seed=9, env_id_base=rank * E,
+                    world_size=world, lstm=cfg.get('lstm', False))
+    ref.reset()
+    return ref
+
+
+def _worker_partitioned(rank, world, port, out, cfg):
     _init(rank, world, port)
     from src.distributed import PartitionedPS
-    from oracle.engine_ref import EngineRef
-    p, names = _shared_start(rank)
-    ref = EngineRef(p, 3, 2, 6, 'a3c', 0, 16, seed=9, env_id_base=rank * 3, world_size=world)
-    ref.reset()
-    eng = _CpuShardEngine(ref, names)
-    ps = PartitionedPS(sum(ref.params[n].size for n in names), device='cpu')
+    p, ns = _shared_start(rank, cfg.get('A', 6), cfg.get('lstm', False))
+    ref = _ref(p, rank, world, cfg)
+    eng = _CpuShardEngine(ref, ns)
+    ps = PartitionedPS(eng.total, device='cpu')
     mine = []
-    for it in range(3):
+    for it in range(cfg.get('iters', 3)):
         o = ref.iterate()
         eng.set_grads(o['clipped'])
         mine.append(eng.grads.numpy().copy())
         ps.apply(eng)
-    out[rank] = dict(params=eng.flat(ref.params), grads=mine, ms=eng.ms.copy(), lo=ps.lo, n=ps.n)
+    out[rank] = dict(params=eng.flat(ref.params), grads=mine, ms=eng.ms.copy(), lo=ps.lo, n=ps.n,
+                     step=ref.global_step)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _worker_sum(rank, world, port, out):
+def _worker_sum(rank, world, port, out, cfg):
     _init(rank, world, port)
     from src.distributed import GradExchange
-    from oracle.engine_ref import EngineRef
-    p, names = _shared_start(rank)
-    ref = EngineRef(p, 3, 2, 6, 'a3c', 0, 16, seed=9, env_id_base=rank * 3, world_size=world)
-    ref.reset()
+    p, ns = _shared_start(rank)
+    names = [n for n, _ in ns]
+    ref = _ref(p, rank, world, cfg)
     xch = GradExchange()
     for it in range(2):
         o = ref.iterate()
@@ -132,44 +155,68 @@ def _worker_sum(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def _spawn(fn, world=2):
+def _spawn(fn, world=2, cfg=None):
     port = _free_port()
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(fn, args=(world, port, out), nprocs=world, join=True)
+        mp.spawn(fn, args=(world, port, out, dict(cfg or {})), nprocs=world, join=True)
         return dict(out)
 
 
-def _replay(world, iters, combine):
+def _replay(world, iters, combine, cfg=None):
     """Single process: every shard's EngineRef from rank 0's parameters, combine(refs, outs)."""
     _setup_paths()
     from src.initializers import init_params
     from src.kernels import param_names_shapes
-    from oracle.engine_ref import EngineRef
-    ns = param_names_shapes(6, 'a3c')
+    cfg = dict(cfg or {})
+    ns = param_names_shapes(cfg.get('A', 6), 'a3c', lstm=cfg.get('lstm', False))
     names = [n for n, _ in ns]
     p = init_params(ns, seed=5, stddev=0.08)               # rank 0's params (broadcast source)
-    refs = [EngineRef(p, 3, 2, 6, 'a3c', 0, 16, seed=9, env_id_base=r * 3, world_size=world) for r in range(world)]
-    for r in refs:
-        r.reset()
+    refs = [_ref(p, r, world, cfg) for r in range(world)]
     for _ in range(iters):
         combine(refs, [r.iterate() for r in refs], names)
-    return np.concatenate([refs[0].params[n].reshape(-1) for n in names])
+    return refs[0], ns
+
+
+def _check_partitioned(world, cfg):
+    res = _spawn(_worker_partitioned, world, cfg)
+    for r in range(1, world):
+        assert np.array_equal(res[0]['params'], res[r]['params']), r           # replicas identical
+    assert not np.allclose(res[0]['grads'][0], res[1]['grads'][0])             # different shards, grads
+    lo, n = res[0]['lo'], res[0]['n']
+    total = res[0]['params'].size
+    assert sum(n) == total and all(lo[r + 1] == lo[r] + n[r] for r in range(world - 1))
+    assert all(x % 64 == 0 for x in lo)
+
+    def sequential(refs, outs, names):
+        for r in refs:
+            r.apply_sequence([o['clipped'] for o in outs])             # rank 0's step, then rank 1's, ...
+    ref0, ns = _replay(world, cfg.get('iters', 3), sequential, cfg)
+    np.testing.assert_array_equal(res[0]['params'], _CpuShardEngine(ref0, ns).flat(ref0.params))
+    assert res[0]['step'] == ref0.global_step
+    return res
 
 
 @pytest.mark.timeout(300)
 def test_gloo_two_rank_partitioned_ps_is_the_reference_ps_rule():
-    world = 2
-    res = _spawn(_worker_partitioned, world)
-    assert np.array_equal(res[0]['params'], res[1]['params'])           # replicas identical
-    assert not np.allclose(res[0]['grads'][0], res[1]['grads'][0])      # different shards, grads
-    assert res[0]['lo'] == [0, res[0]['n'][0]] and sum(res[0]['n']) == res[0]['params'].size
+    _check_partitioned(2, {})
 
-    def sequential(refs, outs, names):
-        for r in refs:
-            r.apply_sequence([o['clipped'] for o in outs])             # rank 0's step, then rank 1's
-    flat = _replay(world, 3, sequential)
-    np.testing.assert_array_equal(res[0]['params'], flat)
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('cfg', [dict(A=6), dict(A=4, lives=5)], ids=['pong', 'breakout'])
+def test_gloo_eight_rank_partitioned_ps_is_the_reference_ps_rule(cfg):
+    """BASELINE configs 3/4 are 8-GPU runs: 8 ranks, 8 sequential RMSProp steps per range, and
+    the last 64-aligned range ragged (Pong: 7 x 84,800 + 84,544 of 678,144 floats; Breakout:
+    7 x 84,736 + 84,480 of 677,632)."""
+    res = _check_partitioned(8, dict(cfg, iters=2))
+    n = res[0]['n']
+    assert n[-1] < n[0] and len(set(n[:-1])) == 1
+
+
+@pytest.mark.timeout(600)
+def test_gloo_four_rank_partitioned_ps_lstm_head():
+    """C5 (LSTM head, 1,203,456 floats) through the same exchange at world 4."""
+    _check_partitioned(4, dict(A=6, lives=3, lstm=True, iters=2))
 
 
 @pytest.mark.timeout(300)
@@ -182,7 +229,9 @@ def test_gloo_two_rank_sum_exchange():
         s = {n: sum(o['clipped'][n] for o in outs).astype(np.float32) for n in names}
         for r in refs:
             r.apply(s)
-    np.testing.assert_allclose(res[0]['params'], _replay(world, 2, summed), rtol=1e-6, atol=1e-9)
+    ref0, ns = _replay(world, 2, summed)
+    flat = np.concatenate([ref0.params[n].reshape(-1) for n, _ in ns])
+    np.testing.assert_allclose(res[0]['params'], flat, rtol=1e-6, atol=1e-9)
 
 
 def test_summed_step_is_not_the_reference_ps_rule():
