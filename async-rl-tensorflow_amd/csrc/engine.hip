@@ -102,6 +102,9 @@ struct a3c_engine {
   int ext_t;               // next rollout step (0..n; n: ready for rollout_grad)
   bool ext_begun;          // a3c_engine_ext_begin done since reset
   int32_t* ext_idx;        // [E] identity frame index into the staging buffer (pool)
+  std::vector<uint8_t> ext_sent;   // [E] env frame sent by a3c_engine_ext_upload this step
+  int ext_nsent;                   // envs marked in ext_sent
+  bool ext_acted;                  // ext_act of step ext_t issued, its ext_observe not yet
   int64_t iter;            // rollouts issued since reset
   bool grad_ready;         // the last rollout_grad call computed a gradient
   bool grad_applied;       // ... and a3c_engine_iterate already applied it (apply is then a no-op)
@@ -752,6 +755,7 @@ extern "C" int a3c_engine_reset(a3c_engine* e, const float* host_params, void* s
   e->reset_done = true;
   e->ext_t = 0;
   e->ext_begun = false;
+  e->ext_acted = false;
   return 0;
 }
 
@@ -911,6 +915,7 @@ extern "C" int a3c_engine_ext_begin(a3c_engine* e, const uint8_t* rgb, void* str
   if (rc) return rc;
   e->ext_begun = true;
   e->ext_t = 0;
+  e->ext_acted = false;
   return 0;
 }
 
@@ -918,8 +923,9 @@ extern "C" int a3c_engine_ext_begin(a3c_engine* e, const uint8_t* rgb, void* str
 // (host, pinned for a true async copy, or device), valid once the stream reaches this point
 extern "C" int a3c_engine_ext_act(a3c_engine* e, int32_t* actions, void* stream) {
   if (int rc = ext_check(e, "a3c_engine_ext_act")) return rc;
-  if (!e->ext_begun || e->ext_t >= e->n || !actions)
-    return a3c_set_error(A3C_ERR_STATE, "a3c_engine_ext_act", "ext_begin first; at most n steps per rollout");
+  if (!e->ext_begun || e->ext_t >= e->n || e->ext_acted || !actions)
+    return a3c_set_error(A3C_ERR_STATE, "a3c_engine_ext_act",
+                         "ext_begin first; one ext_observe per ext_act; at most n steps per rollout");
   hipStream_t s = (hipStream_t)stream;
   const Slot& sl = e->slot[0];
   if (e->ext_t == 0) {
@@ -929,6 +935,9 @@ extern "C" int a3c_engine_ext_act(a3c_engine* e, int32_t* actions, void* stream)
   int rc = enqueue_step(e, sl, e->ext_t, s);
   if (rc) return rc;
   A3C_CHECK(hipMemcpyAsync(actions, sl.actions + (int64_t)e->ext_t * e->E, (size_t)e->E * 4, hipMemcpyDefault, s));
+  e->ext_sent.assign(e->E, 0);          // the step's uploads start empty
+  e->ext_nsent = 0;
+  e->ext_acted = true;
   return 0;
 }
 
@@ -937,7 +946,7 @@ extern "C" int a3c_engine_ext_act(a3c_engine* e, int32_t* actions, void* stream)
 // the next; a3c_engine_ext_observe(rgb = NULL, ...) then completes the step
 extern "C" int a3c_engine_ext_upload(a3c_engine* e, const uint8_t* rgb, int env_lo, int env_hi, void* stream) {
   if (int rc = ext_check(e, "a3c_engine_ext_upload")) return rc;
-  if (!e->ext_begun || e->ext_t >= e->n || !rgb)
+  if (!e->ext_begun || !e->ext_acted || !rgb)
     return a3c_set_error(A3C_ERR_STATE, "a3c_engine_ext_upload", "ext_act of this step first");
   if (env_lo < 0 || env_hi > e->E || env_lo > env_hi)
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_ext_upload", "env range outside [0, num_envs]");
@@ -945,18 +954,26 @@ extern "C" int a3c_engine_ext_upload(a3c_engine* e, const uint8_t* rgb, int env_
   if (env_hi > env_lo)
     A3C_CHECK(hipMemcpyAsync(e->pool + env_lo * fb, rgb + env_lo * fb, (size_t)(env_hi - env_lo) * fb,
                              hipMemcpyDefault, (hipStream_t)stream));
+  for (int i = env_lo; i < env_hi; ++i) {
+    e->ext_nsent += !e->ext_sent[i];
+    e->ext_sent[i] = 1;
+  }
   return 0;
 }
 
 // observe of rollout step t: the post-act RGB frames [E][210][160][3] u8, rewards [E] f32 and
 // terminals [E] u8 of every env (GymEnvironment.act, environment.py:78-96, done on the host) ->
 // reward clip (agent.py:154), Environment.screen + History.add into the frame ring
-// rgb == NULL: the frames of every env were already sent by a3c_engine_ext_upload this step.
+// rgb == NULL: the frames of every env were already sent by a3c_engine_ext_upload this step
+// (checked: the step's uploaded ranges must cover [0, E), else the screen would read stale frames).
 extern "C" int a3c_engine_ext_observe(a3c_engine* e, const uint8_t* rgb, const float* rewards,
                                       const uint8_t* terminals, void* stream) {
   if (int rc = ext_check(e, "a3c_engine_ext_observe")) return rc;
-  if (!e->ext_begun || e->ext_t >= e->n || !rewards || !terminals)
+  if (!e->ext_begun || !e->ext_acted || !rewards || !terminals)
     return a3c_set_error(A3C_ERR_STATE, "a3c_engine_ext_observe", "ext_act of this step first");
+  if (!rgb && e->ext_nsent != e->E)
+    return a3c_set_error(A3C_ERR_STATE, "a3c_engine_ext_observe",
+                         "rgb == NULL but ext_upload did not send every env's frame this step");
   hipStream_t s = (hipStream_t)stream;
   const Slot& sl = e->slot[0];
   const int E = e->E, t = e->ext_t;
@@ -969,6 +986,7 @@ extern "C" int a3c_engine_ext_observe(a3c_engine* e, const uint8_t* rgb, const f
   int rc = a3c_env_screen_launch(E, e->ext_idx, e->pool, e->ring, e->R, e->counters, t, s);
   if (rc) return rc;
   e->ext_t = t + 1;
+  e->ext_acted = false;
   return 0;
 }
 

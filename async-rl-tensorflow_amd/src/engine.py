@@ -266,14 +266,18 @@ class Engine:
         if not t.is_cuda and not t.is_pinned():
             raise ValueError(f'{name}: host buffers must be pinned (async copies)')
 
-    def iterate_host(self, pool, exchange=None):
-        """One iteration with host-stepped envs (src/host_env.HostEnvPool): per rollout step the
-        GPU draws the actions, the host steps every env, the post-act frames go back to the GPU
-        for Environment.screen + History.add; then loss, backward, exchange, apply."""
+    def begin_host(self, pool):
+        """New random games of every host env; their first screens fill the history (ext_begin)."""
+        self.ext_begin(pool.begin())
+        self._ext_began = True
+        self._ext_actions = torch.zeros(self.E, dtype=torch.int32).pin_memory()
+
+    def rollout_host(self, pool):
+        """The n env steps of one iteration with host-stepped envs (src/host_env.HostEnvPool): per
+        rollout step the GPU draws the actions, the host steps every env, the post-act frames go
+        back to the GPU for Environment.screen + History.add.  Finish with rollout_grad()."""
         if not getattr(self, '_ext_began', False):
-            self.ext_begin(pool.begin())
-            self._ext_began = True
-            self._ext_actions = torch.zeros(self.E, dtype=torch.int32).pin_memory()
+            self.begin_host(pool)
         stream = torch.cuda.current_stream()
         # pools that step env ranges (SyntheticHostEnvPool) are stepped in `upload_chunks` ranges:
         # the H2D copy of one range runs while the host steps the next
@@ -291,6 +295,10 @@ class Engine:
                 pool.step_range(acts, lo, hi)
                 self.ext_upload(pool.rgb, lo, hi)
             self.ext_observe(None, pool.rewards, pool.terminals)
+
+    def iterate_host(self, pool, exchange=None):
+        """One iteration with host-stepped envs: rollout_host, then loss, backward, exchange, apply."""
+        self.rollout_host(pool)
         self.rollout_grad()
         if getattr(exchange, 'owns_apply', False):
             exchange.apply(self)

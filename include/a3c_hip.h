@@ -351,7 +351,8 @@ int a3c_engine_ext_act(a3c_engine* eng, int32_t* actions, void* stream);
 int a3c_engine_ext_observe(a3c_engine* eng, const uint8_t* rgb, const float* rewards, const uint8_t* terminals,
                            void* stream);
 /* part of observe (same step, before it): frames of envs [env_lo, env_hi) only, so the copy of
- * one range overlaps the host stepping of the next; observe is then called with rgb = NULL */
+ * one range overlaps the host stepping of the next; observe is then called with rgb = NULL, which
+ * fails with A3C_ERR_STATE unless the step's ranges covered every env in [0, E) */
 int a3c_engine_ext_upload(a3c_engine* eng, const uint8_t* rgb, int env_lo, int env_hi, void* stream);
 
 /* Host-side batched synthetic env (the device env's emulator, bit-identical dynamics, stepped by

@@ -29,11 +29,13 @@ REF_KEYS = ('target_q_update_step', 'learning_rate', 'frame84')
 
 
 def build(algo, A, E, n, lives, seed, frames=48, use_graph=False, scale=4.0, **kw):
-    """An engine and an oracle from the same seed and initial parameters (stddev 0.02*scale)."""
+    """An engine and an oracle from the same seed and initial parameters (stddev 0.02*scale).
+    external_env=True: the engine's frames come from host-stepped envs (no device frame pool)."""
     from src.engine import Engine
     from src.initializers import init_params, flatten_host
     from src.kernels import param_names_shapes
-    eng = Engine(num_envs=E, n_step=n, action_size=A, algo=algo, start_lives=lives, num_frames=frames, seed=seed,
+    eng_frames = 1 if kw.get('external_env') else frames
+    eng = Engine(num_envs=E, n_step=n, action_size=A, algo=algo, start_lives=lives, num_frames=eng_frames, seed=seed,
                  use_graph=use_graph, **kw)
     ns = param_names_shapes(A, algo)
     p = init_params(ns, seed=seed, stddev=0.02 * scale)
@@ -95,19 +97,31 @@ def assert_env_state(eng, ref, tag):
         assert np.array_equal(eng.env_field(f).cpu().numpy(), ref_v.astype(np.int32)), (tag, f)
 
 
-def check_sync_vs_oracle(algo, A, E, n, lives, iters=3, seed=None, frames=48, scale=4.0, independent=True, **kw):
-    """Synchronous engine (rollout_grad + apply): every iteration against the oracle."""
+def check_sync_vs_oracle(algo, A, E, n, lives, iters=3, seed=None, frames=48, scale=4.0, independent=True,
+                         host_pool=None, **kw):
+    """Synchronous engine (rollout_grad + apply): every iteration against the oracle.
+    host_pool(seed): a host env pool factory -- the engine then runs with external_env and its
+    n env steps are driven by Engine.rollout_host."""
     seed = 123 + E if seed is None else seed
     kw.setdefault('target_q_update_step', 40)
+    pool = None
+    if host_pool is not None:
+        kw['external_env'] = True
     eng, ref, ns = build(algo, A, E, n, lives, seed=seed, frames=frames, scale=scale, **kw)
+    if host_pool is not None:
+        pool = host_pool(seed)
+        eng.begin_host(pool)
     torch.cuda.synchronize()
-    assert np.array_equal(eng.env_frame.cpu().numpy(), ref.env.frame.astype(np.int32))
+    if pool is None:
+        assert np.array_equal(eng.env_frame.cpu().numpy(), ref.env.frame.astype(np.int32))
     R = eng.ring_slots
     ring = eng.frame_ring.cpu().numpy()
     for c in range(4):
         assert np.array_equal(ring[:, c % R], ref.ring[:, c % R])
     for it in range(iters):
         Pk = unflat(eng, ns, eng.params)          # the parameters this rollout runs with
+        if pool is not None:
+            eng.rollout_host(pool)
         eng.rollout_grad()
         torch.cuda.synchronize()
         acts = eng.actions.cpu().numpy()
@@ -142,11 +156,14 @@ def check_sync_vs_oracle(algo, A, E, n, lives, iters=3, seed=None, frames=48, sc
         assert_params(eng, ns, ref, it)
         cnt = eng.counters.cpu().numpy()
         assert cnt[0] == ref.tau and cnt[1] == ref.global_step
-        assert_env_state(eng, ref, it)
+        if pool is None:
+            assert_env_state(eng, ref, it)
         if algo == 'q':
             T = unflat(eng, ns, eng.target_params)
             for name, _ in ns:
                 np.testing.assert_allclose(T[name], ref.tparams[name], rtol=1e-5, atol=1e-6)
+    if pool is not None:
+        pool.close()
     return eng, ref
 
 

@@ -67,6 +67,41 @@ def test_batched_env_matches_oracle(game, repeat, training):
             ref.new_random_game(tt.copy())
 
 
+def test_batched_env_matches_reference_act_rule(golden_dir):
+    """The device env (a3c_env_*: the same act / new_random_game code the engine's head kernels
+    inline) against the reference's own GymEnvironment driving the synthetic emulator's primitives
+    (tests/golden/synth_env_golden.npz, environment.py:28-96 + agent.py:66-67): frame id, reward,
+    terminal and lives after every call."""
+    from src.environment import BatchedEnvironment
+    g = np.load(f'{golden_dir}/synth_env_golden.npz')
+    for i, (game, c) in enumerate(zip(g['games'], g['cases'])):
+        seed, env_id, P, rep, rs, training, _ = (int(x) for x in c)
+        cfg = make_config(str(game), action_repeat=rep, random_start=rs)
+        env = BatchedEnvironment(cfg, num_envs=1, env_id_base=env_id, seed=seed, num_frames=P)
+        tr = g[f'trace{i}']
+        env.new_random_game()
+        k = 0
+
+        def check(row, r=None, t=None):
+            torch.cuda.synchronize()
+            assert int(env._frame.cpu()[0]) == int(row[1]), (i, k, row)
+            assert int(env.lives_all.cpu()[0]) == int(row[4]), (i, k, row)
+            if r is not None:
+                assert float(r.cpu()[0]) == row[2] and int(t.cpu()[0]) == int(row[3]), (i, k, row)
+        check(tr[0])
+        k = 1
+        for a in g[f'actions{i}']:
+            _, r, t = env.act(torch.tensor([a], dtype=torch.int32), is_training=bool(training))
+            assert tr[k, 0] == 1
+            check(tr[k], r, t)
+            k += 1
+            if int(t.cpu()[0]):
+                env.new_random_game(torch.ones(1, dtype=torch.uint8, device='cuda'))
+                check(tr[k])
+                k += 1
+        assert k == len(tr)
+
+
 def test_simple_env_and_single_env_wrappers():
     from src.environment import BatchedEnvironment, GymEnvironment, SimpleGymEnvironment, game_spec
     with pytest.raises(ValueError):

@@ -1,8 +1,15 @@
-"""Host-stepped envs feeding the engine (a3c_engine_ext_*, src/host_env.py): with
-the synthetic emulator stepped on the HOST (oracle/synthetic_env.py, one object per env, raw RGB
-frames through pinned buffers), the external-env engine must reproduce the device-env engine bit
-for bit: same actions, rewards, terminals, frame ring (Environment.screen of the uploaded frames),
-and the same losses and parameters."""
+"""Host-stepped envs feeding the engine (a3c_engine_ext_*, src/host_env.py).
+
+With the synthetic emulator stepped on the HOST (oracle/synthetic_env.py one object per env, or the
+C++ worker threads of a3c_hostenv_*, raw RGB frames through pinned buffers):
+* the external-env engine is checked against the CPU replay oracle (oracle/engine_ref.py) directly,
+  at the bar of tests/_engine_parity.py (frames, rewards, terminals bit-exact; returns, losses,
+  gradients, parameters to fp tolerance), including the headline shape (256 envs) with chunked
+  uploads;
+* and it reproduces the device-env engine bit for bit (same actions, rewards, terminals, frame
+  ring, losses and parameters).
+The synthetic env's act / life-loss / no-op rule itself is pinned to the reference's own
+GymEnvironment code by tests/golden/synth_env_golden.npz (tests/test_host_env.py)."""
 import numpy as np
 import pytest
 
@@ -11,6 +18,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip('torch')
 
 from oracle.synthetic_env import SyntheticAtari, pool_frame  # noqa: E402
+from _engine_parity import check_sync_vs_oracle  # noqa: E402
 
 
 class HostSynthEnv:
@@ -68,6 +76,25 @@ def test_external_envs_equal_device_envs(algo, A, E, n, lives, lstm):
     pool.close()
 
 
+@pytest.mark.parametrize('algo,A,E,n,lives,P,kind', [
+    ('a3c', 6, 8, 5, 3, 40, 'py'), ('a3c', 4, 7, 3, 5, 40, 'py'), ('q', 6, 4, 6, 3, 40, 'py'),
+    ('a3c', 6, 13, 5, 3, 64, 'cpp3'), ('a3c', 6, 256, 5, 0, 512, 'cpp2'), ('a3c', 4, 256, 5, 5, 512, 'cpp2')],
+    ids=['a3c-py', 'breakout-py', 'q-py', 'a3c-cpp-3ranges', 'pong256-cpp-2ranges', 'breakout256-cpp-2ranges'])
+def test_external_envs_match_oracle(algo, A, E, n, lives, P, kind):
+    """The external-env engine (Engine.rollout_host + rollout_grad + apply) against EngineRef: the
+    host envs are either Python objects (HostEnvPool of per-env oracle emulators) or the C++ worker
+    threads stepping env ranges whose frames go up by a3c_engine_ext_upload while the next range
+    steps (SyntheticHostEnvPool, `upload_chunks` ranges)."""
+    from src.host_env import HostEnvPool, SyntheticHostEnvPool
+
+    def pool(seed):
+        if kind == 'py':
+            return HostEnvPool([HostSynthEnv(seed, e, P, A, lives) for e in range(E)], threads=2)
+        return SyntheticHostEnvPool(E, A, lives, num_frames=P, seed=seed, threads=4, upload_chunks=int(kind[-1]))
+    check_sync_vs_oracle(algo, A, E, n, lives, iters=3, seed=500 + E, frames=P, host_pool=pool,
+                         learning_rate=2e-3)
+
+
 def test_external_env_call_order_enforced():
     from src.engine import Engine
     ext = Engine(num_envs=2, n_step=2, action_size=6, external_env=True, num_frames=1)
@@ -115,5 +142,17 @@ def test_ext_upload_checks():
     ext.ext_act(torch.zeros(3, dtype=torch.int32).pin_memory())
     with pytest.raises(RuntimeError):
         ext.ext_upload(rgb, 2, 4)               # range outside [0, E]
-    ext.ext_upload(rgb, 0, 3)
+    ext.ext_upload(rgb, 0, 2)
+    r = torch.zeros(3, dtype=torch.float32).pin_memory()
+    t = torch.zeros(3, dtype=torch.uint8).pin_memory()
+    with pytest.raises(RuntimeError):
+        ext.ext_observe(None, r, t)             # env 2's frame was never sent this step
+    ext.ext_upload(rgb, 1, 3)                   # overlapping ranges: [0, 3) covered
+    ext.ext_observe(None, r, t)
+    with pytest.raises(RuntimeError):
+        ext.ext_upload(rgb, 0, 3)               # observe closed the step: ext_act first
+    ext.ext_act(torch.zeros(3, dtype=torch.int32).pin_memory())
+    with pytest.raises(RuntimeError):
+        ext.ext_act(torch.zeros(3, dtype=torch.int32).pin_memory())    # one observe per act
+    ext.ext_observe(rgb, r, t)
     torch.cuda.synchronize()
