@@ -33,7 +33,8 @@ struct Slot {
   int64_t* tau;            // tau at rollout start (sync: the live counter)
   int32_t* actions;        // [n][E]
   int32_t* frames;         // [n][E] post-act frame index per step
-  float* rewards;          // [n][E]
+  float* rewards;          // [n][E] observe-clipped (agent.py:154)
+  float* rewards_raw;      // [n][E] unclipped act() rewards (the summaries' sums, agent.py:91-100)
   uint8_t* terms;          // [n][E]
   float* z;                // [(n+1)][E][zs]
   float* R_buf;            // [n][E] returns / TD targets
@@ -81,6 +82,8 @@ struct a3c_engine {
   float* ldh;              // LSTM: dL/dh_t from the heads [nE][U]
   double* opt_part;
   float* sched;            // [0] lr, [1] target-sync flag (device)
+  double* stats;           // [A3C_STATS_N] train_with_summary aggregates since the last read
+  double* ep_acc;          // [E] running episode reward per env (agent.py:91-98)
   TensorTab tt;
   // sync: one graph (rollout + grad); overlap: rollout and grad graphs per slot
   hipGraph_t graph[NGRAPH];
@@ -106,6 +109,7 @@ struct a3c_engine {
   int ext_nsent;                   // envs marked in ext_sent
   bool ext_acted;                  // ext_act of step ext_t issued, its ext_observe not yet
   int64_t iter;            // rollouts issued since reset
+  int64_t step0_g, step0_w;   // global / worker step the counters start from (a3c_engine_set_step)
   bool grad_ready;         // the last rollout_grad call computed a gradient
   bool grad_applied;       // ... and a3c_engine_iterate already applied it (apply is then a no-op)
   bool reset_done;
@@ -260,6 +264,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     ALLOC(sl.actions, nE * 4);
     ALLOC(sl.frames, nE * 4);
     ALLOC(sl.rewards, nE * 4);
+    ALLOC(sl.rewards_raw, nE * 4);
     ALLOC(sl.terms, nE);
     ALLOC(sl.z, (nE + E) * zs * 4);
     ALLOC(sl.R_buf, nE * 4);
@@ -294,6 +299,8 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   ALLOC(e->fcpart, (int64_t)FC_NS * E * FC * 4);
   ALLOC(e->opt_part, (int64_t)SS_MAX_BLOCKS * 8);
   ALLOC(e->sched, 64);
+  ALLOC(e->stats, A3C_STATS_N * 8);
+  ALLOC(e->ep_acc, E * 8);
 #undef ALLOC
   if (a3c_make_tab(L.nt, L.off, L.size, L.total, &e->tt)) {
     a3c_engine_destroy(e);
@@ -363,13 +370,80 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
 }
 
 // ---- small device kernels -------------------------------------------------------------------
+// ---- train_with_summary aggregates (agent.py:69-139) ----------------------------------------
+// stats: [0] sum of act() rewards over env-steps, [1] sum / [2] max / [3] min of finished episodes'
+// rewards, [4] games, [5] sum of per-update loss (per sample), [6] sum of per-update mean Q(s) (q:
+// over actions; a3c: V(s)), [7] updates, [8] env-steps, [9..11] sums of per-sample policy / value
+// loss and entropy (a3c)
+__global__ void k_stats_reset(double* st) {
+  const int i = threadIdx.x;
+  if (i < A3C_STATS_N) st[i] = i == 2 ? -INFINITY : (i == 3 ? INFINITY : 0.0);
+}
+
+// one update's rollout (n steps of E envs), in the reference chief's order per env: the episode
+// reward excludes the terminal step's reward and restarts after it (agent.py:91-98); total reward
+// includes every step (agent.py:101).  One workgroup, fixed-order tree reductions: deterministic.
+__global__ void __launch_bounds__(256) k_stats(const float* __restrict__ rraw, const uint8_t* __restrict__ terms,
+                                               const float* __restrict__ z, int zs, int A, int q, int n, int E,
+                                               const float* __restrict__ loss, double* __restrict__ ep_acc,
+                                               double* __restrict__ st) {
+  __shared__ double red[6][256];
+  double tr = 0.0, es = 0.0, emax = -INFINITY, emin = INFINITY, games = 0.0, qs = 0.0;
+  for (int e = threadIdx.x; e < E; e += 256) {
+    double acc = ep_acc[e];
+    for (int t = 0; t < n; ++t) {
+      const int64_t b = (int64_t)t * E + e;
+      const double r = rraw[b];
+      tr += r;
+      if (terms[b]) {
+        games += 1.0; es += acc; emax = fmax(emax, acc); emin = fmin(emin, acc);
+        acc = 0.0;
+      } else {
+        acc += r;
+      }
+      const float* zr = z + b * zs;
+      if (q) {
+        double m = 0.0;
+        for (int a = 0; a < A; ++a) m += zr[a];
+        qs += m / A;
+      } else {
+        qs += zr[A];
+      }
+    }
+    ep_acc[e] = acc;
+  }
+  const int i = threadIdx.x;
+  red[0][i] = tr; red[1][i] = es; red[2][i] = emax; red[3][i] = emin; red[4][i] = games; red[5][i] = qs;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (i < o) {
+      red[0][i] += red[0][i + o]; red[1][i] += red[1][i + o];
+      red[2][i] = fmax(red[2][i], red[2][i + o]); red[3][i] = fmin(red[3][i], red[3][i + o]);
+      red[4][i] += red[4][i + o]; red[5][i] += red[5][i + o];
+    }
+    __syncthreads();
+  }
+  if (i == 0) {
+    const double B = (double)n * E;
+    st[0] += red[0][0]; st[1] += red[1][0];
+    st[2] = fmax(st[2], red[2][0]); st[3] = fmin(st[3], red[3][0]);
+    st[4] += red[4][0];
+    st[5] += q ? (double)loss[0] : (double)loss[3] / B;
+    st[6] += red[5][0] / B;
+    st[7] += 1.0;
+    st[8] += B;
+    if (!q) { st[9] += (double)loss[0] / B; st[10] += (double)loss[1] / B; st[11] += (double)loss[2] / B; }
+  }
+}
+
 __global__ void k_eps(float* __restrict__ eps, const float* __restrict__ ep_end, int E,
-                      const int64_t* __restrict__ counters, float ep_start, int64_t ep_end_t,
+                      const int64_t* __restrict__ counters, int t, float ep_start, int64_t ep_end_t,
                       int64_t learn_start) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= E) return;
-  // agent.py:142-144
-  const double step = (double)counters[1];
+  // agent.py:142-144 at the worker's own step (agent.py:55 loop counter): the workers' base step
+  // plus the env steps taken so far (tau - (HIST-1)) plus rollout step t
+  const double step = (double)(counters[2] + counters[0] - (HIST - 1) + t);
   const double ee = ep_end[i];
   double d = (double)ep_end_t - fmax(0.0, step - (double)learn_start);
   double v = ee + fmax(0.0, ((double)ep_start - ee) * d / (double)ep_end_t);
@@ -401,13 +475,19 @@ static bool fc_split(const a3c_engine* e) { return conv_fused(e) && e->fc_split 
 
 __global__ void k_advance_tau(int64_t* counters, int n) { counters[0] += n; }
 
-static OptParams opt_params(const a3c_engine* e) {
+// optimizer parameters of the update of the rollout in slot sl (its tau gives the worker step of
+// the lr schedule, OptParams)
+static OptParams opt_params(const a3c_engine* e, const Slot& sl) {
   const a3c_engine_config& c = e->cfg;
   OptParams op = {};
   op.clip = c.clip_norm;
   op.sched = e->sched;
   op.step_ptr = e->counters + 1;
   op.step_add = e->nE * c.world_size;
+  op.wstep_ptr = e->counters + 2;
+  op.tau_ptr = sl.tau;
+  op.tau0 = HIST - 1;
+  op.n_step = e->n;
   op.lr0 = c.learning_rate;
   op.max_step = c.max_step;
   op.target_period = e->L.algo == A3C_ALGO_Q ? c.target_q_update_step : 0;
@@ -447,11 +527,6 @@ static int enqueue_rollout_begin(a3c_engine* e, const Slot& sl, hipStream_t s) {
     rc = a3c_lstm_transpose_launch(sl.P + e->L.off[T_LW], sl.lwt, s);
     if (rc) return rc;
   }
-  if (e->L.algo == A3C_ALGO_Q) {
-    hipLaunchKernelGGL(k_eps, dim3((e->E + 255) / 256), dim3(256), 0, s, e->eps, e->ep_end, e->E, e->counters,
-                       c.ep_start, c.ep_end_t, c.learn_start);
-    A3C_CHECK(hipGetLastError());
-  }
   return 0;
 }
 
@@ -471,6 +546,11 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
   sel.env_ids = nullptr; sel.env_id_base = c.env_id_base; sel.E = E;
   sel.eps = e->eps;
   const int64_t o = (int64_t)t * E;
+  if (q) {        // epsilon of this step (agent.py:142-144; q engines are synchronous: tau is live)
+    hipLaunchKernelGGL(k_eps, dim3((E + 255) / 256), dim3(256), 0, s, e->eps, e->ep_end, E, e->counters, t,
+                       c.ep_start, c.ep_end_t, c.learn_start);
+    A3C_CHECK(hipGetLastError());
+  }
   sel.actions = sl.actions + o;
   sel.env_on = dev_env ? 1 : 0;
   if (dev_env) {
@@ -478,6 +558,7 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
     sel.envp = e->envp;
     sel.envb = e->env;
     sel.rewards = sl.rewards + o;
+    sel.rewards_raw = sl.rewards_raw + o;
     sel.terms = sl.terms + o;
     sel.frames_out = sl.frames + o;
     if (e->fused_screen) {      // Environment.screen of the new frame inside the head kernel
@@ -644,7 +725,7 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
                            L.lstm ? &lb : nullptr);
   if (rc) return rc;
   // per-tensor squared norms (+ lr / target-sync schedule from the device step counter)
-  OptParams op = opt_params(e);
+  OptParams op = opt_params(e, sl);
   rc = a3c_sumsq_launch(e->grads, e->tt, op, e->opt_part, s);
   if (rc) return rc;
   if (c.world_size > 1) {
@@ -664,7 +745,7 @@ static int enqueue_rollout_grad(a3c_engine* e, hipStream_t s) {
 // advance in one launch; world_size == 1: the per-tensor clip as well.  Overlap: then the
 // parameter snapshot of the rollout that will use slot `snap` (the slot just back-propagated).
 static int enqueue_apply(a3c_engine* e, int snap, hipStream_t s) {
-  OptParams op = opt_params(e);
+  OptParams op = opt_params(e, e->slot[snap]);    // (the schedule was evaluated by k_sumsq)
   op.mode = e->cfg.world_size > 1 ? OPT_APPLY : (OPT_CLIP | OPT_APPLY);
   // overlap: the same pass writes the parameter snapshot of the rollout that will use slot `snap`
   if (e->overlap) op.snap = e->slot[snap].P;
@@ -746,7 +827,12 @@ extern "C" int a3c_engine_reset(a3c_engine* e, const float* host_params, void* s
       A3C_CHECK(hipMemsetAsync(e->slot[k].terms, 0, (size_t)e->nE, s));
     }
   A3C_CHECK(hipMemsetAsync(e->xflags, 0, 64, s));
+  if (e->ext) A3C_CHECK(hipMemsetAsync(e->counters, 0, 64, s));   // ext_begin sets them
+  A3C_CHECK(hipMemsetAsync(e->ep_acc, 0, (size_t)e->E * 8, s));
+  hipLaunchKernelGGL(k_stats_reset, dim3(1), dim3(A3C_STATS_N), 0, s, e->stats);
+  A3C_CHECK(hipGetLastError());
   A3C_CHECK(hipStreamSynchronize(s));
+  e->step0_g = e->step0_w = 0;
   e->s_seq = e->r_seq = 0;
   e->roll_seq[0] = e->roll_seq[1] = 0;
   e->iter = 0;
@@ -875,7 +961,7 @@ extern "C" int a3c_engine_apply_shard(a3c_engine* e, const float* grads_by_rank,
 extern "C" int a3c_engine_apply_commit(a3c_engine* e, const float* params_src, void* stream) {
   if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_apply_commit", "null");
   if (!e->grad_ready || e->grad_applied) return 0;
-  const OptParams op = opt_params(e);
+  const OptParams op = opt_params(e, e->slot[0]);
   float* snap = e->overlap ? e->slot[(int)(e->iter & 1)].P : nullptr;
   int rc = a3c_commit_launch(params_src ? params_src : e->params, e->L.total, e->params, snap, op.target, e->sched,
                              e->counters, op.dtau, op.step_add, (hipStream_t)stream);
@@ -884,15 +970,15 @@ extern "C" int a3c_engine_apply_commit(a3c_engine* e, const float* params_src, v
 }
 
 // ---- external (host) environments (env workers feeding host RGB buffers) ----
-__global__ void k_ext_init(int64_t* counters, int32_t* frame1, int E) {
+__global__ void k_ext_init(int64_t* counters, int32_t* frame1, int E, int64_t step0_g, int64_t step0_w) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e == 0) { counters[0] = HIST - 1; counters[1] = 0; }
+  if (e == 0) { counters[0] = HIST - 1; counters[1] = step0_g; counters[2] = step0_w; }
   if (e < E) frame1[e] = e;      // env state parity (HIST-1)&1 = 1: frame e of the staging buffer
 }
 
-__global__ void k_ext_clip(float* r, int E) {
+__global__ void k_ext_clip(const float* raw, float* r, int E) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < E) r[e] = fmaxf(-1.0f, fminf(1.0f, r[e]));   // observe clip, agent.py:154
+  if (e < E) r[e] = fmaxf(-1.0f, fminf(1.0f, raw[e]));   // observe clip, agent.py:154
 }
 
 static int ext_check(a3c_engine* e, const char* what) {
@@ -909,7 +995,8 @@ extern "C" int a3c_engine_ext_begin(a3c_engine* e, const uint8_t* rgb, void* str
   hipStream_t s = (hipStream_t)stream;
   const int E = e->E;
   A3C_CHECK(hipMemcpyAsync(e->pool, rgb, (size_t)E * SCREEN_H * SCREEN_W * 3, hipMemcpyDefault, s));
-  hipLaunchKernelGGL(k_ext_init, dim3((E + 255) / 256), dim3(256), 0, s, e->counters, e->env.frame + E, E);
+  hipLaunchKernelGGL(k_ext_init, dim3((E + 255) / 256), dim3(256), 0, s, e->counters, e->env.frame + E, E,
+                     e->step0_g, e->step0_w);
   A3C_CHECK(hipGetLastError());
   int rc = a3c_env_init_screens_launch(e->env, E, e->pool, e->ring, e->R, s);
   if (rc) return rc;
@@ -979,14 +1066,192 @@ extern "C" int a3c_engine_ext_observe(a3c_engine* e, const uint8_t* rgb, const f
   const int E = e->E, t = e->ext_t;
   const int64_t o = (int64_t)t * E;
   if (rgb) A3C_CHECK(hipMemcpyAsync(e->pool, rgb, (size_t)E * SCREEN_H * SCREEN_W * 3, hipMemcpyDefault, s));
-  A3C_CHECK(hipMemcpyAsync(sl.rewards + o, rewards, (size_t)E * 4, hipMemcpyDefault, s));
+  A3C_CHECK(hipMemcpyAsync(sl.rewards_raw + o, rewards, (size_t)E * 4, hipMemcpyDefault, s));
   A3C_CHECK(hipMemcpyAsync(sl.terms + o, terminals, (size_t)E, hipMemcpyDefault, s));
-  hipLaunchKernelGGL(k_ext_clip, dim3((E + 255) / 256), dim3(256), 0, s, sl.rewards + o, E);
+  hipLaunchKernelGGL(k_ext_clip, dim3((E + 255) / 256), dim3(256), 0, s, sl.rewards_raw + o, sl.rewards + o, E);
   A3C_CHECK(hipGetLastError());
   int rc = a3c_env_screen_launch(E, e->ext_idx, e->pool, e->ring, e->R, e->counters, t, s);
   if (rc) return rc;
   e->ext_t = t + 1;
   e->ext_acted = false;
+  return 0;
+}
+
+// ---- summaries (agent.py:69-139 train_with_summary) ------------------------------------------
+// Adds the rollout whose gradient the last rollout_grad / iterate computed to the aggregates, on
+// `stream` after that call's backward (overlap: the rollout of the previous call).
+extern "C" int a3c_engine_stats_accumulate(a3c_engine* e, void* stream) {
+  if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_stats_accumulate", "null");
+  if (!e->reset_done) return a3c_set_error(A3C_ERR_STATE, "a3c_engine_stats_accumulate", "call a3c_engine_reset first");
+  if (!e->grad_ready) return 0;
+  const Slot& sl = e->slot[e->overlap ? (int)(e->iter & 1) : 0];
+  hipLaunchKernelGGL(k_stats, dim3(1), dim3(256), 0, (hipStream_t)stream, sl.rewards_raw, sl.terms, sl.z, e->L.zs,
+                     e->L.A, e->L.algo == A3C_ALGO_Q ? 1 : 0, e->n, e->E, e->loss, e->ep_acc, e->stats);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+// Waits for `stream`, copies the A3C_STATS_N aggregates to out; reset = 1 starts a new interval
+// (the per-env running episode rewards carry on).
+extern "C" int a3c_engine_stats_read(a3c_engine* e, double* out, int reset, void* stream) {
+  if (!e || !out) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_stats_read", "null");
+  if (!e->reset_done) return a3c_set_error(A3C_ERR_STATE, "a3c_engine_stats_read", "call a3c_engine_reset first");
+  hipStream_t s = (hipStream_t)stream;
+  A3C_CHECK(hipStreamSynchronize(s));
+  A3C_CHECK(hipMemcpy(out, e->stats, A3C_STATS_N * 8, hipMemcpyDeviceToHost));
+  if (reset) {
+    hipLaunchKernelGGL(k_stats_reset, dim3(1), dim3(A3C_STATS_N), 0, s, e->stats);
+    A3C_CHECK(hipGetLastError());
+  }
+  return 0;
+}
+
+// ---- checkpoint / resume (the Supervisor's Saver, main.py:74-90, agent.py:29) ----
+__global__ void k_set_step(int64_t* counters, int64_t g, int64_t w) {
+  counters[1] = g;
+  counters[2] = w;
+}
+
+// Resume from a checkpoint of parameters + step only (the reference's Saver keeps no more): the
+// global step T and the workers' loop counter restart at the restored step (agent.py:34,46).
+extern "C" int a3c_engine_set_step(a3c_engine* e, int64_t global_step, int64_t worker_step, void* stream) {
+  if (!e || global_step < 0 || worker_step < 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_set_step", "bad argument");
+  if (!e->reset_done) return a3c_set_error(A3C_ERR_STATE, "a3c_engine_set_step", "call a3c_engine_reset first");
+  e->step0_g = global_step;
+  e->step0_w = worker_step;
+  if (!e->ext || e->ext_begun) {
+    hipLaunchKernelGGL(k_set_step, dim3(1), dim3(1), 0, (hipStream_t)stream, e->counters, global_step, worker_step);
+    A3C_CHECK(hipGetLastError());
+  }
+  return 0;
+}
+
+namespace {
+struct StateRegion { void* p; size_t bytes; };
+struct StateHeader {
+  uint32_t magic, version;
+  int32_t E, n, R, algo, A, lstm, overlap, world, frame84, env_id_base;
+  int64_t total, bytes, iter;
+  uint64_t seed;
+  int32_t grad_ready, grad_applied;
+};
+constexpr uint32_t STATE_MAGIC = 0x53433341u;   // "A3CS"
+}
+
+// every device buffer whose contents carry from one iteration to the next: parameters, target,
+// RMSProp slots, counters, env state, frame ring, the LSTM carry, and in overlap mode the rollout
+// in flight (its parameter snapshot, tau, transitions and saved activations)
+static std::vector<StateRegion> state_regions(const a3c_engine* e) {
+  std::vector<StateRegion> r;
+  const int64_t T = e->L.total, E = e->E, nE = e->nE, zs = e->L.zs;
+  auto add = [&](const void* p, int64_t b) { r.push_back({const_cast<void*>(p), (size_t)b}); };
+  add(e->params, T * 4); add(e->tparams, T * 4); add(e->ms, T * 4); add(e->mom, T * 4);
+  add(e->counters, 64); add(e->loss, 64); add(e->stats, A3C_STATS_N * 8); add(e->ep_acc, E * 8);
+  add(e->ring, E * e->R * PLANE);
+  add(e->env.episode, 2 * E * 4); add(e->env.ep_step, 2 * E * 4); add(e->env.ep_len, 2 * E * 4);
+  add(e->env.lives, 2 * E * 4); add(e->env.frame, 2 * E * 4); add(e->env.reward, 2 * E * 4);
+  add(e->env.terminal, 2 * E);
+  for (int k = 0; k < e->nslot; ++k) {
+    const Slot& sl = e->slot[k];
+    if (e->overlap) {
+      add(sl.P, T * 4); add(sl.tau, 64);
+      add(sl.actions, nE * 4); add(sl.frames, nE * 4); add(sl.rewards, nE * 4); add(sl.rewards_raw, nE * 4);
+      add(sl.terms, nE);
+      add(sl.z, (nE + E) * zs * 4); add(sl.R_buf, nE * 4);
+      add(sl.act_l1, nE * C1_P * C1_N * 4); add(sl.act_l2, nE * FLAT * 4); add(sl.act_l3, nE * FC * 4);
+    }
+    if (e->L.lstm) {
+      add(sl.lh, nE * LSTM_U * 4); add(sl.lc, nE * LSTM_U * 4);
+      if (!e->overlap) add(sl.terms, nE);
+      else {
+        add(sl.lhp, nE * LSTM_U * 4); add(sl.lcp, nE * LSTM_U * 4); add(sl.lg, nE * LSTM_G * 4);
+        add(sl.lhb, E * LSTM_U * 4); add(sl.lcb, E * LSTM_U * 4);
+      }
+    }
+  }
+  return r;
+}
+
+static StateHeader state_header(const a3c_engine* e) {
+  StateHeader h = {};
+  h.magic = STATE_MAGIC; h.version = 1;
+  h.E = e->E; h.n = e->n; h.R = e->R; h.algo = e->L.algo; h.A = e->L.A; h.lstm = e->L.lstm ? 1 : 0;
+  h.overlap = e->overlap; h.world = e->cfg.world_size; h.frame84 = e->frame84;
+  h.env_id_base = e->cfg.env_id_base; h.seed = e->cfg.seed;   // the env shard and its random streams
+  h.total = e->L.total;
+  int64_t b = sizeof(StateHeader);
+  for (const StateRegion& x : state_regions(e)) b += (int64_t)x.bytes;
+  h.bytes = b;
+  return h;
+}
+
+static int state_check(const a3c_engine* e, const char* what) {
+  if (!e) return a3c_set_error(A3C_ERR_INVALID, what, "null");
+  if (e->ext)
+    return a3c_set_error(A3C_ERR_INVALID, what, "host-stepped envs cannot be snapshotted: resume from params + "
+                         "RMSProp slots + a3c_engine_set_step");
+  if (!e->reset_done) return a3c_set_error(A3C_ERR_STATE, what, "call a3c_engine_reset first");
+  return 0;
+}
+
+extern "C" int a3c_engine_state_bytes(a3c_engine* e, int64_t* bytes) {
+  if (int rc = state_check(e, "a3c_engine_state_bytes")) return rc;
+  if (!bytes) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_state_bytes", "null");
+  *bytes = state_header(e).bytes;
+  return 0;
+}
+
+// Waits for the engine's work on `stream` and its rollout stream, then copies the state to host.
+extern "C" int a3c_engine_state_save(a3c_engine* e, void* host, int64_t bytes, void* stream) {
+  if (int rc = state_check(e, "a3c_engine_state_save")) return rc;
+  StateHeader h = state_header(e);
+  if (!host || bytes != h.bytes) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_state_save", "buffer size");
+  A3C_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  if (e->rs) A3C_CHECK(hipStreamSynchronize(e->rs));
+  h.iter = e->iter;
+  h.grad_ready = e->grad_ready;
+  h.grad_applied = e->grad_applied;
+  uint8_t* o = (uint8_t*)host;
+  memcpy(o, &h, sizeof(h));
+  o += sizeof(h);
+  for (const StateRegion& x : state_regions(e)) {
+    A3C_CHECK(hipMemcpy(o, x.p, x.bytes, hipMemcpyDeviceToHost));
+    o += x.bytes;
+  }
+  return 0;
+}
+
+// Restores a state written by a3c_engine_state_save into an engine of the same configuration
+// (after a3c_engine_reset: the frame pool is regenerated there); the next iteration continues
+// the saved run bit for bit.
+extern "C" int a3c_engine_state_load(a3c_engine* e, const void* host, int64_t bytes, void* stream) {
+  if (int rc = state_check(e, "a3c_engine_state_load")) return rc;
+  const StateHeader want = state_header(e);
+  StateHeader h;
+  if (!host || bytes < (int64_t)sizeof(h)) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_state_load", "short buffer");
+  memcpy(&h, host, sizeof(h));
+  if (h.magic != STATE_MAGIC || h.version != want.version)
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_state_load", "not an engine state");
+  if (h.E != want.E || h.n != want.n || h.R != want.R || h.algo != want.algo || h.A != want.A ||
+      h.lstm != want.lstm || h.overlap != want.overlap || h.world != want.world || h.frame84 != want.frame84 ||
+      h.env_id_base != want.env_id_base || h.seed != want.seed || h.total != want.total || h.bytes != want.bytes ||
+      bytes != want.bytes)
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_state_load", "state of a different engine configuration");
+  hipStream_t s = (hipStream_t)stream;
+  A3C_CHECK(hipStreamSynchronize(s));
+  if (e->rs) A3C_CHECK(hipStreamSynchronize(e->rs));
+  const uint8_t* o = (const uint8_t*)host + sizeof(h);
+  for (const StateRegion& x : state_regions(e)) {
+    A3C_CHECK(hipMemcpy(x.p, o, x.bytes, hipMemcpyHostToDevice));
+    o += x.bytes;
+  }
+  A3C_CHECK(hipMemset(e->xflags, 0, 64));       // fresh cross-stream sequence numbers
+  A3C_CHECK(hipDeviceSynchronize());
+  e->s_seq = e->r_seq = 0;
+  e->roll_seq[0] = e->roll_seq[1] = 0;
+  e->iter = h.iter;
+  e->grad_ready = h.grad_ready != 0;
+  e->grad_applied = h.grad_applied != 0;
   return 0;
 }
 

@@ -27,7 +27,7 @@ __global__ void k_pool_fill(uint8_t* __restrict__ pool, int64_t chunks_per_frame
 // state lives at parity (tau & 1) of the double-buffered state arrays.
 __global__ void k_env_init_state(EnvParams p, EnvBufs b, int E, int64_t* __restrict__ counters) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e == 0) { counters[0] = HIST - 1; counters[1] = 0; }
+  if (e == 0) { counters[0] = HIST - 1; counters[1] = 0; counters[2] = 0; }   // tau, global, worker step
   if (e >= E) return;
   EnvState s = {0u, 0u, 0u, 0, 0, 0.f, 0u};
   env_new_random_game(s, p, (uint32_t)(p.env_id_base + e));

@@ -106,6 +106,7 @@ struct HeadSelect {
   EnvParams envp;
   EnvBufs envb;
   float* rewards;           // [E] observe-clipped reward (agent.py:154)
+  float* rewards_raw;       // [E] nullable: the unclipped act() reward (train_with_summary's sums)
   uint8_t* terms;           // [E]
   int32_t* frames_out;      // [E] post-act frame index (the screen the history gets)
   // fused Environment.screen of the post-act frame into the frame ring (engine rollout):

@@ -592,6 +592,7 @@ __device__ inline int32_t head_act(float myz, int lane, int A, const HeadSelect&
       EnvState s = env_load(sel.envb, cur);
       env_act(s, sel.envp, id, (uint32_t)a, true);
       sel.rewards[e] = fmaxf(-1.0f, fminf(1.0f, s.reward));   // observe clip, agent.py:154
+      if (sel.rewards_raw) sel.rewards_raw[e] = s.reward;
       sel.terms[e] = (uint8_t)s.terminal;
       sel.frames_out[e] = s.frame;
       frame = s.frame;
@@ -672,6 +673,7 @@ __device__ inline int32_t head_act_env(const float* __restrict__ h3, const float
     EnvState s = env_load(sel.envb, cur);
     const uint32_t draw = env_act_pre(s, sel.envp, id, true);
     sel.rewards[e] = fmaxf(-1.0f, fminf(1.0f, s.reward));   // observe clip, agent.py:154
+    if (sel.rewards_raw) sel.rewards_raw[e] = s.reward;
     sel.terms[e] = (uint8_t)s.terminal;
     s_draw = draw;
     s_term = s.terminal;

@@ -20,12 +20,20 @@ struct OptParams {
   int mode;              // OPT_CLIP | OPT_APPLY
   float clip;            // <= 0: no clipping
   float lr;              // used when sched == nullptr
-  // schedule (engine): the sum-of-squares kernel computes, from the device global step,
+  // schedule (engine): the sum-of-squares kernel computes
   //   sched[0] = lr = (max_step - step + 1)/max_step * lr0              (agent.py:393-395)
-  //   sched[1] = 1 if a target sync falls in (step, step + step_add]    (agent.py:165-167)
+  //   sched[1] = 1 if a target sync falls in (T, T + step_add]          (agent.py:165-167)
+  // where T = *step_ptr is the global step (the reference's step_op, every worker's env steps) and
+  // `step` is the worker's own loop counter (agent.py:55: `for self.step in xrange(T0, max_step)`)
+  // at the update: with wstep_ptr, step = *wstep_ptr + (*tau_ptr - tau0) + n_step - 1 -- the base
+  // the workers started from, plus the env steps before the rollout, plus the rollout's last step
+  // (batch_update runs inside that step's observe, agent.py:162-163); without it, T + step_add.
   float* sched;
   const int64_t* step_ptr;
   int64_t step_add;
+  const int64_t* wstep_ptr;
+  const int64_t* tau_ptr;
+  int64_t tau0, n_step;
   double lr0;
   int64_t max_step;
   int64_t target_period;  // 0: no target network

@@ -59,7 +59,8 @@ __global__ void __launch_bounds__(256) k_sumsq(const float* __restrict__ g, Tens
     part[blockIdx.x] = red[0];
     if (blockIdx.x == 0 && op.sched && op.step_ptr) {
       const int64_t g0 = *op.step_ptr;
-      const double step = (double)(g0 + op.step_add);
+      const double step = op.wstep_ptr ? (double)(*op.wstep_ptr + (*op.tau_ptr - op.tau0) + op.n_step - 1)
+                                       : (double)(g0 + op.step_add);
       // agent.py:393-395; the reference never trains past max_step (agent.py:46,55-57), so the
       // schedule is clamped at 0 there instead of turning negative (RMSProp would ascend)
       const double lr = (double)(op.max_step - step + 1.0) / (double)op.max_step * op.lr0;

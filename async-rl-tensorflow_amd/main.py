@@ -63,7 +63,14 @@ def parse_flags(argv=None):
                       'emulator, frames over PCIe), or gym/ALE envs on the host (AtariEnv, needs gym)')
   p.add_argument('--host_threads', type=int, default=16)
   p.add_argument('--max_step', type=int, default=None)
-  p.add_argument('--log_every', type=int, default=100)
+  p.add_argument('--log_every', type=int, default=None,
+                 help='engine mode: iterations between summaries (default: test_step env-steps per env, '
+                      'agent.py:104)')
+  p.add_argument('--save_model_secs', type=int, default=600, help='checkpoint period (main.py:80)')
+  p.add_argument('--max_to_keep', type=int, default=30, help='checkpoints kept (agent.py:29)')
+  p.add_argument('--checkpoint_dir', default=None, help='default: <logdir>/<model_dir> (main.py:75)')
+  p.add_argument('--resume', type=str2bool, default=True,
+                 help='restore the newest checkpoint of checkpoint_dir, as managed_session does (main.py:90)')
   p.add_argument('--update', choices=['overlap', 'sync', 'hogwild'], default='overlap',
                  help='engine mode: stale-1 overlapped A3C, synchronous exchange, or Hogwild sharded PS')
   p.add_argument('--exchange', choices=['sequential', 'sum'], default='sequential',
@@ -97,20 +104,34 @@ def make_host_pool(config, flags, E, A, lives, rank):
     import gym
   except ImportError as e:
     raise RuntimeError('--envs_on gym needs the gym package (with the Atari ROMs)') from e
-  rng = random.Random(flags.random_seed + rank)
+  # one emulator seed and one no-op-start stream per env (the reference: one env and one `random`
+  # per worker process, environment.py:37), so the pool's threads cannot reorder the draws
   envs = []
   for e in range(E):
-    g = gym.make(config.env_name)
-    if hasattr(g, 'seed'):
-      g.seed(flags.random_seed + rank * E + e)
-    envs.append(AtariEnv(g, action_repeat=config.action_repeat, random_start=config.random_start, rng=rng))
+    sid = flags.random_seed + rank * E + e
+    envs.append(AtariEnv(gym.make(config.env_name), action_repeat=config.action_repeat,
+                         random_start=config.random_start, rng=random.Random(sid), seed=sid))
   return HostEnvPool(envs, threads=flags.host_threads)
 
 
+def _agree(flag, world):
+  """Rank 0's decision on every rank (checkpoint times must match across the ranks)."""
+  if world == 1:
+    return bool(flag)
+  import torch.distributed as dist
+  t = torch.tensor([1 if flag else 0], dtype=torch.int32,
+                   device='cuda' if dist.get_backend() == 'nccl' else 'cpu')
+  dist.broadcast(t, src=0)
+  return bool(t.item())
+
+
 def run_engine(config, flags):
+  from src import checkpoint as C
   from src import distributed as D
+  from src.base import BaseModel
   from src.engine import Engine
   from src.environment import game_spec
+  from src.kernels import param_names_shapes
   rank, world, local = D.init_from_env()
   torch.cuda.set_device(local)
   A, lives = game_spec(config.env_name)
@@ -125,16 +146,28 @@ def run_engine(config, flags):
   if host and flags.update == 'hogwild':
     raise ValueError('--envs_on host/gym drives a synchronous engine; use --update sync or overlap')
   overlap = flags.update == 'overlap' and flags.algo == 'a3c' and not host
+  if flags.update == 'overlap' and not overlap and rank == 0:
+    print('main.py: --update overlap needs the a3c algo and device envs; running the synchronous engine',
+          file=sys.stderr, flush=True)
   pool = make_host_pool(config, flags, E, A, lives, rank) if host else None
   eng = Engine(num_envs=E, n_step=flags.n_step, action_size=A, algo=flags.algo, start_lives=lives,
                num_frames=1 if host else flags.num_frames, seed=flags.random_seed, env_id_base=rank * E,
                world_size=world, overlap=overlap, external_env=host, **opts)
-  eng.reset(initial_params(eng, A, flags.algo, flags.random_seed))
-  D.broadcast_params(eng.params, src=0)
-  if flags.algo == 'q':
-    eng.target_params.copy_(eng.params)
-  if overlap:
-    eng.reset()    # keeps the broadcast parameters, re-takes the pipeline snapshots
+  ns = param_names_shapes(A, flags.algo, lstm=eng.lstm)
+  # checkpoints: <logdir>/<model_dir> as the Supervisor's logdir (main.py:75), Saver max_to_keep
+  # (agent.py:29); restored at start as managed_session does (main.py:90)
+  ckdir = flags.checkpoint_dir or os.path.join(flags.logdir, BaseModel(config, verbose=False).model_dir)
+  saver = C.Saver(ckdir, max_to_keep=flags.max_to_keep)
+  restored = C.restore_engine(saver, eng, ns, rank, world) if flags.resume else None
+  if restored is None:
+    eng.reset(initial_params(eng, A, flags.algo, flags.random_seed))
+    D.broadcast_params(eng.params, src=0)
+    if flags.algo == 'q':
+      eng.target_params.copy_(eng.params)
+    if overlap:
+      eng.reset()    # keeps the broadcast parameters, re-takes the pipeline snapshots
+  elif rank == 0:
+    print(json.dumps({'restored': saver.latest(), 'global_step': restored}), flush=True)
   xch = None
   if world > 1:
     xch = D.PartitionedPS(eng.params.numel()) if flags.exchange == 'sequential' else D.GradExchange()
@@ -142,12 +175,17 @@ def run_engine(config, flags):
   if flags.update == 'hogwild':
     from src.hogwild import HogwildPS
     ps = HogwildPS(eng.params, decay=config.decay, momentum=config.momentum, epsilon=config.epsilon)
-  # the reference trains until the global step reaches max_step (agent.py:46,55-57): every
-  # applied update adds E*n*world env-steps, the overlap pipeline's first call applies none
-  per_update = E * flags.n_step * world
-  iterations = min(flags.iterations, -(-int(config.max_step) // per_update) + (1 if overlap else 0))
+  # the reference's worker loop `for self.step in xrange(self.step, self.max_step)` (agent.py:46,55):
+  # each worker -- here each env, all in lock-step -- takes env-steps up to max_step on its own
+  # counter; one rollout is n of them, and the overlap pipeline applies one call later
+  n = flags.n_step
+  remaining = max(0, int(config.max_step) - eng.worker_step)
+  iterations = min(flags.iterations, -(-remaining // n) + (1 if overlap else 0))
+  test_step = int(getattr(config, 'test_step', getattr(config, '_test_step', 5000)))
+  log_every = flags.log_every or max(1, test_step // n)
   torch.cuda.synchronize()
   t0 = time.time()
+  last_save = t0
   log = None
   if rank == 0:
     os.makedirs(flags.logdir, exist_ok=True)
@@ -159,17 +197,28 @@ def run_engine(config, flags):
       eng.iterate_host(pool, exchange=xch)
     else:
       eng.iterate(exchange=xch)
-    if rank == 0 and (it + 1) % flags.log_every == 0:
-      loss = eng.loss.tolist()
-      torch.cuda.synchronize()
-      dt = time.time() - t0
-      rec = dict(iteration=it + 1, global_step=int(eng.counters[1].item()),
-                 env_steps_per_sec=(it + 1) * E * flags.n_step * world / dt,
-                 loss_policy=loss[0], loss_value=loss[1], entropy=loss[2], loss_total=loss[3],
-                 mean_return=float(eng.returns.mean().item()), reward_sum=float(eng.rewards.sum().item()))
-      print(json.dumps(rec), flush=True)
-      log.write(json.dumps(rec) + '\n')
+    if rank == 0:
+      eng.stats_accumulate()       # train_with_summary's aggregates (agent.py:91-131), on device
+    if (it + 1) % log_every == 0:
+      if rank == 0:
+        loss = eng.loss.tolist()
+        st = eng.read_stats(reset=True)
+        torch.cuda.synchronize()
+        dt = time.time() - t0
+        wstep = eng.worker_step
+        rec = dict(iteration=it + 1, global_step=int(eng.counters[1].item()), worker_step=wstep,
+                   env_steps_per_sec=(it + 1) * E * n * world / dt, **st,
+                   learning_rate=max(0.0, (config.max_step - wstep + 1.) / config.max_step * config.learning_rate),
+                   loss_policy=loss[0], loss_value=loss[1], entropy=loss[2], loss_total=loss[3],
+                   mean_return=float(eng.returns.mean().item()))
+        print(json.dumps(rec), flush=True)
+        log.write(json.dumps(rec) + '\n')
+      if _agree(rank == 0 and time.time() - last_save >= flags.save_model_secs, world):
+        C.save_engine(saver, eng, ns, rank, world, barrier=_barrier(world))
+        last_save = time.time()
   torch.cuda.synchronize()
+  if iterations > 0:
+    C.save_engine(saver, eng, ns, rank, world, barrier=_barrier(world))    # the final state
   if ps is not None:
     ps.close()
   if pool is not None:
@@ -177,6 +226,13 @@ def run_engine(config, flags):
   if log:
     log.close()
   return eng
+
+
+def _barrier(world):
+  if world == 1:
+    return None
+  import torch.distributed as dist
+  return dist.barrier
 
 
 def run_agent(config, flags):

@@ -113,6 +113,12 @@ SIGNATURES = {
     'a3c_engine_slot_buffers': (c_int, [c_void_p, c_int, ctypes.POINTER(EngineBuffers)]),
     'a3c_engine_grad_ready': (c_int, [c_void_p]),
     'a3c_engine_advance': (c_int, [c_void_p, c_void_p]),
+    'a3c_engine_set_step': (c_int, [c_void_p, c_i64, c_i64, c_void_p]),
+    'a3c_engine_stats_accumulate': (c_int, [c_void_p, c_void_p]),
+    'a3c_engine_stats_read': (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    'a3c_engine_state_bytes': (c_int, [c_void_p, ctypes.POINTER(c_i64)]),
+    'a3c_engine_state_save': (c_int, [c_void_p, c_void_p, c_i64, c_void_p]),
+    'a3c_engine_state_load': (c_int, [c_void_p, c_void_p, c_i64, c_void_p]),
     'a3c_engine_apply_shard': (c_int, [c_void_p, c_void_p, c_int, c_i64, c_i64, c_void_p, c_void_p]),
     'a3c_engine_apply_commit': (c_int, [c_void_p, c_void_p, c_void_p]),
     'a3c_engine_ext_begin': (c_int, [c_void_p, c_void_p, c_void_p]),

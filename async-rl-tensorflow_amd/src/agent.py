@@ -23,6 +23,7 @@ import torch
 
 from . import kernels as K
 from . import ops
+from . import checkpoint as C
 from .base import BaseModel, load_checkpoint, save_checkpoint
 from .distributed import GradExchange, gather_grads
 from .history import History
@@ -377,15 +378,18 @@ class Agent(BaseModel):
 
   # -- checkpoints (Saver, agent.py:29) ------------------------------------------------------
   def save(self, path):
-    named = dict(self.w)
-    named.update({'target/' + k: v for k, v in self.t_w.items()})
+    """Saver of agent.py:29 (prediction weights + step) keyed by the TF variable names, plus the
+    target network (agent.py:257-296 names)."""
+    named = {C.tf_name(k, 'q'): v for k, v in self.w.items()}
+    named.update({C.tf_target_name(k): v for k, v in self.t_w.items()})
     return save_checkpoint(path, named, self.step_op)
 
   def load(self, path):
     arrays, step = load_checkpoint(path)
+    dst = {C.tf_name(k, 'q'): v for k, v in self.w.items()}
+    dst.update({C.tf_target_name(k): v for k, v in self.t_w.items()})
     for k, v in arrays.items():
-      dst = self.t_w[k[7:]] if k.startswith('target/') else self.w.get(k)
-      if dst is not None:
-        dst.copy_(torch.as_tensor(v).reshape(dst.shape))
+      if k in dst:
+        dst[k].copy_(torch.as_tensor(v).reshape(dst[k].shape))
     self.step_op = step
     return step

@@ -4,7 +4,7 @@ The model copies every public attribute of its config onto itself (a leading und
 dropped: ``_test_step`` -> ``test_step``), and derives ``model_dir`` from the config values
 (everything but ``display``), which the reference uses as the run / checkpoint directory.
 Checkpoints (the Saver of agent.py:29 / main.py:74-80) are ``.npz`` files keyed by the TF
-variable names plus the global step.
+variable names (src/checkpoint.py) plus the global step ``step``.
 """
 import inspect
 import os
@@ -61,16 +61,18 @@ class BaseModel(object):
 
 
 def save_checkpoint(path, named_tensors, step):
-  """{tf variable name: tensor} + global step -> path.npz (max_to_keep handled by callers)."""
+  """{tf variable name: tensor} + the global step (TF variable ``step``, agent.py:25) -> path.npz
+  (max_to_keep handled by callers; src/checkpoint.py has the names and the Saver)."""
   d = os.path.dirname(path)
   if d:
     os.makedirs(d, exist_ok=True)
   arrays = {k: (v.detach().cpu().numpy() if hasattr(v, 'detach') else np.asarray(v)) for k, v in named_tensors.items()}
-  np.savez(path, __step__=np.array(int(step), np.int64), **arrays)
+  np.savez(path, step=np.array(int(step), np.int64), **arrays)
   return path if path.endswith('.npz') else path + '.npz'
 
 
 def load_checkpoint(path):
   with np.load(path, allow_pickle=False) as f:
-    step = int(f['__step__'])
-    return {k: f[k] for k in f.files if k != '__step__'}, step
+    key = 'step' if 'step' in f.files else '__step__'     # (files of rounds 1-2)
+    step = int(f[key])
+    return {k: f[k] for k in f.files if k != key}, step

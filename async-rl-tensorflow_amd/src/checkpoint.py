@@ -1,0 +1,248 @@
+"""Checkpoints keyed by TensorFlow variable names.
+
+The reference checkpoints with a Saver over the prediction weights plus the global ``step``
+(agent.py:29, ``tf.train.Saver(self.w.values() + [self.step_op], max_to_keep=30)``), written by the
+Supervisor every 600 s (main.py:74-80) into ``./logs/<model_dir>`` and restored by
+``managed_session`` (main.py:90); training resumes at the restored step (agent.py:34,46).
+
+Here a checkpoint is ``<dir>/model.ckpt-<step>.npz`` (numpy, loaded with allow_pickle=False) whose
+keys are the TF variable names the reference's graph would give each tensor:
+
+* Q-learning agent (agent.py:218-252, ``prediction`` scope, ops.py ``w``/``biases``/``Matrix``/
+  ``bias``): ``prediction/l1/w``, ``prediction/l1/biases``, ``prediction/l2/w``, ...,
+  ``prediction/l3/Matrix``, ``prediction/l3/bias``, ``prediction/q/Matrix``, ``prediction/q/bias``;
+  the target network (agent.py:257-296) ``target/target_l1/w`` ...;
+* A3C network (network.py:43-79): ``l1_conv/w``, ``l1_conv/biases``, ``l2_conv/...``,
+  ``l4_linear/Matrix``, ``l4_linear/bias``, ``policy/linear/Matrix``, ``policy/linear/bias``,
+  ``value/linear/Matrix``, ``value/linear/bias`` (the nature trunk under ``Nature_DQN/``);
+* C5 LSTM head (build-defined, TF1 BasicLSTMCell naming): ``lstm/basic_lstm_cell/weights``,
+  ``lstm/basic_lstm_cell/biases``;
+* ``step``: the global step (the reference's ``step`` variable).
+
+Beyond what the reference's Saver keeps, the file also holds the RMSProp slots under TF1's slot
+names (``<var>/RMSProp`` = ms, ``<var>/RMSProp_1`` = momentum) and, for the batched engine, the
+whole engine state (``__engine_state__``: counters, env state, frame ring, LSTM carry, the overlap
+pipeline's rollout in flight), so that a resumed run continues bit for bit.  With several GPUs each
+rank writes its own env shard's state to ``model.ckpt-<step>.rank<r>.npz``.  A ``checkpoint``
+index file (JSON) lists the kept checkpoints, newest last; ``max_to_keep`` (30) bounds it.  The
+``world`` key records how many ranks wrote the checkpoint: the engine states are only taken back by
+a run of the same size (each rank's env shard); any other run resumes from parameters + step.
+"""
+import glob
+import json
+import os
+
+import numpy as np
+
+STEP_KEY = 'step'
+STATE_KEY = '__engine_state__'
+
+_Q = {'l1_w': 'l1/w', 'l1_b': 'l1/biases', 'l2_w': 'l2/w', 'l2_b': 'l2/biases',
+      'l3_w': 'l3/Matrix', 'l3_b': 'l3/bias', 'q_w': 'q/Matrix', 'q_b': 'q/bias',
+      # dueling (agent.py:234-249)
+      'l3_val_w': 'value_hid/Matrix', 'l3_val_b': 'value_hid/bias', 'l3_adv_w': 'adv_hid/Matrix',
+      'l3_adv_b': 'adv_hid/bias', 'val_w_out': 'value_out/Matrix', 'val_w_b': 'value_out/bias',
+      'adv_w_out': 'adv_out/Matrix', 'adv_w_b': 'adv_out/bias'}
+_A3C_NIPS = {'l1_w': 'l1_conv/w', 'l1_b': 'l1_conv/biases', 'l2_w': 'l2_conv/w', 'l2_b': 'l2_conv/biases',
+             'l4_w': 'l4_linear/Matrix', 'l4_b': 'l4_linear/bias',
+             'p_w': 'policy/linear/Matrix', 'p_b': 'policy/linear/bias',
+             'q_w': 'value/linear/Matrix', 'q_b': 'value/linear/bias',
+             'lstm_w': 'lstm/basic_lstm_cell/weights', 'lstm_b': 'lstm/basic_lstm_cell/biases'}
+
+
+def tf_name(name, algo='a3c', dqn_type='nips'):
+    """TF variable name of flat tensor ``name`` (the python dict keys of agent.py / network.py)."""
+    if algo == 'q':
+        return 'prediction/' + _Q[name]
+    if dqn_type.lower() == 'nature':
+        m = dict(_A3C_NIPS, l3_w='l3_conv/w', l3_b='l3_conv/biases')
+        n = m[name]
+        return n if n.split('/')[0] in ('policy', 'value', 'lstm') else 'Nature_DQN/' + n
+    return _A3C_NIPS[name]
+
+
+def tf_target_name(name):
+    """agent.py:257-296: the target network's layers are ``target_<layer>`` under ``target``."""
+    layer, var = _Q[name].split('/')
+    return 'target/target_%s/%s' % (layer, var)
+
+
+def slot_names(var):
+    """TF1 RMSPropOptimizer slot variables of ``var``: (rms, momentum)."""
+    return var + '/RMSProp', var + '/RMSProp_1'
+
+
+class Saver(object):
+    """tf.train.Saver stand-in: ``save(arrays, step)`` -> ``<dir>/model.ckpt-<step>.npz`` and the
+    index; ``latest()`` -> newest kept path (tf.train.latest_checkpoint)."""
+
+    def __init__(self, directory, max_to_keep=30, basename='model.ckpt'):
+        self.dir, self.max_to_keep, self.basename = directory, int(max_to_keep), basename
+
+    @property
+    def index_path(self):
+        return os.path.join(self.dir, 'checkpoint')
+
+    def path(self, step, rank=0):
+        p = os.path.join(self.dir, '%s-%d' % (self.basename, int(step)))
+        return p + ('.rank%d.npz' % rank if rank else '.npz')
+
+    def kept(self):
+        try:
+            with open(self.index_path) as f:
+                return list(json.load(f)['all_model_checkpoint_paths'])
+        except (OSError, ValueError, KeyError):
+            return []
+
+    def latest(self):
+        k = self.kept()
+        for p in reversed(k):
+            if os.path.exists(p):
+                return p
+        return None
+
+    def write(self, arrays, step, rank=0):
+        """Write one file (every rank its own); the index is updated by ``commit``."""
+        os.makedirs(self.dir, exist_ok=True)
+        path = self.path(step, rank)
+        tmp = path[:-4] + '.tmp.npz'
+        np.savez(tmp, **arrays)
+        os.replace(tmp, path)
+        return path
+
+    def commit(self, step):
+        """Rank 0, after every rank wrote: add the checkpoint to the index, drop the oldest beyond
+        max_to_keep (with their rank files)."""
+        path = self.path(step)
+        kept = [p for p in self.kept() if p != path] + [path]
+        while self.max_to_keep > 0 and len(kept) > self.max_to_keep:
+            old = kept.pop(0)
+            for f in [old] + glob.glob(old[:-4] + '.rank*.npz'):
+                try:
+                    os.remove(f)
+                except OSError:
+                    pass
+        tmp = self.index_path + '.tmp'
+        with open(tmp, 'w') as f:
+            json.dump({'model_checkpoint_path': path, 'all_model_checkpoint_paths': kept}, f)
+        os.replace(tmp, self.index_path)
+        return path
+
+    def save(self, arrays, step):
+        self.write(arrays, step)
+        return self.commit(step)
+
+
+def load(path):
+    with np.load(path, allow_pickle=False) as f:
+        return {k: f[k] for k in f.files}
+
+
+# ------------------------------------------------------------------------------ batched engine
+def engine_arrays(eng, names_shapes, with_state=True):
+    """The engine's parameters (+ target for q, RMSProp slots, step) keyed by TF names, and its
+    whole state blob."""
+    algo = eng.algo
+    state = eng.save_state() if with_state else None     # (first: waits for every engine stream)
+
+    def tensors(flat):
+        f = flat.detach().cpu().numpy()
+        return {name: f[off:off + sz].reshape(shp).copy()
+                for (name, shp), off, sz in zip(names_shapes, eng.offsets, eng.sizes)}
+    P, MS, MOM = tensors(eng.params), tensors(eng.ms), tensors(eng.mom)
+    out = {}
+    for name, _ in names_shapes:
+        tn = tf_name(name, algo)
+        out[tn] = P[name]
+        rms, mom = slot_names(tn)
+        out[rms], out[mom] = MS[name], MOM[name]
+    if algo == 'q':
+        T = tensors(eng.target_params)
+        for name, _ in names_shapes:
+            out[tf_target_name(name)] = T[name]
+    out[STEP_KEY] = np.array(int(eng.counters[1].item()), np.int64)
+    if state is not None:
+        out[STATE_KEY] = state
+    return out
+
+
+def engine_restore(eng, names_shapes, arrays, state=None):
+    """Restore into a created engine.  With a state blob of the same configuration: the exact
+    state (bit-continuous).  Otherwise the reference's resume: parameters (and whatever of the
+    target / RMSProp slots the file has) on freshly reset envs, global and worker step at the
+    restored ``step`` (agent.py:34,46).  Returns the global step."""
+    import torch
+    algo = eng.algo
+    step = int(arrays[STEP_KEY])
+    if state is not None and not eng.external_env:
+        eng.reset()
+        try:
+            eng.load_state(state)
+            return step
+        except RuntimeError:
+            pass        # another engine configuration: fall back to params + step
+
+    def flat(get, default=None):
+        out = np.zeros(eng.params.numel(), np.float32)
+        for (name, shp), off, sz in zip(names_shapes, eng.offsets, eng.sizes):
+            v = get(name)
+            if v is None:
+                if default is None:
+                    return None
+                v = default[off:off + sz]
+            out[off:off + sz] = np.asarray(v, np.float32).reshape(-1)
+        return out
+    P = flat(lambda n: arrays.get(tf_name(n, algo)))
+    if P is None:
+        missing = [tf_name(n, algo) for n, _ in names_shapes if tf_name(n, algo) not in arrays]
+        raise ValueError('checkpoint lacks %s' % missing)
+    eng.reset(P)
+    if algo == 'q':
+        T = flat(lambda n: arrays.get(tf_target_name(n)), P)
+        eng.target_params.copy_(torch.as_tensor(T))
+    ms = flat(lambda n: arrays.get(slot_names(tf_name(n, algo))[0]))
+    mom = flat(lambda n: arrays.get(slot_names(tf_name(n, algo))[1]))
+    if ms is not None and mom is not None:
+        eng.ms.copy_(torch.as_tensor(ms))
+        eng.mom.copy_(torch.as_tensor(mom))
+    eng.set_step(step, step)
+    torch.cuda.synchronize()
+    return step
+
+
+def save_engine(saver, eng, names_shapes, rank=0, world=1, barrier=None):
+    """Every rank writes its file (rank 0: parameters + its state; rank r: its state), then rank 0
+    commits the index once all are on disk (``barrier``: a callable, e.g. dist.barrier)."""
+    step = int(eng.counters[1].item())
+    if rank == 0:
+        arrays = engine_arrays(eng, names_shapes, with_state=not eng.external_env)
+        arrays['world'] = np.array(world)
+        saver.write(arrays, step)
+    elif not eng.external_env:
+        saver.write({STATE_KEY: eng.save_state(), 'world': np.array(world)}, step, rank)
+    if barrier is not None and world > 1:
+        barrier()
+    if rank == 0:
+        saver.commit(step)
+    return step
+
+
+def restore_engine(saver, eng, names_shapes, rank=0, world=1):
+    """Restore the newest checkpoint of ``saver`` (None if there is none).  Rank r takes its own
+    env shard's state when the checkpoint was written by as many ranks, else resumes from
+    parameters + step like the reference."""
+    path = saver.latest()
+    if path is None:
+        return None
+    arrays = load(path)
+    state = None
+    # the exact state only if the checkpoint was written by as many ranks (each rank's env shard);
+    # otherwise every rank falls back alike to parameters + step
+    if int(arrays.get('world', -1)) == world:
+        if rank == 0:
+            state = arrays.get(STATE_KEY)
+        else:
+            rp = path[:-4] + '.rank%d.npz' % rank
+            if os.path.exists(rp):
+                state = load(rp).get(STATE_KEY)
+    return engine_restore(eng, names_shapes, arrays, state)

@@ -94,7 +94,8 @@ class Engine:
         self.grads = _view(b.grads, (P,), torch.float32)
         self.frame_ring = _view(b.frame_ring, (E, b.ring_slots, 84, 84), torch.uint8)
         self.ring_slots = int(b.ring_slots)
-        self.counters = _view(b.tau, (2,), torch.int64)
+        # [0] tau, [1] global step T (agent.py:165), [2] the workers' base step (agent.py:34,55)
+        self.counters = _view(b.tau, (3,), torch.int64)
         self.loss = _view(b.loss, (4,), torch.float32)
         self.sched_ptr = int(b.sched)             # device [0] = lr of the last gradient
         self.sumsq = _view(b.sumsq, (b.n_tensors,), torch.float32)
@@ -206,6 +207,67 @@ class Engine:
         if exchange is not None:
             exchange(self.grads)
         self.apply()
+
+    # ---------------------------------------------------------------- summaries (agent.py:69-139)
+    STATS = ('reward_sum', 'ep_reward_sum', 'ep_reward_max', 'ep_reward_min', 'games', 'loss_sum', 'q_sum',
+             'updates', 'env_steps', 'policy_loss_sum', 'value_loss_sum', 'entropy_sum')
+
+    def stats_accumulate(self):
+        """Add the rollout whose gradient the last iterate() computed to the device aggregates."""
+        check(lib().a3c_engine_stats_accumulate(self._h, _lib.stream_handle()), 'a3c_engine_stats_accumulate')
+
+    def read_stats(self, reset=True):
+        """train_with_summary's aggregates since the last read (agent.py:104-131) over this GPU's
+        envs: avg reward per env-step, avg loss / q per update, episode max / min / avg reward,
+        number of games."""
+        out = (ctypes.c_double * 16)()
+        check(lib().a3c_engine_stats_read(self._h, out, 1 if reset else 0, _lib.stream_handle()),
+              'a3c_engine_stats_read')
+        raw = dict(zip(self.STATS, list(out)[:len(self.STATS)]))
+        games, upd, steps = raw['games'], raw['updates'], raw['env_steps']
+        res = {'avg_reward': raw['reward_sum'] / steps if steps else 0.0,
+               'avg_loss': raw['loss_sum'] / upd if upd else 0.0,
+               'avg_q': raw['q_sum'] / upd if upd else 0.0,
+               # agent.py:110-115: 0 when no episode finished in the interval
+               'avg_ep_reward': raw['ep_reward_sum'] / games if games else 0.0,
+               'max_ep_reward': raw['ep_reward_max'] if games else 0.0,
+               'min_ep_reward': raw['ep_reward_min'] if games else 0.0,
+               'num_game': int(games), 'updates': int(upd), 'env_steps': int(steps)}
+        if self.algo == 'a3c' and upd:
+            res.update(avg_policy_loss=raw['policy_loss_sum'] / upd, avg_value_loss=raw['value_loss_sum'] / upd,
+                       avg_entropy=raw['entropy_sum'] / upd)
+        return res
+
+    # ---------------------------------------------------------------- checkpoint / resume
+    @property
+    def worker_step(self):
+        """agent.py:55's loop counter (the lr / epsilon schedules' step) at the next rollout."""
+        c = self.counters.cpu()
+        return int(c[2]) + int(c[0]) - 3
+
+    def set_step(self, global_step, worker_step=None):
+        """Resume from parameters + step (the reference's Saver, agent.py:29): the global step and
+        the workers' loop counter restart there (agent.py:34,46)."""
+        w = global_step if worker_step is None else worker_step
+        check(lib().a3c_engine_set_step(self._h, int(global_step), int(w), _lib.stream_handle()),
+              'a3c_engine_set_step')
+
+    def save_state(self):
+        """The whole engine state as a host u8 array (parameters, RMSProp slots, counters, envs,
+        frame ring, LSTM carry, the overlap pipeline's rollout in flight)."""
+        nb = _lib.c_i64()
+        check(lib().a3c_engine_state_bytes(self._h, ctypes.byref(nb)), 'a3c_engine_state_bytes')
+        buf = np.empty(int(nb.value), np.uint8)
+        check(lib().a3c_engine_state_save(self._h, buf.ctypes.data_as(ctypes.c_void_p), buf.size,
+                                          _lib.stream_handle()), 'a3c_engine_state_save')
+        return buf
+
+    def load_state(self, buf):
+        """Restore save_state()'s array into this (reset) engine of the same configuration; the
+        next iteration continues the saved run bit for bit."""
+        buf = np.ascontiguousarray(np.asarray(buf, np.uint8))
+        check(lib().a3c_engine_state_load(self._h, buf.ctypes.data_as(ctypes.c_void_p), buf.size,
+                                          _lib.stream_handle()), 'a3c_engine_state_load')
 
     def advance(self):
         check(lib().a3c_engine_advance(self._h, _lib.stream_handle()), 'a3c_engine_advance')

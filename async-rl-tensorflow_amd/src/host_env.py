@@ -24,11 +24,18 @@ SCREEN_SHAPE = (210, 160, 3)
 class AtariEnv(object):
   """One game with environment.py:14-96 semantics on raw frames (u8 [210,160,3])."""
 
-  def __init__(self, gym_env, action_repeat=1, random_start=30, rng=None):
+  def __init__(self, gym_env, action_repeat=1, random_start=30, rng=None, seed=None):
     self.env = gym_env
     self.action_repeat = int(action_repeat)
     self.random_start = int(random_start)
     self.rng = rng if rng is not None else _random     # environment.py:37 uses module `random`
+    # emulator seed: gym < 0.26 has env.seed(s); newer gym seeds through the first reset(seed=s)
+    self._reset_seed = None
+    if seed is not None:
+      if callable(getattr(gym_env, 'seed', None)):
+        gym_env.seed(int(seed))
+      else:
+        self._reset_seed = int(seed)
     self._screen = None
     self.reward = 0
     self.terminal = True
@@ -53,7 +60,11 @@ class AtariEnv(object):
 
   def new_game(self, from_random_game=False):          # environment.py:28-33
     if self.lives == 0:
-      out = self.env.reset()
+      if self._reset_seed is not None:
+        out = self.env.reset(seed=self._reset_seed)
+        self._reset_seed = None
+      else:
+        out = self.env.reset()
       self._screen = out[0] if isinstance(out, tuple) else out
     self._step(0)
     return self._screen, 0, 0, self.terminal

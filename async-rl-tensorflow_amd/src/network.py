@@ -20,6 +20,7 @@ import torch
 from . import _lib
 from . import kernels as K
 from . import ops
+from . import checkpoint as C
 from .base import load_checkpoint, save_checkpoint
 
 
@@ -198,7 +199,8 @@ class Network(object):
     print(" [*] Saving checkpoints...")
     os.makedirs(checkpoint_dir, exist_ok=True)
     name = type(self).__name__ + ('-%d' % step if step is not None else '')
-    return save_checkpoint(os.path.join(checkpoint_dir, name), self.w, step or 0)
+    named = {C.tf_name(k, 'a3c', self.dqn_type): v for k, v in self.w.items()}     # network.py scopes
+    return save_checkpoint(os.path.join(checkpoint_dir, name), named, step or 0)
 
   def load_model(self, saver, checkpoint_dir):
     files = sorted(glob.glob(os.path.join(checkpoint_dir, type(self).__name__ + '*.npz')), key=os.path.getmtime)
@@ -206,8 +208,9 @@ class Network(object):
       print(" [!] Load FAILED: %s" % checkpoint_dir)
       return False
     arrays, step = load_checkpoint(files[-1])
-    for name, v in arrays.items():
-      if name in self.w:
-        self.w[name].copy_(torch.as_tensor(v).reshape(self.w[name].shape))
+    for name, w in self.w.items():
+      v = arrays.get(C.tf_name(name, 'a3c', self.dqn_type))
+      if v is not None:
+        w.copy_(torch.as_tensor(v).reshape(w.shape))
     print(" [*] Load SUCCESS: %s" % files[-1])
     return True

@@ -301,7 +301,7 @@ int a3c_engine_destroy(a3c_engine* eng);
 int a3c_engine_reset(a3c_engine* eng, const float* host_params, void* stream);
 /* n rollout steps + bootstrap + loss + backward + per-tensor clip -> grads */
 int a3c_engine_rollout_grad(a3c_engine* eng, void* stream);
-/* RMSProp apply of grads (lr from the device global step) and advance counters.
+/* RMSProp apply of grads (lr from the device worker step, agent.py:393-395) and advance counters.
  * overlap: a no-op until the pipeline holds a gradient (first call after reset). */
 int a3c_engine_apply(a3c_engine* eng, void* stream);
 /* a3c_engine_rollout_grad + a3c_engine_apply as one enqueue (single GPU, device envs only: no
@@ -331,6 +331,41 @@ int a3c_engine_advance(a3c_engine* eng, void* stream);
 int a3c_engine_apply_shard(a3c_engine* eng, const float* grads_by_rank, int nranks, int64_t lo, int64_t n,
                            float* w_out, void* stream);
 int a3c_engine_apply_commit(a3c_engine* eng, const float* params_src, void* stream);
+
+/* ----------------------------------------------------------------------------
+ * Summaries: the aggregates train_with_summary logs every test_step
+ * (agent.py:69-139), kept on device over every env of this GPU.
+ *  stats_accumulate: adds the rollout whose gradient the last rollout_grad / iterate computed
+ *                    (enqueue after it on the same stream; a no-op while no gradient is ready).
+ *  stats_read:       waits for `stream`, copies the A3C_STATS_N doubles; reset = 1 starts a new
+ *                    interval (each env's running episode reward carries on).
+ * out: [0] sum of act() rewards (unclipped, every env-step; agent.py:101), [1] sum, [2] max,
+ *      [3] min of finished episodes' rewards (the terminal step's reward excluded, agent.py:91-98;
+ *      max -inf / min +inf when none), [4] games, [5] sum over updates of the per-sample loss
+ *      (q: the MSE, agent.py:196; a3c: total / (n*E)), [6] sum over updates of the batch mean
+ *      Q(s) (q: over actions, agent.py:200; a3c: V(s)), [7] updates, [8] env-steps, [9..11] sums
+ *      of per-sample policy loss, value loss, entropy (a3c). */
+#define A3C_STATS_N 16
+int a3c_engine_stats_accumulate(a3c_engine* eng, void* stream);
+int a3c_engine_stats_read(a3c_engine* eng, double* out, int reset, void* stream);
+
+/* ----------------------------------------------------------------------------
+ * Checkpoint / resume.  Replaces the Supervisor's Saver (main.py:74-90, which saves
+ * the prediction weights + `step` every 600 s, agent.py:29) and its restore at managed_session.
+ *  set_step:    resume from parameters + step only (what the reference's Saver keeps; the caller
+ *               writes params / target / RMSProp slots through a3c_engine_get_buffers): the global
+ *               step T (agent.py:165) and the workers' loop counter (agent.py:34,46,55: the lr and
+ *               epsilon schedules run on it) restart at the given values.  After a3c_engine_reset.
+ *  state_*:     the whole engine state -- parameters, target, RMSProp slots, counters, env state,
+ *               frame ring, LSTM carry and, in overlap mode, the rollout in flight -- so a restored
+ *               engine of the same configuration continues the run bit for bit.  state_save / load
+ *               wait for the engine's streams; load needs a3c_engine_reset first (frame pool).
+ *               Engines with host-stepped envs (external_env) refuse: the host envs cannot be
+ *               snapshotted, they resume with set_step. */
+int a3c_engine_set_step(a3c_engine* eng, int64_t global_step, int64_t worker_step, void* stream);
+int a3c_engine_state_bytes(a3c_engine* eng, int64_t* bytes);
+int a3c_engine_state_save(a3c_engine* eng, void* host, int64_t bytes, void* stream);
+int a3c_engine_state_load(a3c_engine* eng, const void* host, int64_t bytes, void* stream);
 
 /* ----------------------------------------------------------------------------
  * External (host-stepped) environments, cfg.external_env = 1.  Per rollout:
@@ -379,8 +414,9 @@ typedef struct a3c_engine_buffers {
   int64_t n_params;
   uint8_t* frame_ring;     /* [E][R][84*84] u8                                */
   int ring_slots;
-  int64_t* tau;            /* device: current frame index tau                 */
-  int64_t* global_step;    /* device: env-steps taken by all GPUs             */
+  int64_t* tau;            /* device: current frame index tau; tau[2] = the workers' base step
+                              (worker step of rollout step t = tau[2] + tau - 3 + t)  */
+  int64_t* global_step;    /* device: env-steps taken by all GPUs (= tau + 1)  */
   int32_t* actions;        /* [n][E]                                           */
   float* rewards;          /* [n][E]                                           */
   uint8_t* terminals;      /* [n][E]                                           */

@@ -35,6 +35,9 @@ class EngineRef:
         self.R = self.n + 4 + (1 if algo == 'q' else 0)
         self.ring = np.zeros((self.E, self.R, 84, 84), np.uint8)
         self.tau, self.global_step = 3, 0
+        # the workers' base step: the loop counter of agent.py:55 starts at the global step read
+        # in before_train (agent.py:34); worker step of rollout step t = wstep0 + tau - 3 + t
+        self.wstep0 = 0
         self.params = {k: np.array(v, np.float32) for k, v in params.items()}
         self.tparams = {k: v.copy() for k, v in self.params.items()}
         self.ms = {k: np.ones_like(v) for k, v in self.params.items()}      # TF1 rms slot = 1
@@ -76,7 +79,7 @@ class EngineRef:
             s = self.screen_of(self.env.frame[e])
             for c in range(4):
                 self.ring[e, c % self.R] = s
-        self.tau, self.global_step = 3, 0
+        self.tau, self.global_step, self.wstep0 = 3, 0, 0
         if self.lstm:
             self.hc = (np.zeros_like(self.hc[0]), np.zeros_like(self.hc[1]))
 
@@ -103,15 +106,20 @@ class EngineRef:
         if self.algo == 'a3c':
             pi, _, _ = R.softmax_stats(z[:, :self.A])
             return R.sample_categorical(pi.astype(np.float32), px.u01(x[0])), pi
-        eps = self.eps()
+        eps = self.eps(t)
         q = z[:, :self.A].astype(np.float32)
         greedy = np.argmax(q, axis=1).astype(np.int32)
         rnd = (x[1] % np.uint32(self.A)).astype(np.int32)
         return np.where(px.u01(x[0]) < eps, rnd, greedy).astype(np.int32), None
 
-    def eps(self):
+    def worker_step(self, t=0, tau=None):
+        """agent.py:55's loop counter at rollout step t of the rollout starting at tau."""
+        return self.wstep0 + (self.tau if tau is None else tau) - 3 + t
+
+    def eps(self, t=0):
+        """agent.py:142-144 at the worker step of rollout step t."""
         h = self.h
-        step = float(self.global_step)
+        step = float(self.worker_step(t))
         d = float(h['ep_end_t']) - max(0.0, step - float(h['learn_start']))
         ee = self.ep_end.astype(np.float64)
         return (ee + np.maximum(0.0, (float(h['ep_start']) - ee) * d / float(h['ep_end_t']))).astype(np.float32)
@@ -122,6 +130,7 @@ class EngineRef:
         acts = np.zeros((n, E), np.int32)
         sampled = np.zeros((n, E), np.int32)
         rewards = np.zeros((n, E), np.float32)
+        rewards_raw = np.zeros((n, E), np.float32)
         terms = np.zeros((n, E), np.uint8)
         zs, pis, frames = [], [], []
         h0c0 = self.hc
@@ -134,6 +143,7 @@ class EngineRef:
             zs.append(z)
             pis.append(pi)
             frame, reward, term = self.env.act(acts[t], is_training=True)
+            rewards_raw[t] = reward
             rewards[t] = np.clip(reward, -1.0, 1.0)                      # agent.py:154
             terms[t] = term
             if self.lstm:
@@ -146,8 +156,9 @@ class EngineRef:
                 self.env.new_random_game(term.astype(bool))
         states = np.concatenate([self.states(self.tau + t) for t in range(n)])      # b = t*E + e
         B = n * E
-        out = dict(actions=acts, sampled=sampled, rewards=rewards, terminals=terms, z=np.stack(zs),
-                   pi=pis, frames=np.stack(frames))
+        out = dict(actions=acts, sampled=sampled, rewards=rewards, rewards_raw=rewards_raw, terminals=terms,
+                   z=np.stack(zs),
+                   pi=pis, frames=np.stack(frames), tau=self.tau)
         if self.algo == 'a3c':
             zb, _ = self._step_z(self.states(self.tau + n), self.hc)
             Rt = R.nstep_returns(rewards, terms, zb[:, A].astype(np.float32), h['gamma'])
@@ -181,17 +192,18 @@ class EngineRef:
         out.update(losses=losses, grads=grads, sumsq=sumsq, clipped=clipped, z_batch=fwd['z'])
         return out
 
-    def apply(self, clipped, advance_tau=True):
+    def apply(self, clipped, advance_tau=True, tau=None):
         """RMSProp apply (+ q target sync).  advance_tau=False: the caller advances tau at
-        rollout time (the engine's overlap pipeline, where rollout k+1 precedes apply k)."""
-        return self.apply_sequence([clipped], advance_tau)
+        rollout time (the engine's overlap pipeline, where rollout k+1 precedes apply k); tau: the
+        applied rollout's start (default: the current tau, the synchronous order)."""
+        return self.apply_sequence([clipped], advance_tau, tau)
 
-    def apply_sequence(self, clipped_seq, advance_tau=True):
+    def apply_sequence(self, clipped_seq, advance_tau=True, tau=None):
         """The reference PS's rule for several workers (main.py:63-65, agent.py:321): every
         worker's clipped gradient is an RMSProp step of its own, applied in the given (arrival)
         order with this iteration's learning rate; then the target sync / counters once."""
         h = self.h
-        lr = self.next_lr()
+        lr = self.next_lr(tau)
         for clipped in clipped_seq:
             for k in self.params:
                 R.rmsprop_apply(self.params[k], self.ms[k], self.mom[k], clipped[k].astype(np.float32), lr,
@@ -199,11 +211,12 @@ class EngineRef:
         self.finish_update(advance_tau)
         return lr
 
-    def next_lr(self):
-        """Learning rate of the pending update (agent.py:393-395 at the step after it)."""
+    def next_lr(self, tau=None):
+        """Learning rate of the update of the rollout starting at tau: agent.py:393-395 evaluated
+        at the worker's own step (agent.py:55 `self.step`, not the global T) of the rollout's last
+        env step, whose observe runs the update (agent.py:162-163)."""
         h = self.h
-        inc = self.n * self.E * self.world
-        return R.learning_rate(self.global_step + inc, h['max_step'], h['learning_rate'])
+        return R.learning_rate(self.worker_step(self.n - 1, tau), h['max_step'], h['learning_rate'])
 
     def finish_update(self, advance_tau=True):
         """Target sync (q, agent.py:166-167) and counter advance of an applied update."""

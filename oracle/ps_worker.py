@@ -61,7 +61,7 @@ def _worker(wid, E, n, A, algo, lives, seed, seconds, shm_name, layout, start_ev
         for k in ref.params:                           # theta' <- theta (pull from the PS)
             ref.params[k][...] = shared_p[k]
         out = ref.iterate()
-        lr = R.learning_rate(iters * E * n, ref.h['max_step'], ref.h['learning_rate'])
+        lr = ref.next_lr()                             # agent.py:393-395 at this worker's own step
         for k in shared_p:                             # unlocked shared RMSProp apply
             R.rmsprop_apply(shared_p[k], shared_ms[k], shared_mom[k], out['clipped'][k], lr,
                             ref.h['decay'], ref.h['momentum'], ref.h['epsilon'])

@@ -203,7 +203,7 @@ def check_overlap_vs_oracle(A, E, n, lives, rollouts=5, seed=77, frames=48, scal
         for name, _ in ns:
             assert rel_l2(G[name], g_same[name]) < 1e-4, (k, name, rel_l2(G[name], g_same[name]))
             assert rel_l2(G[name], out_p['grads'][name]) < 2e-2, (k, name)
-        ref.apply({kk: Rc.clip_by_norm(v, 40.0) for kk, v in g_same.items()}, advance_tau=False)
+        ref.apply({kk: Rc.clip_by_norm(v, 40.0) for kk, v in g_same.items()}, advance_tau=False, tau=out_p['tau'])
         assert_params(eng, ns, ref, k)
         assert int(eng.counters[1].item()) == ref.global_step
     return eng, ref

@@ -415,15 +415,18 @@ def test_main_engine_mode_host_envs(tmp_path, update):
 def test_main_engine_mode_initialises_params_and_stops_at_max_step(tmp_path):
     """main.py --mode engine starts from the reference initialisers (conv truncated_normal(0,
     0.02) agent.py:214, linear normal(0.02) ops.py:36-37, zero biases), not from whatever
-    hipMalloc returned, and trains no further than max_step (agent.py:46,55-57)."""
+    hipMalloc returned, and trains no further than max_step on each worker's own loop counter
+    (agent.py:46,55: `for self.step in xrange(self.step, self.max_step)`; here every env is such a
+    worker, stepping in lock-step)."""
     import main
     from src.kernels import param_names_shapes
     E, n = 16, 5
     eng = main.main(['--mode', 'engine', '--env_name', 'Pong-v0', '--num_envs', str(E), '--num_frames', '64',
                      '--iterations', '50', '--log_every', '100', '--logdir', str(tmp_path), '--update', 'sync',
-                     '--max_step', str(3 * E * n - 1), '--random_seed', '7'])
+                     '--max_step', str(3 * n - 1), '--random_seed', '7', '--resume', 'false'])
     torch.cuda.synchronize()
-    assert int(eng.counters[1].item()) == 3 * E * n          # 3 updates reach max_step, then stop
+    assert int(eng.counters[1].item()) == 3 * E * n          # 3 rollouts of n reach max_step, then stop
+    assert eng.worker_step == 3 * n
     flat = eng.params.cpu().numpy()
     ns = param_names_shapes(6, 'a3c')
     for (name, shp), off, size in zip(ns, eng.offsets, eng.sizes):

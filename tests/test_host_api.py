@@ -36,6 +36,38 @@ def test_checkpoint_roundtrip(tmp_path):
     path = save_checkpoint(str(tmp_path / 'a' / 'm'), named, 42)
     arrays, step = load_checkpoint(path)
     assert step == 42 and np.array_equal(arrays['l1_w'], named['l1_w'].numpy())
+    assert int(np.load(path)['step']) == 42           # the global step under its TF name
+
+
+def test_checkpoint_tf_names_and_saver(tmp_path):
+    """Keys follow the TF variable names of the reference graphs (agent.py:218-296 + ops.py,
+    network.py:43-79) and TF1's RMSProp slot names; the Saver keeps max_to_keep checkpoints
+    (agent.py:29) with an index, dropping the oldest and its rank files."""
+    from src import checkpoint as C
+    from src.kernels import param_names_shapes
+    q = [C.tf_name(n, 'q') for n, _ in param_names_shapes(6, 'q')]
+    assert q == ['prediction/l1/w', 'prediction/l1/biases', 'prediction/l2/w', 'prediction/l2/biases',
+                 'prediction/l3/Matrix', 'prediction/l3/bias', 'prediction/q/Matrix', 'prediction/q/bias']
+    assert [C.tf_target_name(n) for n in ('l1_w', 'l3_b', 'q_w')] == \
+        ['target/target_l1/w', 'target/target_l3/bias', 'target/target_q/Matrix']
+    a = [C.tf_name(n, 'a3c') for n, _ in param_names_shapes(6, 'a3c', lstm=True)]
+    assert a == ['l1_conv/w', 'l1_conv/biases', 'l2_conv/w', 'l2_conv/biases', 'l4_linear/Matrix', 'l4_linear/bias',
+                 'policy/linear/Matrix', 'policy/linear/bias', 'value/linear/Matrix', 'value/linear/bias',
+                 'lstm/basic_lstm_cell/weights', 'lstm/basic_lstm_cell/biases']
+    assert C.tf_name('l3_w', 'a3c', 'nature') == 'Nature_DQN/l3_conv/w'
+    assert C.tf_name('p_b', 'a3c', 'nature') == 'policy/linear/bias'
+    assert C.slot_names('l1_conv/w') == ('l1_conv/w/RMSProp', 'l1_conv/w/RMSProp_1')
+    saver = C.Saver(str(tmp_path), max_to_keep=3)
+    assert saver.latest() is None
+    for step in (10, 20, 30, 40):
+        saver.write({'world': np.array(2)}, step, rank=1)
+        saver.save({'step': np.array(step), 'l1_conv/w': np.full(3, step, np.float32)}, step)
+    assert saver.latest().endswith('model.ckpt-40.npz')
+    assert [p.split('-')[-1] for p in saver.kept()] == ['20.npz', '30.npz', '40.npz']
+    assert not (tmp_path / 'model.ckpt-10.npz').exists() and not (tmp_path / 'model.ckpt-10.rank1.npz').exists()
+    assert (tmp_path / 'model.ckpt-20.rank1.npz').exists()
+    got = C.load(saver.latest())
+    assert int(got['step']) == 40 and got['l1_conv/w'][0] == 40
 
 
 def test_initializers():
