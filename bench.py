@@ -3,16 +3,21 @@
 
 One "step" = one engine iteration on every GPU: E envs x n rollout steps (forward, categorical
 draw, synthetic Atari step, Environment.screen preprocessing into the frame ring), bootstrap
-forward, n-step returns, loss + backward, per-tensor clip, sync RCCL all-reduce of the clipped
-gradients (N > 1) and the RMSProp apply.  Inputs (the HBM-resident RGB frame pool) are on the
-device before the timed region.
+forward, n-step returns, loss + backward, per-tensor clip, the RMSProp apply and, for N > 1, the
+multi-GPU exchange: by default the partitioned parameter server (src/distributed.py PartitionedPS:
+RCCL all-to-all of the per-worker-clipped gradients, each owned range stepped once per worker in
+rank order, RCCL all-gather); `--exchange sum` is the plain SUM all-reduce baseline and
+`--update hogwild` the collective-free IPC parameter server.  Inputs (the HBM-resident RGB frame
+pool) are on the device before the timed region.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Rank 0 prints ONE JSON line (value = all GPUs' env-steps / max-over-ranks wall time), with the
-dominant kernel's roofline (HIP-event timing of that kernel on its live buffers) and the CPU
-baseline (oracle/engine_ref.py on host cores, bounded sample).
+dominant kernel's roofline (live in-graph launch spans, plus HIP-event timing of that kernel alone
+on its live buffers) and the CPU baseline: oracle/ps_worker.py, the reference's ps/worker
+algorithm restated in numpy (shared-memory PS, unlocked RMSProp workers) on host cores, bounded
+sample.
 """
 import argparse
 import json
