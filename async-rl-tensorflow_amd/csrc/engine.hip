@@ -1429,3 +1429,37 @@ extern "C" int a3c_engine_span_stats(a3c_engine* e, int which, int reset, double
   if (launches) *launches = n;
   return 0;
 }
+
+// Per-step split of the k_head_screen_conv12 records.  Step t of the rollout at tau writes record
+// (tau + t + 1) % SPAN_RECS (its Conv12Next reads state tau + t + 1), and every rollout's tau is
+// congruent to the live counter modulo n, so record r belongs to the most recent value
+// v = tau + t + 1 <= tau_now + n with v = r (mod SPAN_RECS), and t = (v - 1 - tau_now) mod n.
+extern "C" int a3c_engine_span_steps(a3c_engine* e, double* avg_us, int64_t* launches) {
+  if (!e || !avg_us || !launches) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_span_steps", "bad argument");
+  const int n = e->n;
+  const size_t per = (size_t)SPAN_RECS * SPAN_WGS * 2;
+  std::vector<unsigned long long> h(per);
+  int64_t tau_now = 0;
+  A3C_CHECK(hipDeviceSynchronize());
+  A3C_CHECK(hipMemcpy(h.data(), e->spans + per, per * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  A3C_CHECK(hipMemcpy(&tau_now, e->counters, sizeof(int64_t), hipMemcpyDeviceToHost));
+  std::vector<double> sum(n, 0.0);
+  for (int t = 0; t < n; ++t) launches[t] = 0;
+  for (int r = 0; r < SPAN_RECS; ++r) {
+    unsigned long long lo = ~0ull, hi = 0ull;
+    for (int w = 0; w < SPAN_WGS; ++w) {
+      const unsigned long long a = h[2 * ((size_t)r * SPAN_WGS + w)], b = h[2 * ((size_t)r * SPAN_WGS + w) + 1];
+      if (a == ~0ull || b == 0ull) continue;
+      lo = a < lo ? a : lo;
+      hi = b > hi ? b : hi;
+    }
+    if (hi == 0ull || lo == ~0ull || hi < lo) continue;
+    const int64_t top = tau_now + n;
+    const int64_t v = top - (((top - r) % SPAN_RECS) + SPAN_RECS) % SPAN_RECS;
+    const int t = (int)((((v - 1 - tau_now) % n) + n) % n);
+    sum[t] += (double)(hi - lo) * 0.01;
+    launches[t] += 1;
+  }
+  for (int t = 0; t < n; ++t) avg_us[t] = launches[t] ? sum[t] / (double)launches[t] : 0.0;
+  return 0;
+}

@@ -377,6 +377,13 @@ class Engine:
                                           ctypes.byref(mx), ctypes.byref(cnt)), 'a3c_engine_span_stats')
         return float(avg.value), float(mx.value), int(cnt.value)
 
+    def span_steps(self):
+        """k_head_screen_conv12's live spans split by rollout step: ([avg_us] * n, [launches] * n)."""
+        avg = (ctypes.c_double * self.n)()
+        cnt = (ctypes.c_int64 * self.n)()
+        check(lib().a3c_engine_span_steps(self._h, avg, cnt), 'a3c_engine_span_steps')
+        return [round(float(a), 2) for a in avg], [int(c) for c in cnt]
+
     def time_kernel(self, kernel, iters=20):
         """Average device ms of one engine kernel (HIP events on the current stream)."""
         out = ctypes.c_float()

@@ -218,6 +218,8 @@ def main():
     if live:
         spans['k_conv_bwd'] = eng.span_stats(0)
         spans['k_head_screen_conv12'] = eng.span_stats(1)
+        if eng.overlap:     # per rollout step (the last step's launch also runs the bootstrap conv)
+            spans['k_head_screen_conv12_by_step'] = eng.span_steps()
     loss = eng.loss.cpu().numpy().tolist()
     finite = bool(torch.isfinite(eng.params).all().item())
 
@@ -274,6 +276,8 @@ def main():
             else:
                 ach = w / (ms[k] * 1e-3) / (1e12 if bound == 'mfma' else 1e9)
                 kernels[k].update(achieved=round(ach, 2), unit='TFLOP/s' if bound == 'mfma' else 'GB/s')
+        if 'k_head_screen_conv12_by_step' in spans and 'k_head_screen_conv12' in kernels:
+            kernels['k_head_screen_conv12']['live_us_by_step'] = spans['k_head_screen_conv12_by_step'][0]
         dom = max(ms, key=lambda k: live_ms.get(k, ms[k]) * count[k])
         bound, w = work[dom]
         t_dom = live_ms.get(dom, ms[dom])

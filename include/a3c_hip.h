@@ -456,6 +456,11 @@ int a3c_engine_slot_buffers(a3c_engine* eng, int slot, a3c_engine_buffers* out);
  * average and max span in microseconds and the number of launches recorded (at most 1024). */
 int a3c_engine_span_stats(a3c_engine* eng, int which, int reset, double* avg_us, double* max_us,
                           int64_t* launches);
+/* The same records of k_head_screen_conv12 (which = 1) split by rollout step: avg_us[t] is the
+ * average live span of the launch that runs step t's head (t = 0..n-1; the last one also runs the
+ * bootstrap state's conv1+conv2), launches[t] how many were recorded.  Call synchronised, after a
+ * timed region with no a3c_engine_set_step/reset since the records were cleared. */
+int a3c_engine_span_steps(a3c_engine* eng, double* avg_us, int64_t* launches);
 int a3c_engine_time_kernel(a3c_engine* eng, int kernel, int iters, void* stream, float* avg_ms);
 
 #ifdef __cplusplus
