@@ -520,8 +520,15 @@ static int enqueue_rollout_begin(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
   // params are fixed for the rollout; overlap: the prep kernel also snapshots tau for the slot's
   // backward (sync: the slot's tau is the live counter)
-  int rc = a3c_prep_fwd_launch(e->L, sl.P, sl.prep, s, e->overlap ? e->counters : nullptr,
-                               e->overlap ? sl.tau : nullptr);
+#ifdef A3C_ABL_PREP
+  static int abl_prep_n = 0;   // measurement only: no forward-weight prep after the first rollouts
+  int rc = 0;
+  if (abl_prep_n++ < 4)
+#else
+  int rc =
+#endif
+  rc = a3c_prep_fwd_launch(e->L, sl.P, sl.prep, s, e->overlap ? e->counters : nullptr,
+                           e->overlap ? sl.tau : nullptr);
   if (rc) return rc;
   if (e->L.lstm) {
     rc = a3c_lstm_transpose_launch(sl.P + e->L.off[T_LW], sl.lwt, s);
@@ -590,6 +597,9 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
     nx.W2 = sl.P + L.off[T_L2W];
     nx.b2 = sl.P + L.off[T_L2B];
     nx.act_l1 = t + 1 < n ? sl.act_l1 + (o + E) * C1_P * C1_N : nullptr;
+#ifdef A3C_ABL_NOL1
+    nx.act_l1 = nullptr;   // measurement only: the fused rollout kernel saves no conv1 output
+#endif
     nx.act_l2 = t + 1 < n ? sl.act_l2 + (o + E) * FLAT : sl.scr_l2;
   }
   int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
@@ -650,6 +660,7 @@ __global__ void k_mark(int id) {
   }
 }
 static void mark(int id, hipStream_t s) { hipLaunchKernelGGL(k_mark, dim3(1), dim3(1), 0, s, id); }
+void a3c_mark(int id, hipStream_t s) { mark(id, s); }   // (net_bwd.hip: 4 = conv backward start, 5 = its end)
 extern "C" int a3c_debug_marks(unsigned long long* host, int reset) {
   A3C_CHECK(hipDeviceSynchronize());
   A3C_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_marks), sizeof(g_marks)));
@@ -1427,6 +1438,32 @@ extern "C" int a3c_engine_span_stats(a3c_engine* e, int which, int reset, double
   if (avg_us) *avg_us = n ? sum / (double)n : 0.0;
   if (max_us) *max_us = mx;
   if (launches) *launches = n;
+  return 0;
+}
+
+// Raw records (measurement): out[2 r] / out[2 r + 1] = first workgroup start / last workgroup end
+// (s_memrealtime, 0 when not recorded) of record r of `which`; *tau_now = the live tau counter.
+extern "C" int a3c_engine_span_raw(a3c_engine* e, int which, unsigned long long* out, int64_t* tau_now) {
+  if (!e || which < 0 || which > 1 || !out || !tau_now)
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_span_raw", "bad argument");
+  const size_t per = (size_t)SPAN_RECS * SPAN_WGS * 2;
+  std::vector<unsigned long long> h(per);
+  A3C_CHECK(hipDeviceSynchronize());
+  A3C_CHECK(hipMemcpy(h.data(), e->spans + (size_t)which * per, per * sizeof(unsigned long long),
+                      hipMemcpyDeviceToHost));
+  A3C_CHECK(hipMemcpy(tau_now, e->counters, sizeof(int64_t), hipMemcpyDeviceToHost));
+  for (int r = 0; r < SPAN_RECS; ++r) {
+    unsigned long long lo = ~0ull, hi = 0ull;
+    for (int w = 0; w < SPAN_WGS; ++w) {
+      const unsigned long long a = h[2 * ((size_t)r * SPAN_WGS + w)], b = h[2 * ((size_t)r * SPAN_WGS + w) + 1];
+      if (a == ~0ull || b == 0ull) continue;
+      lo = a < lo ? a : lo;
+      hi = b > hi ? b : hi;
+    }
+    const bool ok = hi != 0ull && lo != ~0ull && hi >= lo;
+    out[2 * r] = ok ? lo : 0ull;
+    out[2 * r + 1] = ok ? hi : 0ull;
+  }
   return 0;
 }
 

@@ -22,6 +22,10 @@ struct GemmArgs {
   int kchunk;                 // set by a3c_gemm
   float* colsum;              // optional [nsplit_eff][N] column sums of B over each K-chunk
   int defer_reduce;           // a3c_gemm: leave the split-K fold to the caller (a3c_gemm_reduce)
+  // XCD-aware tile order (a3c_gemm): 0 = plain 3-D grid; 1 = the N-tiles of one (M-tile, K-chunk)
+  // on one XCD (they share the A strip); 2 = the M-tiles of one (N-tile, K-chunk) on one XCD
+  // (they share the B strip).  Speed only: every tile computes the same sums in the same order.
+  int xcd;
 };
 
 int a3c_gemm(bool a_kcontig, bool b_ncontig, GemmArgs g, hipStream_t s);

@@ -6,6 +6,7 @@
 // Tile 64x64x16, 256 threads = 2x2 waves of 32x32, LDS-staged operands with a register
 // prefetch of the next K-tile, optional split-K into fp32 slabs (reduced by k_reduce_slabs
 // with the epilogue) and an optional fused column sum of the B operand (bias gradients).
+#include <cstdlib>
 #include "gemm.h"
 
 #define BM 64
@@ -123,6 +124,22 @@ __global__ void __launch_bounds__(256) k_gemm_f32(GemmArgs g) {
   gemm_tile<A_KC, B_NC>(g, blockIdx.x, blockIdx.y, blockIdx.z, As, Bs);
 }
 
+// The same tiles on a 1-D grid in XCD-grouped order: workgroup id goes to XCD id % 8 under the
+// round-robin dispatch, so the J tiles of group g (which share one operand strip) all get ids
+// with id % 8 == g % 8 and that strip is fetched from HBM by one XCD's L2 instead of several.
+// Ids past the last group exit at once.
+template <bool A_KC, bool B_NC>
+__global__ void __launch_bounds__(256) k_gemm_f32_x(GemmArgs g, int G, int J) {
+  __shared__ __attribute__((aligned(16))) float As[BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[BK][BN + PAD];
+  const int id = blockIdx.x, slot = id >> 3;
+  const int grp = 8 * (slot / J) + (id & 7), j = slot % J;
+  if (grp >= G) return;
+  const int gx = (g.N + BN - 1) / BN, gy = (g.M + BM - 1) / BM;
+  if (g.xcd == 1) gemm_tile<A_KC, B_NC>(g, j, grp % gy, grp / gy, As, Bs);
+  else gemm_tile<A_KC, B_NC>(g, grp % gx, j, grp / gx, As, Bs);
+}
+
 // Several independent GEMMs in one launch (the backward's dW_head, dW_fc and dl2 all need only
 // dz / dl3): workgroup ids [0, nb[0]) are GEMM 0's tiles, then GEMM 1's, then GEMM 2's -- one
 // kernel boundary instead of three and one fill/drain tail.  Flavours: (A k-contiguous, B
@@ -213,6 +230,20 @@ int a3c_gemm(bool a_kc, bool b_nc, GemmArgs g, hipStream_t s) {
   int rc = gemm_setup(a_kc, b_nc, g);
   if (rc) return rc;
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, g.nsplit);
+  // (off by default: it halves the backward GEMMs' HBM bytes, 124 -> 73 MB per iteration, but
+  // the overlapped bench drops 4.56M -> 4.05M env-steps/s: tools/ab.sh, profile r3v1)
+  static const int env_xcd = getenv("A3C_GEMM_XCD") ? atoi(getenv("A3C_GEMM_XCD")) : 0;
+  if (g.xcd && env_xcd) {
+    const int G = g.xcd == 1 ? (int)(grid.y * grid.z) : (int)(grid.x * grid.z);
+    const int J = g.xcd == 1 ? (int)grid.x : (int)grid.y;
+    const dim3 g1((unsigned)(8 * ((G + 7) / 8) * J));
+    if (a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_x<true, true>), g1, dim3(256), 0, s, g, G, J);
+    else if (a_kc && !b_nc) hipLaunchKernelGGL((k_gemm_f32_x<true, false>), g1, dim3(256), 0, s, g, G, J);
+    else if (!a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_x<false, true>), g1, dim3(256), 0, s, g, G, J);
+    else hipLaunchKernelGGL((k_gemm_f32_x<false, false>), g1, dim3(256), 0, s, g, G, J);
+    A3C_CHECK(hipGetLastError());
+    return g.defer_reduce ? 0 : a3c_gemm_reduce(g, s);
+  }
   if (a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32<true, true>), grid, dim3(256), 0, s, g);
   else if (a_kc && !b_nc) hipLaunchKernelGGL((k_gemm_f32<true, false>), grid, dim3(256), 0, s, g);
   else if (!a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32<false, true>), grid, dim3(256), 0, s, g);

@@ -19,6 +19,9 @@
 #include "net.h"
 #include "gemm.h"
 #include "net_bwd.h"
+#ifdef A3C_MARKERS
+void a3c_mark(int id, hipStream_t s);
+#endif
 
 // ---------------------------------------------------------------------------------------
 __global__ void k_returns(const float* __restrict__ rewards, const uint8_t* __restrict__ terms,
@@ -327,6 +330,77 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     // LDS addresses out of the sample loop (they would pin ~80 VGPRs)
     int bj4 = j4, bi16 = i16;
     asm volatile("" : "+v"(bj4), "+v"(bi16));
+    // Two forms of (b), bit-identical.  The branch-free one below is faster alone (conv backward
+    // 131 -> 122 us compact, 82 -> 77 us DMA) but its denser MFMA issue slows the co-resident
+    // rollout more than it saves in overlap mode (4.45M vs 4.57M env-steps/s, tools/ab.sh): the
+    // 8-wave sync kernel takes it (3.48M vs 3.45M), the compact overlap kernel keeps the old one.
+#ifdef CB_NEWB_ALL
+    constexpr bool NEWB = true;
+#else
+    constexpr bool NEWB = NW == 8;
+#endif
+    if constexpr (NEWB) {
+    // One basic block per sample: the epilogue is branch-free, so the scheduler can run a tile's
+    // address math, ReLU-mask reads and next operands under the previous tile's MFMAs.  Rows past
+    // position 99 (tile 6) duplicate row 99: their A rows are row 99's (clamped), so their D rows
+    // are bit-identical to it, the mask is read before any write of the tile, and all of them
+    // store the same value into position 99's slot; only their db1 contribution is dropped.
+    // (tile loop rolled: unrolled, the scheduler hoists every tile's addresses and spills)
+#pragma unroll 1
+    for (int u = 0; u < MTB; ++u) {
+      const int mt = mt_lo + u;
+      if (mt >= mt_hi) break;
+      const int pc = 16 * mt + bi16;
+      const int pcc = pc < 100 ? pc : 99;
+      const int ay = pcc / 10, cx = pcc - ay * 10;
+      const int base = ay * C2_O + cx;
+      // epilogue slots of rows r = 0..3: p = p0 + 2 rr + 20 [cx0 + rr >= 10], rr = min(r, 99 - prc0)
+      const int pr0 = 16 * mt + 4 * bj4;
+      const int prc0 = pr0 < 100 ? pr0 : 99;
+      const int ay0 = prc0 / 10, cx0 = prc0 - ay0 * 10;
+      const int p0 = (2 * ay0 + py) * C1_O + 2 * cx0 + px;
+      int eo[4];
+      float msk[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = min(r, 99 - prc0);
+        eo[r] = (p0 + 2 * rr + (cx0 + rr >= 10 ? 20 : 0)) * CB_L1_LD + bi16;
+        msk[r] = l1s[eo[r]];                    // l1 (the ReLU mask), before any write of the tile
+      }
+      int qo[4];
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx) {
+          // dl2 position (ay - dy, cx - dx); off the 9x9 grid -> the zero row
+          const bool v = (dy ? ay > 0 : ay < C2_O) && (dx ? cx > 0 : cx < C2_O);
+          qo[dy * 2 + dx] = (v ? base - C2_O * dy - dx : C2_Q) * CB_DL2_LD + 4 * bj4;
+        }
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accb = {0.f, 0.f, 0.f, 0.f};   // two chains (nb)
+      f32x4 op[2][2];                          // two taps' operands in flight
+      op[0][0] = *(const f32x4*)(dl2s + qo[0]);
+      op[0][1] = *(const f32x4*)(dl2s + qo[0] + 16);
+#pragma unroll
+      for (int tp = 0; tp < 4; ++tp) {
+        if (tp + 1 < 4) {
+          op[(tp + 1) & 1][0] = *(const f32x4*)(dl2s + qo[tp + 1]);
+          op[(tp + 1) & 1][1] = *(const f32x4*)(dl2s + qo[tp + 1] + 16);
+        }
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(op[tp & 1][0][c4], w2c[tp * 8 + c4], acc, 0, 0, 0);
+          accb = __builtin_amdgcn_mfma_f32_16x16x4f32(op[tp & 1][1][c4], w2c[tp * 8 + 4 + c4], accb, 0, 0, 0);
+        }
+      }
+      acc += accb;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float g = msk[r] > 0.f ? acc[r] : 0.f;
+        l1s[eo[r]] = g;                          // dl1 in place over l1 (this lane's own slot)
+        db1acc = pr0 + r < 100 ? db1acc + g : db1acc;
+      }
+    }
+    } else {
 #pragma unroll
     for (int u = 0; u < MTB; ++u) {
       const int mt = mt_lo + u;
@@ -364,6 +438,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
           db1acc += g;
         }
       }
+    }
     }
     // db2[n] += sum_q dl2[q][n]
     if (tid < C2_N) {
@@ -656,6 +731,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   gf.C = grads + L.off[T_FCW]; gf.ldc = FC;
   gf.M = FLAT; gf.N = FC; gf.K = (int)B;
   gf.epi = EPI_STORE; gf.slab = ws + p.fcslab; gf.nsplit = p.fc_split; gf.colsum = ws + p.fccol;
+  gf.xcd = 1;                           // the 4 column tiles of an l2 strip on one XCD
   // dl2[B][2592] = (dl3 W^T) * (l2 > 0)
   GemmArgs gd = {};
   gd.A = dh3; gd.lda = FC;               // A(m=b, k) = dl3[b][k]
@@ -663,6 +739,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   gd.C = dl2; gd.ldc = FLAT;
   gd.M = (int)B; gd.N = FLAT; gd.K = FC;
   gd.epi = EPI_MASK; gd.mask = act_l2; gd.ldm = FLAT; gd.nsplit = 1;
+  gd.xcd = 2;                           // the 20 row tiles of a W strip on one XCD
   int rc;
   // sync mode: the three GEMMs in one launch (3.32M -> 3.41M env-steps/s); overlapped with the
   // next rollout the 1,420-workgroup launch slows it more than it gains (4.40M -> 4.30M), and so
@@ -689,15 +766,26 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     if (!rc) rc = a3c_gemm_reduce(gf, s);
     if (rc) return rc;
   } else {
-    rc = a3c_gemm(false, true, gh, ws_s);
+#ifdef A3C_MARKERS
+    static const bool abl_gemm = getenv("A3C_ABL_GEMM") != nullptr;   // measurement only: no fc/head GEMMs
+#else
+    constexpr bool abl_gemm = false;
+#endif
+    rc = abl_gemm ? 0 : a3c_gemm(false, true, gh, ws_s);
     if (rc) return rc;
-    rc = a3c_gemm(false, true, gf, ws_s);
+    rc = abl_gemm ? 0 : a3c_gemm(false, true, gf, ws_s);
     if (rc) return rc;
     if (fork) A3C_CHECK(hipEventRecord(ev_join, side));
-    rc = a3c_gemm(true, false, gd, s);
+    rc = abl_gemm ? 0 : a3c_gemm(true, false, gd, s);
     if (rc) return rc;
+#ifdef A3C_MARKERS
+    a3c_mark(4, s);
+#endif
     rc = a3c_conv_bwd_launch(L, P, sa, B, act_l1, dl2, ws, s);
     if (rc) return rc;
+#ifdef A3C_MARKERS
+    a3c_mark(5, s);
+#endif
   }
 
   FinalizeSegs fs = {};

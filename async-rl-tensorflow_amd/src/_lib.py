@@ -110,6 +110,7 @@ SIGNATURES = {
     'a3c_engine_iterate': (c_int, [c_void_p, c_void_p]),
     'a3c_engine_span_stats': (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     'a3c_engine_span_steps': (c_int, [c_void_p, c_void_p, c_void_p]),
+    'a3c_engine_span_raw': (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
     'a3c_engine_get_buffers': (c_int, [c_void_p, ctypes.POINTER(EngineBuffers)]),
     'a3c_engine_slot_buffers': (c_int, [c_void_p, c_int, ctypes.POINTER(EngineBuffers)]),
     'a3c_engine_grad_ready': (c_int, [c_void_p]),

@@ -461,6 +461,10 @@ int a3c_engine_span_stats(a3c_engine* eng, int which, int reset, double* avg_us,
  * bootstrap state's conv1+conv2), launches[t] how many were recorded.  Call synchronised, after a
  * timed region with no a3c_engine_set_step/reset since the records were cleared. */
 int a3c_engine_span_steps(a3c_engine* eng, double* avg_us, int64_t* launches);
+/* The raw records behind both (measurement): out[2 r], out[2 r + 1] = first workgroup start and
+ * last workgroup end (s_memrealtime ticks, 100 MHz; 0 = not recorded) of record r < 1024 of
+ * `which`, and the live tau counter (records are keyed by tau, see a3c_engine_span_steps). */
+int a3c_engine_span_raw(a3c_engine* eng, int which, unsigned long long* out, int64_t* tau_now);
 int a3c_engine_time_kernel(a3c_engine* eng, int kernel, int iters, void* stream, float* avg_ms);
 
 #ifdef __cplusplus

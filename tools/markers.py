@@ -36,12 +36,16 @@ rows = []
 for a, b in zip(t0s[5:-2], t0s[6:-1]):
     seg = ev[(ev[:, 1] >= a) & (ev[:, 1] < b)]
     r = {'len': (b - a) / 100.0}
-    for k in (1, 2, 3):
+    for k in (1, 2, 3, 4, 5):
         s = seg[seg[:, 0] == k, 1]
         r[k] = (s[0] - a) / 100.0 if len(s) else np.nan
     rows.append(r)
 lens = np.array([r['len'] for r in rows])
 print('%s: %d iterations, mean %.1f us (min %.1f, max %.1f)' % (mode, len(rows), lens.mean(), lens.min(), lens.max()))
-for k, nm in ((1, 'rollout end'), (2, 'backward start'), (3, 'apply end')):
+for k, nm in ((1, 'rollout end'), (2, 'backward start'), (4, 'conv bwd start'), (5, 'conv bwd end'), (3, 'apply end')):
     v = np.array([r[k] for r in rows])
     print('  %-15s at %7.1f us (median %.1f)' % (nm, np.nanmean(v), np.nanmedian(v)))
+# raw marks of three iterations (id, us from the first rollout start shown)
+a = t0s[len(t0s) // 2]
+seg = ev[(ev[:, 1] >= a - 30000) & (ev[:, 1] < a + 3 * 30000)]
+print('raw:', ' '.join('%d@%.1f' % (i, (t - a) / 100.0) for i, t in seg[:40]))
