@@ -695,8 +695,100 @@ static int enqueue_grad(a3c_engine* e, const Slot& sl, hipStream_t s) {
   return rc;
 }
 
+#ifdef A3C_HOG
+// Measurement only (-DA3C_HOG): in place of the backward, a synthetic kernel with the conv
+// backward's footprint (183 workgroups x 4 waves, 74 KB LDS, one wave per SIMD) that keeps one
+// resource busy for A3C_HOG_ITERS loop trips, so the rollout's sensitivity to each kind of
+// co-resident work can be read from its launch spans (tools/span_timeline.py).
+// type: 0 fp32 16x16x4 MFMA, 1 fp32 32x32x2 MFMA, 2 bf16 16x16x32 MFMA, 3 VALU fma, 4 LDS b128
+// reads, 5 s_sleep (occupancy only), 6 HBM stream reads
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k_hog(int type, int iters,
+                                                                                    const float* src, float* out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x & 63;
+  f32x4 a4 = {0.f, 0.f, 0.f, 0.f}, b4 = a4;
+  f32x16 a16 = {}, b16 = {};
+  float x = (float)lane * 1e-3f, y = x + 1.f, z = 0.f;
+  if (type == 0) {
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(x, y, a4, 0, 0, 0);
+        b4 = __builtin_amdgcn_mfma_f32_16x16x4f32(y, x, b4, 0, 0, 0);
+      }
+    }
+  } else if (type == 1) {
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a16 = __builtin_amdgcn_mfma_f32_32x32x2f32(x, y, a16, 0, 0, 0);
+        b16 = __builtin_amdgcn_mfma_f32_32x32x2f32(y, x, b16, 0, 0, 0);
+      }
+    }
+  } else if (type == 2) {
+    bf16x8 av = __builtin_bit_cast(bf16x8, make_uint4(lane, lane + 1, lane + 2, lane + 3));
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        a4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, av, a4, 0, 0, 0);
+        b4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, av, b4, 0, 0, 0);
+      }
+    }
+  } else if (type == 3) {
+    float p = x, q = y, r = x + y, t = x - y;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        p = fmaf(p, 0.999f, 1e-3f); q = fmaf(q, 0.999f, 1e-3f);
+        r = fmaf(r, 0.999f, 1e-3f); t = fmaf(t, 0.999f, 1e-3f);
+      }
+    }
+    z = p + q + r + t;
+  } else if (type == 4) {
+    const uint4* l = (const uint4*)smem;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint4 v = l[(lane + 64 * k + 7 * i) & 1023];
+        acc.x ^= v.x; acc.y += v.y; acc.z ^= v.z; acc.w += v.w;
+      }
+    }
+    z = (float)(acc.x + acc.y + acc.z + acc.w);
+  } else if (type == 5) {
+    for (int i = 0; i < iters; ++i) __builtin_amdgcn_s_sleep(10);
+  } else {
+    const f32x4* g = (const f32x4*)src + (size_t)blockIdx.x * 8192;
+    for (int i = 0; i < iters; ++i) {
+      const f32x4 v = g[(threadIdx.x + 256 * (i & 31)) & 8191];
+      z += v[0] + v[1] + v[2] + v[3];
+    }
+  }
+  float sum = z + a4[0] + b4[1] + a16[0] + b16[3];
+  if (sum == 1234.5f) out[blockIdx.x * 256 + threadIdx.x] = sum;   // (keeps the work alive)
+}
+#endif
+
 static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
+#ifdef A3C_HOG
+  {
+    static const int hog_type = getenv("A3C_HOG_TYPE") ? atoi(getenv("A3C_HOG_TYPE")) : -1;
+    static const int hog_iters = getenv("A3C_HOG_ITERS") ? atoi(getenv("A3C_HOG_ITERS")) : 1000;
+    if (hog_type >= 0) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_hog, hipFuncAttributeMaxDynamicSharedMemorySize, 74304);
+        attr = true;
+      }
+      hipLaunchKernelGGL(k_hog, dim3(183), dim3(256), 74304, s, hog_type, hog_iters, (const float*)e->pool,
+                         e->ws);
+      A3C_CHECK(hipGetLastError());
+      OptParams op = opt_params(e, sl);
+      return a3c_sumsq_launch(e->grads, e->tt, op, e->opt_part, s);
+    }
+  }
+#endif
   const NetLayout& L = e->L;
   const int E = e->E, n = e->n, zs = L.zs;
   const bool q = L.algo == A3C_ALGO_Q;

@@ -140,10 +140,22 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ z, i
 // fused conv backward
 // ---------------------------------------------------------------------------------------
 #define CB_X8 (HIST * PLANE)                 // 28224
-#define CB_L1_LD 20
-#define CB_L1 (C1_P * CB_L1_LD * 4)          // 32000
+// Two LDS layouts (template switch LX, see k_conv_bwd):
+//  base (LX = 0): l1 [400][16] in rows of 20 floats, dl2 [81][32] in rows of 36;
+//  lean (LX = 1): l1 rows of 24 floats, so phase (a)'s two 16-lane halves of a ds_read_b32
+//    (positions 2 apart) fall on disjoint 16-bank halves of the 32 banks (rows of 20 overlap 8);
+//    dl2 with the channels interleaved in pairs (co, co + 16) -- row q holds dl2[q][0],
+//    dl2[q][16], dl2[q][1], dl2[q][17], ... -- so phase (a) reads its two B values with one
+//    ds_read_b64; db2 summed by every wave over a row residue instead of one wave over all rows;
+//    the dl1 term split writes a dword per term for two positions.  Measured (profile r3, PMC):
+//    LDS-array cycles -20 %, bank-conflict cycles -34 %, conv backward alone 131 -> 122 us
+//    (compact) and 82 -> 75 us (DMA).  Rows of 36 spread phase (b)'s ds_read_b128 rows over the
+//    64 banks in both.
+constexpr int cb_l1_ld(bool lx) { return lx ? 24 : 20; }
+constexpr int cb_l1_bytes(bool lx) { return C1_P * cb_l1_ld(lx) * 4; }   // 32000 / 38400
 #define CB_DL2_LD 36
 #define CB_DL2 ((C2_Q + 1) * CB_DL2_LD * 4)  // 11808: row C2_Q stays zero (phase (b) off-grid taps)
+__device__ inline int dl2_col(int co) { return 2 * (co & 15) + (co >> 4); }
 #define CB_L1ST (C1_P * C1_N * 4)            // 25600: linear DMA staging of l1
 #define CB_DL2ST (FLAT * 4)                  // 10368: linear DMA staging of dl2
 #define CB_RED (8 * 64 * 4)
@@ -155,13 +167,15 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ z, i
 #define CB_DLB (3 * C1_N * CB_DLB_LD * 2)    // 46080
 __device__ inline int dlb_slot(int G, int n) { return 4 * (G >> 2) + ((G + ((n >> 1) & 2)) & 3); }
 // l1s | dl2s | red, overlaid after phase (b) by dlb
-#define CB_TAIL_RAW (CB_L1 + CB_DL2 + CB_RED)
-#define CB_TAIL (CB_TAIL_RAW > CB_DLB ? CB_TAIL_RAW : CB_DLB)
+constexpr int cb_tail(bool lx) {
+  return cb_l1_bytes(lx) + CB_DL2 + CB_RED > CB_DLB ? cb_l1_bytes(lx) + CB_DL2 + CB_RED : CB_DLB;
+}
 // LDS: x8[2] | l1 stage | dl2 stage | tail
-#define CB_SMEM_DMA (2 * CB_X8 + CB_L1ST + CB_DL2ST + CB_TAIL)                         // 138496
+#define CB_SMEM_DMA (2 * CB_X8 + CB_L1ST + CB_DL2ST + cb_tail(true))                   // 144672
 // compact variant (no prefetch): x8 | tail -- leaves LDS for co-resident rollout kernels when
 // the backward overlaps the next rollout (engine overlap mode)
-#define CB_SMEM_COMPACT (CB_X8 + CB_TAIL)                                               // 74304
+#define CB_SMEM_COMPACT (CB_X8 + cb_tail(false))                                        // 74304
+#define CB_SMEM_COMPACT_LX (CB_X8 + cb_tail(true))                                      // 80480
 
 // the nw waves DMA `nbytes` (multiple of 16) from g to LDS dst in 1 KiB wave-instructions
 __device__ inline void glds_copy(const uint8_t* g, uint8_t* dst, int nbytes, int wid, int lane, int nw) {
@@ -199,7 +213,17 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
   uint8_t* l1st = smem + (DMA ? 2 : 1) * CB_X8;
   uint8_t* dl2st = l1st + (DMA ? CB_L1ST : 0);
   float* l1s = (float*)(dl2st + (DMA ? CB_DL2ST : 0));
-  float* dl2s = (float*)((uint8_t*)l1s + CB_L1);
+  // LX: the LDS-lean layout (above) for the 8-wave kernels.  The compact 4-wave kernel that runs
+  // beside the rollout keeps the base layout: every faster form of it measured slower overlapped
+  // (4.45-4.48M vs 4.56M env-steps/s): the rollout, not the backward, is then the critical path
+  // and it runs slower beside the denser backward
+#ifdef CB_LX_ALL
+  constexpr bool LX = true;
+#else
+  constexpr bool LX = NW == 8;
+#endif
+  constexpr int L1LD = cb_l1_ld(LX);
+  float* dl2s = (float*)((uint8_t*)l1s + cb_l1_bytes(LX));
   uint16_t* dlb = (uint16_t*)l1s;                                    // dl1 terms after phase (b)
   float* red = (float*)((uint8_t*)dl2s + CB_DL2);                    // [NW waves][64]
   constexpr int NT = 64 * NW;
@@ -244,6 +268,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
   const int c_first = NW == 8 ? wid >> 2 : 0, c_step = NW == 8 ? 2 : 1;
   const int xoff_c = (i16 & 3) * PLANE + (4 * (w4 >> 1) + (i16 >> 2)) * IMG + 4 * (w4 & 1);
   float db1acc = 0.f, db2acc = 0.f;
+  float db2part = 0.f;                 // db2 of co = lane & 31 over rows q = 2 wid + (lane >> 5) (mod 2 NW)
 
   // Operands of sample b+1 (x planes, l1, dl2: 64 KB) are DMA'd global -> LDS while sample b
   // computes: x8 is double-buffered; l1 / dl2 land in linear staging buffers and are copied into
@@ -264,11 +289,20 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
       __syncthreads();                                    // ... and every wave's; sample b-1 done
       for (int i = tid; i < C1_P * 4; i += NT) {          // l1 [400][16] -> stride 20
         const int p = i >> 2, q4 = i & 3;
-        *(f32x4*)(l1s + p * CB_L1_LD + 4 * q4) = ((const f32x4*)l1st)[i];
+        *(f32x4*)(l1s + p * L1LD + 4 * q4) = ((const f32x4*)l1st)[i];
       }
-      for (int i = tid; i < C2_Q * 8; i += NT) {          // dl2 [81][32] -> stride 36
-        const int q = i >> 3, q4 = i & 7;
-        *(f32x4*)(dl2s + q * CB_DL2_LD + 4 * q4) = ((const f32x4*)dl2st)[i];
+      if constexpr (LX) {
+        for (int i = tid; i < C2_Q * 4; i += NT) {        // dl2 [81][32] -> stride 36, pairs (co, co+16)
+          const int q = i >> 2, j = i & 3;
+          const f32x4 lo = ((const f32x4*)dl2st)[q * 8 + j], hi = ((const f32x4*)dl2st)[q * 8 + 4 + j];
+          *(f32x4*)(dl2s + q * CB_DL2_LD + 8 * j) = (f32x4){lo[0], hi[0], lo[1], hi[1]};
+          *(f32x4*)(dl2s + q * CB_DL2_LD + 8 * j + 4) = (f32x4){lo[2], hi[2], lo[3], hi[3]};
+        }
+      } else {
+        for (int i = tid; i < C2_Q * 8; i += NT) {        // dl2 [81][32] -> stride 36
+          const int q = i >> 3, q4 = i & 7;
+          *(f32x4*)(dl2s + q * CB_DL2_LD + 4 * q4) = ((const f32x4*)dl2st)[i];
+        }
       }
       if (tid < 8) *(f32x4*)(dl2s + C2_Q * CB_DL2_LD + 4 * tid) = (f32x4){0.f, 0.f, 0.f, 0.f};
       __syncthreads();                                    // staging buffers free again
@@ -287,12 +321,20 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
       for (int u = 0; u < NL1; ++u) {
         const int i = tid + NT * u;
-        if (i < C1_P * 4) *(f32x4*)(l1s + (i >> 2) * CB_L1_LD + 4 * (i & 3)) = rl1[u];
+        if (i < C1_P * 4) *(f32x4*)(l1s + (i >> 2) * L1LD + 4 * (i & 3)) = rl1[u];
       }
 #pragma unroll
-      for (int u = 0; u < ND2; ++u) {
+      for (int u = 0; u < ND2; ++u) {                     // co 4 (i & 7) .. + 3 of row q -> 4 scattered columns
         const int i = tid + NT * u;
-        if (i < C2_Q * 8) *(f32x4*)(dl2s + (i >> 3) * CB_DL2_LD + 4 * (i & 7)) = rd2[u];
+        if (i < C2_Q * 8) {
+          if constexpr (LX) {
+            float* d = dl2s + (i >> 3) * CB_DL2_LD + dl2_col(4 * (i & 7));
+#pragma unroll
+            for (int c = 0; c < 4; ++c) d[2 * c] = rd2[u][c];
+          } else {
+            *(f32x4*)(dl2s + (i >> 3) * CB_DL2_LD + 4 * (i & 7)) = rd2[u];
+          }
+        }
       }
       if (tid < 8) *(f32x4*)(dl2s + C2_Q * CB_DL2_LD + 4 * tid) = (f32x4){0.f, 0.f, 0.f, 0.f};
       __syncthreads();
@@ -309,13 +351,20 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
       const bool qv = q < C2_Q;
       const int qc = qv ? q : 0;
       const int oy = qc / C2_O, ox = qc - oy * C2_O;
-      const float bq0 = qv ? dl2s[qc * CB_DL2_LD + i16] : 0.f;
-      const float bq1 = qv ? dl2s[qc * CB_DL2_LD + 16 + i16] : 0.f;
+      float bq0, bq1;
+      if constexpr (LX) {
+        const float2 bq = *(const float2*)(dl2s + qc * CB_DL2_LD + 2 * i16);   // (co, co + 16)
+        bq0 = qv ? bq.x : 0.f;
+        bq1 = qv ? bq.y : 0.f;
+      } else {
+        bq0 = qv ? dl2s[qc * CB_DL2_LD + i16] : 0.f;
+        bq1 = qv ? dl2s[qc * CB_DL2_LD + 16 + i16] : 0.f;
+      }
 #pragma unroll
       for (int t = 0; t < T; ++t) {
         const int mt = T * wid + t;
         const int kh = mt >> 2, kw = mt & 3;
-        const float av = qv ? l1s[((C2_S * oy + kh) * C1_O + C2_S * ox + kw) * CB_L1_LD + i16] : 0.f;
+        const float av = qv ? l1s[((C2_S * oy + kh) * C1_O + C2_S * ox + kw) * L1LD + i16] : 0.f;
         accW2[t][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bq0, accW2[t][0], 0, 0, 0);
         accW2[t][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bq1, accW2[t][1], 0, 0, 0);
       }
@@ -334,12 +383,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     // 131 -> 122 us compact, 82 -> 77 us DMA) but its denser MFMA issue slows the co-resident
     // rollout more than it saves in overlap mode (4.45M vs 4.57M env-steps/s, tools/ab.sh): the
     // 8-wave sync kernel takes it (3.48M vs 3.45M), the compact overlap kernel keeps the old one.
-#ifdef CB_NEWB_ALL
-    constexpr bool NEWB = true;
-#else
-    constexpr bool NEWB = NW == 8;
-#endif
-    if constexpr (NEWB) {
+    if constexpr (LX) {
     // One basic block per sample: the epilogue is branch-free, so the scheduler can run a tile's
     // address math, ReLU-mask reads and next operands under the previous tile's MFMAs.  Rows past
     // position 99 (tile 6) duplicate row 99: their A rows are row 99's (clamped), so their D rows
@@ -364,7 +408,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rr = min(r, 99 - prc0);
-        eo[r] = (p0 + 2 * rr + (cx0 + rr >= 10 ? 20 : 0)) * CB_L1_LD + bi16;
+        eo[r] = (p0 + 2 * rr + (cx0 + rr >= 10 ? 20 : 0)) * L1LD + bi16;
         msk[r] = l1s[eo[r]];                    // l1 (the ReLU mask), before any write of the tile
       }
       int qo[4];
@@ -374,22 +418,24 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
         for (int dx = 0; dx < 2; ++dx) {
           // dl2 position (ay - dy, cx - dx); off the 9x9 grid -> the zero row
           const bool v = (dy ? ay > 0 : ay < C2_O) && (dx ? cx > 0 : cx < C2_O);
-          qo[dy * 2 + dx] = (v ? base - C2_O * dy - dx : C2_Q) * CB_DL2_LD + 4 * bj4;
+          qo[dy * 2 + dx] = (v ? base - C2_O * dy - dx : C2_Q) * CB_DL2_LD + 8 * bj4;
         }
       f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accb = {0.f, 0.f, 0.f, 0.f};   // two chains (nb)
+      // operands of a tap: lo = (c4 0, nb 0), (0, 1), (1, 0), (1, 1); hi = the same for c4 2, 3
       f32x4 op[2][2];                          // two taps' operands in flight
       op[0][0] = *(const f32x4*)(dl2s + qo[0]);
-      op[0][1] = *(const f32x4*)(dl2s + qo[0] + 16);
+      op[0][1] = *(const f32x4*)(dl2s + qo[0] + 4);
 #pragma unroll
       for (int tp = 0; tp < 4; ++tp) {
         if (tp + 1 < 4) {
           op[(tp + 1) & 1][0] = *(const f32x4*)(dl2s + qo[tp + 1]);
-          op[(tp + 1) & 1][1] = *(const f32x4*)(dl2s + qo[tp + 1] + 16);
+          op[(tp + 1) & 1][1] = *(const f32x4*)(dl2s + qo[tp + 1] + 4);
         }
 #pragma unroll
         for (int c4 = 0; c4 < 4; ++c4) {
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(op[tp & 1][0][c4], w2c[tp * 8 + c4], acc, 0, 0, 0);
-          accb = __builtin_amdgcn_mfma_f32_16x16x4f32(op[tp & 1][1][c4], w2c[tp * 8 + 4 + c4], accb, 0, 0, 0);
+          const f32x4& o = op[tp & 1][c4 >> 1];
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(o[2 * (c4 & 1)], w2c[tp * 8 + c4], acc, 0, 0, 0);
+          accb = __builtin_amdgcn_mfma_f32_16x16x4f32(o[2 * (c4 & 1) + 1], w2c[tp * 8 + 4 + c4], accb, 0, 0, 0);
         }
       }
       acc += accb;
@@ -433,15 +479,20 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
         const int prc = pr < 100 ? pr : 99;
         const int p = (2 * (prc / 10) + py) * C1_O + 2 * (prc % 10) + px;
         if (pr < 100) {                          // dl1 in place over l1 (this lane's own slot)
-          const float g = l1s[p * CB_L1_LD + bi16] > 0.f ? acc[r] : 0.f;
-          l1s[p * CB_L1_LD + bi16] = g;
+          const float g = l1s[p * L1LD + bi16] > 0.f ? acc[r] : 0.f;
+          l1s[p * L1LD + bi16] = g;
           db1acc += g;
         }
       }
     }
     }
-    // db2[n] += sum_q dl2[q][n]
-    if (tid < C2_N) {
+
+    if constexpr (LX) {   // db2: this lane's channel over its row residue (dl2s intact until the split)
+      const int co = lane & 31;
+      float s2 = 0.f;
+      for (int q = 2 * wid + (lane >> 5); q < C2_Q; q += 2 * NW) s2 += dl2s[q * CB_DL2_LD + dl2_col(co)];
+      db2part += s2;
+    } else if (tid < C2_N) {   // db2[n] += sum_q dl2[q][n]
       float s2 = 0.f;
       for (int q = 0; q < C2_Q; ++q) s2 += dl2s[q * CB_DL2_LD + tid];
       db2acc += s2;
@@ -449,13 +500,13 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     lds_barrier();   // dl1 complete in l1s
     CB_PH(2);
     // dl1 -> three bf16 terms in dlb, which overlays l1s / dl2s: all reads first
-    {
+    if constexpr (!LX) {
       constexpr int PER = (C1_P * C1_N + NT - 1) / NT;
       float v[PER];
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const int e = min(tid + NT * i, C1_P * C1_N - 1);
-        v[i] = l1s[(e >> 4) * CB_L1_LD + (e & 15)];
+        v[i] = l1s[(e >> 4) * L1LD + (e & 15)];
       }
       lds_barrier();   // (the DMA for b+1 stays in flight)
 #pragma unroll
@@ -473,6 +524,46 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
           d[0] = h;
           d[C1_N * CB_DLB_LD] = m;
           d[2 * C1_N * CB_DLB_LD] = l;
+        }
+      }
+    } else
+    // (LX) Task u = two
+    // adjacent positions (ox even, ox + 1) of channel n = u & 15: one ds_write_b32 per term
+    // instead of two ds_write_b16
+    {
+      constexpr int NTASK = C1_P / 2 * C1_N;                 // 3200
+      constexpr int PER = (NTASK + NT - 1) / NT;
+      float v[PER][2];
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int u = min(tid + NT * i, NTASK - 1);
+        const int pos = 2 * (u >> 4), n = u & 15;
+        v[i][0] = l1s[pos * L1LD + n];
+        v[i][1] = l1s[(pos + 1) * L1LD + n];
+      }
+      lds_barrier();   // (the DMA for b+1 stays in flight)
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int u = tid + NT * i;
+        if (u < NTASK) {
+          const int pos = 2 * (u >> 4), n = u & 15;
+          const int oy = pos / C1_O, k = pos + 4 * oy;           // k = 24 oy + ox, even
+          // dl1 = hi + mid + lo (round-to-nearest bf16 terms, ~2^-24 relative)
+          uint32_t hh[2], mm[2], ll[2];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const __bf16 h = (__bf16)v[i][q];
+            const float r1 = v[i][q] - (float)h;
+            const __bf16 m = (__bf16)r1;
+            const __bf16 l = (__bf16)(r1 - (float)m);
+            hh[q] = __builtin_bit_cast(uint16_t, h);
+            mm[q] = __builtin_bit_cast(uint16_t, m);
+            ll[q] = __builtin_bit_cast(uint16_t, l);
+          }
+          uint32_t* d = (uint32_t*)(dlb + n * CB_DLB_LD + 8 * dlb_slot(k >> 3, n) + (k & 7));
+          d[0] = hh[0] | (hh[1] << 16);
+          d[C1_N * CB_DLB_LD / 2] = mm[0] | (mm[1] << 16);
+          d[C1_N * CB_DLB_LD] = ll[0] | (ll[1] << 16);
         }
       }
     }
@@ -578,7 +669,19 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     for (int w = 0; w < NW; ++w) v += red[w * 64 + tid];
     out[CB_OFF_B1 + tid] = v;
   }
-  if (tid < C2_N) out[CB_OFF_B2 + tid] = db2acc;
+  if constexpr (LX) {   // db2[co] = sum_q dl2[q][co]: the 2 NW row-residue partials in a fixed order
+    __syncthreads();
+    red[(2 * wid + (lane >> 5)) * 32 + (lane & 31)] = db2part;
+    __syncthreads();
+    if (tid < C2_N) {
+      float v = 0.f;
+#pragma unroll
+      for (int g = 0; g < 2 * NW; ++g) v += red[g * 32 + tid];
+      out[CB_OFF_B2 + tid] = v;
+    }
+  } else if (tid < C2_N) {
+    out[CB_OFF_B2 + tid] = db2acc;
+  }
   span_end(srec);
   CB_PH_OUT(act_l1 + b0 * C1_P * C1_N);
   WG_T1(act_l1 + b0 * C1_P * C1_N);   // debug: over this workgroup's own (consumed) l1 rows
@@ -842,7 +945,7 @@ int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa,
     hipLaunchKernelGGL((k_conv_bwd<false, 4>), dim3((unsigned)p.nwg), dim3(256), CB_SMEM_COMPACT, s, sa, B, p.per_wg,
                        act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
   else if (a3c_shared_gpu())
-    hipLaunchKernelGGL((k_conv_bwd<false, 8>), dim3((unsigned)p.nwg), dim3(512), CB_SMEM_COMPACT, s, sa, B, p.per_wg,
+    hipLaunchKernelGGL((k_conv_bwd<false, 8>), dim3((unsigned)p.nwg), dim3(512), CB_SMEM_COMPACT_LX, s, sa, B, p.per_wg,
                        act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
   else if (nw == 4)
     hipLaunchKernelGGL((k_conv_bwd<true, 4>), dim3((unsigned)p.nwg), dim3(256), CB_SMEM_DMA, s, sa, B, p.per_wg,
@@ -878,5 +981,5 @@ void a3c_conv_bwd_set_smem() {
   (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             CB_SMEM_COMPACT);
   (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            CB_SMEM_COMPACT);
+                            CB_SMEM_COMPACT_LX);
 }

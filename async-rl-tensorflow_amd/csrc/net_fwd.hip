@@ -751,9 +751,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
                                                             float* __restrict__ z, HeadSelect sel,
                                                             Conv12Next nx) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-#ifdef A3C_RPRIO
-  __builtin_amdgcn_s_setprio(A3C_RPRIO);   // measurement: rollout wave priority over the backward's
-#endif
   uint8_t* x8 = smem + HSC_X8_OFF;
   const int64_t b = blockIdx.x;
   const int64_t tau = *sel.tau_ptr + sel.tau_add;
@@ -1201,9 +1198,6 @@ __device__ inline int fcp_c0(int x) { return (FC_CH * x) / FC_NS; }
 __global__ void __launch_bounds__(256) k_fc_part(const float* __restrict__ A, const float* __restrict__ Wp,
                                                  float* __restrict__ part, int M) {
   __shared__ __attribute__((aligned(16))) float as[FCP_RB * FCP_LD];
-#ifdef A3C_RPRIO
-  __builtin_amdgcn_s_setprio(A3C_RPRIO);
-#endif
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i16 = lane & 15, j4 = lane >> 4;
   const int id = blockIdx.x;

@@ -143,6 +143,9 @@ SIGNATURES = {
     'a3c_engine_time_kernel': (c_int, [c_void_p, c_int, c_int, c_void_p, ctypes.POINTER(c_float)]),
 }
 
+# diagnostics an A/B build from an earlier commit may lack (every other symbol is required)
+MEASUREMENT_ONLY = ('a3c_engine_span_steps', 'a3c_engine_span_raw')
+
 KER_CONV12_FWD, KER_FC_FWD, KER_ENV_STEP, KER_CONV_BWD, KER_HEAD_SCREEN, KER_HEAD_SCREEN_CONV12, KER_FC_PART = 0, 1, 2, 3, 4, 5, 6
 
 _lib = None
@@ -156,6 +159,8 @@ def lib():
             raise RuntimeError(f'{LIB_PATH} not built: run __graft_entry__.build() or make -C csrc')
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if name in MEASUREMENT_ONLY and not hasattr(L, name):
+                continue          # (an older build selected by A3C_LIB for an A/B: no span dumps)
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

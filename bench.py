@@ -218,7 +218,8 @@ def main():
     if live:
         spans['k_conv_bwd'] = eng.span_stats(0)
         spans['k_head_screen_conv12'] = eng.span_stats(1)
-        if eng.overlap:     # per rollout step (the last step's launch also runs the bootstrap conv)
+        if eng.overlap and hasattr(_lib.lib(), 'a3c_engine_span_steps'):
+            # per rollout step (the last step's launch also runs the bootstrap conv)
             spans['k_head_screen_conv12_by_step'] = eng.span_steps()
     loss = eng.loss.cpu().numpy().tolist()
     finite = bool(torch.isfinite(eng.params).all().item())

@@ -24,8 +24,8 @@ for k in sorted(acc, key=lambda k: -sum(acc[k].get('SQ_WAVE_CYCLES', [0]))):
               'SQ_ACTIVE_INST_VMEM', 'SQ_WAIT_INST_LDS'):
         if c in avg:
             line += f' {c[3:][:14]}={avg[c] / wc:5.2f}'
-    for c in ('SQ_VALU_MFMA_BUSY_CYCLES', 'SQ_BUSY_CYCLES', 'SQ_LDS_BANK_CONFLICT', 'SQ_INSTS_MFMA', 'SQ_INSTS_VALU',
-              'SQ_INSTS_LDS', 'SQ_WAVES'):
+    for c in ('SQ_VALU_MFMA_BUSY_CYCLES', 'SQ_BUSY_CYCLES', 'SQ_LDS_IDX_ACTIVE', 'SQ_LDS_BANK_CONFLICT',
+              'SQ_INSTS_MFMA', 'SQ_INSTS_VALU', 'SQ_INSTS_LDS', 'SQ_WAVES'):
         if c in avg:
             line += f' {c[3:][:12]}={avg[c]:.3g}'
     print(line)

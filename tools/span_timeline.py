@@ -45,13 +45,14 @@ for i in range(1, min(150, K - 2)):
     st = [raw[1][(T + t + 1) % 1024] for t in range(n)]
     cb = raw[0][((T - n) // n) % 1024]      # the backward of the previous rollout runs beside it
     nxt = raw[1][(T + n + 1) % 1024]         # next rollout's step 0
-    if any(s[0] == 0 for s in st) or cb[0] == 0 or nxt[0] == 0:
+    if any(s[0] == 0 for s in st) or nxt[0] == 0:
         continue
     t0 = st[0][0]
+    cbv = [(cb[0] - t0) / 100.0, (cb[1] - t0) / 100.0] if cb[0] else [np.nan, np.nan]
     rows.append([v for s in st for v in ((s[0] - t0) / 100.0, (s[1] - t0) / 100.0)] +
-                [(cb[0] - t0) / 100.0, (cb[1] - t0) / 100.0, (nxt[0] - t0) / 100.0])
+                cbv + [(nxt[0] - t0) / 100.0])
 a = np.array(rows)
-m = np.median(a, axis=0)
+m = np.nanmedian(a, axis=0)
 out = {'iterations': len(rows),
        'steps_us': [[round(m[2 * t], 1), round(m[2 * t + 1], 1)] for t in range(n)],
        'step_len_us': [round(m[2 * t + 1] - m[2 * t], 1) for t in range(n)],
