@@ -689,9 +689,11 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s);
 static int enqueue_grad(a3c_engine* e, const Slot& sl, hipStream_t s) {
   // overlap: the backward shares CUs with the next rollout -> small-footprint kernel variants
   a3c_set_shared_gpu(e->overlap != 0);
+  a3c_set_lean_cbwd(e->overlap && e->frame84);   // M2: the backward bounds the iteration
   mark(2, s);
   int rc = enqueue_grad_impl(e, sl, s);
   a3c_set_shared_gpu(false);
+  a3c_set_lean_cbwd(false);
   return rc;
 }
 
@@ -1411,7 +1413,8 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
   const Slot& sl = e->slot[0];
   if (e->rs) A3C_CHECK(hipStreamSynchronize(e->rs));
   a3c_set_shared_gpu(e->overlap != 0);      // time the variants the engine runs
-  struct ResetShared { ~ResetShared() { a3c_set_shared_gpu(false); } } reset_shared;
+  a3c_set_lean_cbwd(e->overlap && e->frame84);
+  struct ResetShared { ~ResetShared() { a3c_set_shared_gpu(false); a3c_set_lean_cbwd(false); } } reset_shared;
   if (kernel == A3C_KER_CONV12_FWD || kernel == A3C_KER_FC_FWD || kernel == A3C_KER_HEAD_SCREEN_CONV12) {
     int rc0 = a3c_prep_fwd_launch(L, e->params, sl.prep, s);
     if (rc0) return rc0;

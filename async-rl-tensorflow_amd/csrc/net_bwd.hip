@@ -202,7 +202,7 @@ __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_b
 #define CB_PH_OUT(dst) ((void)0)
 #endif
 
-template <bool DMA, int NW>
+template <bool DMA, int NW, bool LX>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) k_conv_bwd(StateAddr sa, int64_t B, int per_wg,
                                                   const float* __restrict__ act_l1,
                                                   const float* __restrict__ dl2,
@@ -213,15 +213,11 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
   uint8_t* l1st = smem + (DMA ? 2 : 1) * CB_X8;
   uint8_t* dl2st = l1st + (DMA ? CB_L1ST : 0);
   float* l1s = (float*)(dl2st + (DMA ? CB_DL2ST : 0));
-  // LX: the LDS-lean layout (above) for the 8-wave kernels.  The compact 4-wave kernel that runs
-  // beside the rollout keeps the base layout: every faster form of it measured slower overlapped
-  // (4.45-4.48M vs 4.56M env-steps/s): the rollout, not the backward, is then the critical path
-  // and it runs slower beside the denser backward
-#ifdef CB_LX_ALL
-  constexpr bool LX = true;
-#else
-  constexpr bool LX = NW == 8;
-#endif
+  // LX: the LDS-lean layout (above).  The 8-wave kernels always take it; the compact 4-wave kernel
+  // that runs beside the rollout only where the backward is the critical path (a3c_lean_cbwd):
+  // in mode M1 every faster form of it measured slower overlapped (4.45-4.48M vs 4.56M
+  // env-steps/s), the rollout then being the critical path and slower beside the denser
+  // backward; in mode M2 (pre-sized frames, a shorter rollout) it gains 4.56M -> 4.75-4.82M
   constexpr int L1LD = cb_l1_ld(LX);
   float* dl2s = (float*)((uint8_t*)l1s + cb_l1_bytes(LX));
   uint16_t* dlb = (uint16_t*)l1s;                                    // dl1 terms after phase (b)
@@ -929,6 +925,14 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
 static thread_local bool t_shared_gpu = false;
 bool a3c_shared_gpu() { return t_shared_gpu; }
 void a3c_set_shared_gpu(bool v) { t_shared_gpu = v; }
+// the compact conv backward's LDS-lean form (set by the engine where the backward, not the
+// rollout, bounds the overlapped iteration: mode M2); A3C_CB_LEAN=0/1 overrides
+static thread_local bool t_lean_cbwd = false;
+bool a3c_lean_cbwd() {
+  static const int env = getenv("A3C_CB_LEAN") ? atoi(getenv("A3C_CB_LEAN")) : -1;
+  return env >= 0 ? env != 0 : t_lean_cbwd;
+}
+void a3c_set_lean_cbwd(bool v) { t_lean_cbwd = v; }
 
 int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,
                         const float* dl2, float* ws, hipStream_t s) {
@@ -941,18 +945,21 @@ int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa,
   // 4-wave kernel leaves registers and LDS for the concurrent rollout (measured, tools/ab.sh)
   static const int env_nw = getenv("A3C_CB_WAVES") ? atoi(getenv("A3C_CB_WAVES")) : 0;
   const int nw = env_nw ? env_nw : (a3c_shared_gpu() ? 4 : 8);
-  if (a3c_shared_gpu() && nw == 4)
-    hipLaunchKernelGGL((k_conv_bwd<false, 4>), dim3((unsigned)p.nwg), dim3(256), CB_SMEM_COMPACT, s, sa, B, p.per_wg,
-                       act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
+  if (a3c_shared_gpu() && nw == 4 && a3c_lean_cbwd())
+    hipLaunchKernelGGL((k_conv_bwd<false, 4, true>), dim3((unsigned)p.nwg), dim3(256), CB_SMEM_COMPACT_LX, s, sa, B,
+                       p.per_wg, act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
+  else if (a3c_shared_gpu() && nw == 4)
+    hipLaunchKernelGGL((k_conv_bwd<false, 4, false>), dim3((unsigned)p.nwg), dim3(256), CB_SMEM_COMPACT, s, sa, B,
+                       p.per_wg, act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
   else if (a3c_shared_gpu())
-    hipLaunchKernelGGL((k_conv_bwd<false, 8>), dim3((unsigned)p.nwg), dim3(512), CB_SMEM_COMPACT_LX, s, sa, B, p.per_wg,
-                       act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
+    hipLaunchKernelGGL((k_conv_bwd<false, 8, true>), dim3((unsigned)p.nwg), dim3(512), CB_SMEM_COMPACT_LX, s, sa, B,
+                       p.per_wg, act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
   else if (nw == 4)
-    hipLaunchKernelGGL((k_conv_bwd<true, 4>), dim3((unsigned)p.nwg), dim3(256), CB_SMEM_DMA, s, sa, B, p.per_wg,
+    hipLaunchKernelGGL((k_conv_bwd<true, 4, false>), dim3((unsigned)p.nwg), dim3(256), CB_SMEM_DMA, s, sa, B, p.per_wg,
                        act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
   else
-  hipLaunchKernelGGL((k_conv_bwd<true, 8>), dim3((unsigned)p.nwg), dim3(512), CB_SMEM_DMA, s, sa, B, p.per_wg, act_l1,
-                     dl2, P + L.off[T_L2W], ws + p.cslab);
+    hipLaunchKernelGGL((k_conv_bwd<true, 8, true>), dim3((unsigned)p.nwg), dim3(512), CB_SMEM_DMA, s, sa, B, p.per_wg,
+                       act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
@@ -976,10 +983,10 @@ int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float
 }
 
 void a3c_conv_bwd_set_smem() {
-  (void)hipFuncSetAttribute((const void*)k_conv_bwd<true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_SMEM_DMA);
-  (void)hipFuncSetAttribute((const void*)k_conv_bwd<true, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, CB_SMEM_DMA);
-  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            CB_SMEM_COMPACT);
-  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            CB_SMEM_COMPACT_LX);
+  const int a = hipFuncAttributeMaxDynamicSharedMemorySize;
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<true, 4, false>, (hipFuncAttribute)a, CB_SMEM_DMA);
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<true, 8, true>, (hipFuncAttribute)a, CB_SMEM_DMA);
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 4, false>, (hipFuncAttribute)a, CB_SMEM_COMPACT);
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 4, true>, (hipFuncAttribute)a, CB_SMEM_COMPACT_LX);
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 8, true>, (hipFuncAttribute)a, CB_SMEM_COMPACT_LX);
 }
