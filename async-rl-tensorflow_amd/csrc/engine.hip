@@ -85,6 +85,7 @@ struct a3c_engine {
   double* stats;           // [A3C_STATS_N] train_with_summary aggregates since the last read
   double* ep_acc;          // [E] running episode reward per env (agent.py:91-98)
   TensorTab tt;
+  TensorTab tt_f;             // partial layout of the norms the backward's finalize produces (a3c_fused_tab)
   // sync: one graph (rollout + grad); overlap: rollout and grad graphs per slot
   hipGraph_t graph[NGRAPH];
   hipGraphExec_t gexec[NGRAPH];
@@ -302,7 +303,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   ALLOC(e->stats, A3C_STATS_N * 8);
   ALLOC(e->ep_acc, E * 8);
 #undef ALLOC
-  if (a3c_make_tab(L.nt, L.off, L.size, L.total, &e->tt)) {
+  if (a3c_make_tab(L.nt, L.off, L.size, L.total, &e->tt) || a3c_fused_tab(L, &e->tt_f)) {
     a3c_engine_destroy(e);
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "tensor table");
   }
@@ -336,6 +337,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     // graphs, a combination the pool has not run on several GPUs -- events there)
     e->wait_value = e->cfg.world_size == 1;
     if (const char* v = getenv("A3C_WAIT_VALUE")) e->wait_value = atoi(v) != 0;
+
     if (!ok) {
       a3c_engine_destroy(e);
       return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "stream/event creation failed");
@@ -686,10 +688,20 @@ static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
 // returns / TD target, loss + backward over the slot's n*E samples, per-tensor norms (+ the
 // per-worker clip when gradients are exchanged across GPUs).
 static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s);
+// Overlapped runs where the backward stream, not the rollout, bounds the iteration: mode M2 (a
+// shorter rollout) and several GPUs (the exchange -- all-to-all, sharded apply, all-gather -- runs on
+// the backward's stream).  There the compact conv backward takes its LDS-lean form (M2: 4.56M ->
+// 4.66-4.76M env-steps/s) and the backward starts right behind the rollout it consumes
+// (rollout_grad); in mode M1 the rollout bounds it and both choices cost the rollout more than
+// they save the backward.
+static bool bwd_bound(const a3c_engine* e) {
+  return e->overlap && (e->frame84 || e->cfg.world_size > 1);
+}
+static bool lean_cbwd(const a3c_engine* e) { return bwd_bound(e); }
 static int enqueue_grad(a3c_engine* e, const Slot& sl, hipStream_t s) {
   // overlap: the backward shares CUs with the next rollout -> small-footprint kernel variants
   a3c_set_shared_gpu(e->overlap != 0);
-  a3c_set_lean_cbwd(e->overlap && e->frame84);   // M2: the backward bounds the iteration
+  a3c_set_lean_cbwd(lean_cbwd(e));
   mark(2, s);
   int rc = enqueue_grad_impl(e, sl, s);
   a3c_set_shared_gpu(false);
@@ -787,7 +799,7 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
                          e->ws);
       A3C_CHECK(hipGetLastError());
       OptParams op = opt_params(e, sl);
-      return a3c_sumsq_launch(e->grads, e->tt, op, e->opt_part, s);
+      return a3c_sumsq_launch(e->grads, e->tt_f, op, e->opt_part, s);   // (F tensors read as 0: measurement only)
     }
   }
 #endif
@@ -824,19 +836,19 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
   StateAddr bsa = ring_addr(e, 0, sl.tau);
   bsa.span = spans_on() ? e->spans : nullptr;   // one record per backward (tau advances by n)
   bsa.span_div = n;
+  // the per-tensor squared norms (+ lr / target-sync schedule from the device step counter) come
+  // out of the backward's last kernel (k_finalize): no separate k_sumsq launch (round 3)
+  OptParams op = opt_params(e, sl);
+  const SumsqFused sf = {e->opt_part, &e->tt_f, &op};
   rc = a3c_backward_launch(L, sl.P, bsa, e->nE, sl.act_l1, sl.act_l2, sl.act_l3, sl.z,
                            sl.actions, sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra,
                            fork ? e->gs : nullptr, fork ? e->ev_gfork : nullptr, fork ? e->ev_gjoin : nullptr,
-                           L.lstm ? &lb : nullptr);
-  if (rc) return rc;
-  // per-tensor squared norms (+ lr / target-sync schedule from the device step counter)
-  OptParams op = opt_params(e, sl);
-  rc = a3c_sumsq_launch(e->grads, e->tt, op, e->opt_part, s);
+                           L.lstm ? &lb : nullptr, &sf);
   if (rc) return rc;
   if (c.world_size > 1) {
     // multi-GPU: clip this worker's gradient (agent.py:319) before the cross-GPU exchange
     op.mode = OPT_CLIP;
-    return a3c_apply_launch(nullptr, nullptr, nullptr, e->grads, e->tt, op, e->opt_part, e->sumsq, s);
+    return a3c_apply_launch(nullptr, nullptr, nullptr, e->grads, e->tt_f, op, e->opt_part, e->sumsq, s);
   }
   return 0;
 }
@@ -850,11 +862,11 @@ static int enqueue_rollout_grad(a3c_engine* e, hipStream_t s) {
 // advance in one launch; world_size == 1: the per-tensor clip as well.  Overlap: then the
 // parameter snapshot of the rollout that will use slot `snap` (the slot just back-propagated).
 static int enqueue_apply(a3c_engine* e, int snap, hipStream_t s) {
-  OptParams op = opt_params(e, e->slot[snap]);    // (the schedule was evaluated by k_sumsq)
+  OptParams op = opt_params(e, e->slot[snap]);    // (the schedule was evaluated by the backward)
   op.mode = e->cfg.world_size > 1 ? OPT_APPLY : (OPT_CLIP | OPT_APPLY);
   // overlap: the same pass writes the parameter snapshot of the rollout that will use slot `snap`
   if (e->overlap) op.snap = e->slot[snap].P;
-  int rc = a3c_apply_launch(e->params, e->ms, e->mom, e->grads, e->tt, op, e->opt_part,
+  int rc = a3c_apply_launch(e->params, e->ms, e->mom, e->grads, e->tt_f, op, e->opt_part,
                             e->cfg.world_size > 1 ? nullptr : e->sumsq, s);
   mark(3, s);
   return rc;
@@ -983,14 +995,27 @@ static int rollout_grad(a3c_engine* e, hipStream_t s, bool fused) {
     A3C_CHECK(hipEventRecord(e->ev_start, s));
     A3C_CHECK(hipStreamWaitEvent(e->rs, e->ev_start, 0));
   }
-  int rc = run_graph(e, 1 + p, 1, p, e->rs);   // (its prep kernel snapshots tau into sl.tau)
+  // "rollout k done" (the backward's go): signalled right behind rollout k when the backward bounds
+  // the iteration; otherwise behind the wait for the apply rollout k+1 needs, so that the backward
+  // of k starts with rollout k+1 instead of ~10 us ahead of it, where its GEMMs slow rollout k+1's
+  // first steps (M1 4.42-4.53M -> 4.56-4.57M, M2 4.75-4.82M -> 4.50M if used there).
+  // Either way rollout k is complete in rs order.
+  const bool late_go = !bwd_bound(e);
+  auto signal_rollout = [&](int q) -> int {
+    if (e->wait_value) {
+      A3C_CHECK(hipStreamWriteValue32(e->rs, e->xflags + 1, ++e->r_seq, 0));
+      e->roll_seq[q] = e->r_seq;
+    } else {
+      A3C_CHECK(hipEventRecord(e->ev_roll[q], e->rs));
+    }
+    return 0;
+  };
+  int rc = late_go && e->iter >= 1 ? signal_rollout(p ^ 1) : 0;
   if (rc) return rc;
-  if (e->wait_value) {
-    A3C_CHECK(hipStreamWriteValue32(e->rs, e->xflags + 1, ++e->r_seq, 0));
-    e->roll_seq[p] = e->r_seq;
-  } else {
-    A3C_CHECK(hipEventRecord(e->ev_roll[p], e->rs));
-  }
+  rc = run_graph(e, 1 + p, 1, p, e->rs);   // (its prep kernel snapshots tau into sl.tau)
+  if (rc) return rc;
+  rc = late_go ? 0 : signal_rollout(p);
+  if (rc) return rc;
   e->grad_ready = false;
 #ifdef A3C_MARKERS
   static const bool abl_bwd = getenv("A3C_ABL_BWD") != nullptr;   // measurement only: rollouts alone
@@ -1413,7 +1438,7 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
   const Slot& sl = e->slot[0];
   if (e->rs) A3C_CHECK(hipStreamSynchronize(e->rs));
   a3c_set_shared_gpu(e->overlap != 0);      // time the variants the engine runs
-  a3c_set_lean_cbwd(e->overlap && e->frame84);
+  a3c_set_lean_cbwd(lean_cbwd(e));
   struct ResetShared { ~ResetShared() { a3c_set_shared_gpu(false); a3c_set_lean_cbwd(false); } } reset_shared;
   if (kernel == A3C_KER_CONV12_FWD || kernel == A3C_KER_FC_FWD || kernel == A3C_KER_HEAD_SCREEN_CONV12) {
     int rc0 = a3c_prep_fwd_launch(L, e->params, sl.prep, s);

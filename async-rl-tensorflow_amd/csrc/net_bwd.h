@@ -1,6 +1,7 @@
 #pragma once
 #include "net.h"
 #include "lstm.h"
+#include "optim.h"
 
 // per-workgroup partial slab of k_conv_bwd: dW1 [256][16] (unscaled by 1/255), dW2 [256][32],
 // db1 [16], db2 [32]
@@ -17,12 +18,33 @@ struct FinalizeSeg {
   int64_t dst_off;        // dst[dst_off + r*dst_ld + c] = scale * sum_s
   int dst_ld;
   float scale;
+  int slot;               // >= 0: block x of the segment writes its fp64 sum of squares to part[slot + x]
 };
+#define FIN_X 32          // k_finalize blocks per segment
 struct FinalizeSegs {
   FinalizeSeg s[12];
   int n;
   float* dst;
+  // fused per-tensor norms (engine): the segments' partials as above, then one block per
+  // SS_CHUNK of the tensors the segments do not write (already final: fc weights, LSTM) and the
+  // lr / target-sync schedule -- what k_sumsq would compute, without its launch
+  double* part;           // nullptr: none of this
+  TensorTab tt;           // partial layout (a3c_fused_tab)
+  int nsum;               // tensors summed by chunk blocks
+  int sum_t[4];           // their indices
+  int sum_c0[5];          // prefix sums of their chunk counts
+  OptParams op;
 };
+
+// engine form of the per-tensor norms: k_finalize produces the partials (layout tt) and the schedule
+struct SumsqFused {
+  double* part;
+  const TensorTab* tt;
+  const OptParams* op;
+};
+// the partial layout SumsqFused expects: FIN_X slots for each tensor a finalize segment writes,
+// SS_CHUNK chunks for the others
+int a3c_fused_tab(const NetLayout& L, TensorTab* tt);
 
 struct BwdPlan {
   int nwg, per_wg, head_split, fc_split, groups;
@@ -58,7 +80,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
                         int literal, float* grads, float* loss_out, float* ws, hipStream_t s,
                         const ReturnsArgs* ra = nullptr,
                         hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr,
-                        const LstmBwd* lb = nullptr);
+                        const LstmBwd* lb = nullptr, const SumsqFused* sf = nullptr);
 int a3c_returns_launch(const float* rewards, const uint8_t* terms, const float* boot, int64_t boot_stride,
                        int n, int64_t E, double gamma, float* R, hipStream_t s);
 int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float* qn, int64_t B, int A,

@@ -714,20 +714,70 @@ __device__ void loss_reduce_block(const float* __restrict__ terms, int64_t B, fl
   if (threadIdx.x < 4) out[threadIdx.x] = (float)red[threadIdx.x][0];
 }
 
-// pass 2 + small segments; block row fs.n (x == 0) reduces the per-sample loss terms
+// pass 2 + small segments: blocks [0, FIN_X n) = segment y = b / FIN_X, x = b % FIN_X (grid-stride
+// within the segment; with fs.part, the block's fp64 sum of squares of what it wrote goes to
+// part[slot + x]); block FIN_X n reduces the per-sample loss terms (and evaluates the schedule);
+// the blocks after it sum the other tensors' chunks (fused per-tensor norms, FinalizeSegs)
 __global__ void __launch_bounds__(256) k_finalize(FinalizeSegs fs, const float* __restrict__ terms, int64_t B,
                                                   float* __restrict__ loss_out) {
-  if ((int)blockIdx.y == fs.n) {
-    if (blockIdx.x == 0 && loss_out) loss_reduce_block(terms, B, loss_out);
+  const int b = blockIdx.x;
+  if (b < FIN_X * fs.n) {
+    const int y = b / FIN_X, x = b - y * FIN_X;
+    const FinalizeSeg sg = fs.s[y];
+    const int64_t n = (int64_t)sg.rows * sg.ncols;
+    double ss = 0.0;
+    for (int64_t i = (int64_t)x * 256 + threadIdx.x; i < n; i += (int64_t)FIN_X * 256) {
+      const int r = (int)(i / sg.ncols), c = (int)(i - (int64_t)r * sg.ncols);
+      const float* src = sg.src + (int64_t)r * sg.src_ld + sg.col0 + c;
+      const float v = sum_strided(src, sg.nsplit, sg.split_stride) * sg.scale;
+      fs.dst[sg.dst_off + (int64_t)r * sg.dst_ld + c] = v;
+      ss += (double)v * v;
+    }
+    if (fs.part && sg.slot >= 0) {
+      __shared__ double red[256];
+      red[threadIdx.x] = ss;
+      __syncthreads();
+      for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) fs.part[sg.slot + x] = red[0];
+    }
     return;
   }
-  const FinalizeSeg sg = fs.s[blockIdx.y];
-  const int64_t n = (int64_t)sg.rows * sg.ncols;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int r = (int)(i / sg.ncols), c = (int)(i - (int64_t)r * sg.ncols);
-    const float* src = sg.src + (int64_t)r * sg.src_ld + sg.col0 + c;
-    fs.dst[sg.dst_off + (int64_t)r * sg.dst_ld + c] = sum_strided(src, sg.nsplit, sg.split_stride) * sg.scale;
+  if (b == FIN_X * fs.n) {
+    if (loss_out) loss_reduce_block(terms, B, loss_out);
+    if (fs.part && threadIdx.x == 0) opt_schedule(fs.op);
+    return;
   }
+  const int k = b - FIN_X * fs.n - 1;
+  int j = 0;
+  while (j + 1 < fs.nsum && k >= fs.sum_c0[j + 1]) ++j;
+  const int t = fs.sum_t[j], c = k - fs.sum_c0[j];
+  sumsq_chunk(fs.dst, fs.tt, t, c, fs.part, fs.tt.pb_first[t] + c);
+}
+
+// tensors whose gradient a k_finalize segment writes (a3c_backward_launch's seg() calls)
+static bool finalize_tensor(const NetLayout& L, int t) {
+  return t == T_L1W || t == T_L1B || t == T_L2W || t == T_L2B || t == T_FCB || t == T_HW || t == T_HB ||
+         (L.algo == A3C_ALGO_A3C && (t == T_VW || t == T_VB));
+}
+
+int a3c_fused_tab(const NetLayout& L, TensorTab* tt) {
+  if (L.nt <= 0 || L.nt > A3C_MAX_TENSORS) return -1;
+  tt->n = L.nt;
+  int nb = 0;
+  for (int t = 0; t < L.nt; ++t) {
+    tt->off[t] = L.off[t];
+    tt->size[t] = L.size[t];
+    tt->pb_first[t] = nb;
+    tt->pb_count[t] = finalize_tensor(L, t) ? FIN_X : (int)((L.size[t] + SS_CHUNK - 1) / SS_CHUNK);
+    nb += tt->pb_count[t];
+  }
+  if (nb > SS_MAX_BLOCKS) return -1;
+  tt->nblocks = nb;
+  tt->total = L.total;
+  return 0;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -779,7 +829,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
                         const float* z, const int32_t* actions, const float* target, float beta,
                         int literal, float* grads, float* loss_out, float* ws, hipStream_t s,
                         const ReturnsArgs* ra_in, hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join,
-                        const LstmBwd* lb) {
+                        const LstmBwd* lb, const SumsqFused* sf) {
   ReturnsArgs ra = {};
   if (ra_in) ra = *ra_in;
   if (B <= 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "B must be > 0");
@@ -890,10 +940,11 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   FinalizeSegs fs = {};
   fs.dst = grads;
   auto seg = [&](const float* src, int64_t stride, int nsplit, int rows, int src_ld, int col0,
-                 int ncols, int64_t dst_off, int dst_ld, float scale) {
+                 int ncols, int tensor, int dst_ld, float scale) {
     FinalizeSeg& q = fs.s[fs.n++];
     q.src = src; q.split_stride = stride; q.nsplit = nsplit; q.rows = rows; q.src_ld = src_ld;
-    q.col0 = col0; q.ncols = ncols; q.dst_off = dst_off; q.dst_ld = dst_ld; q.scale = scale;
+    q.col0 = col0; q.ncols = ncols; q.dst_off = L.off[tensor]; q.dst_ld = dst_ld; q.scale = scale;
+    q.slot = sf ? sf->tt->pb_first[tensor] : -1;
   };
   if (fork) A3C_CHECK(hipStreamWaitEvent(s, ev_join, 0));
   // conv slabs: nwg partials -> p.groups partials (pass 1), folded by k_finalize (pass 2)
@@ -902,18 +953,34 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
                      (int64_t)CB_SLAB, ws + p.cgroup);
   A3C_CHECK(hipGetLastError());
   const float* cs = ws + p.cgroup;
-  seg(cs + CB_OFF_W1, CB_SLAB, p.groups, 1, 0, 0, KC1 * C1_N, L.off[T_L1W], 0, 1.0f / 255.0f);
-  seg(cs + CB_OFF_B1, CB_SLAB, p.groups, 1, 0, 0, C1_N, L.off[T_L1B], 0, 1.0f);
-  seg(cs + CB_OFF_W2, CB_SLAB, p.groups, 1, 0, 0, KC2 * C2_N, L.off[T_L2W], 0, 1.0f);
-  seg(cs + CB_OFF_B2, CB_SLAB, p.groups, 1, 0, 0, C2_N, L.off[T_L2B], 0, 1.0f);
-  seg(ws + p.fccol, FC, p.fc_split, 1, 0, 0, FC, L.off[T_FCB], 0, 1.0f);
-  seg(ws + p.hgrad, 0, 1, FC, L.zs, 0, L.A, L.off[T_HW], L.A, 1.0f);
-  seg(ws + p.hcol, L.zs, p.head_split, 1, 0, 0, L.A, L.off[T_HB], 0, 1.0f);
+  seg(cs + CB_OFF_W1, CB_SLAB, p.groups, 1, 0, 0, KC1 * C1_N, T_L1W, 0, 1.0f / 255.0f);
+  seg(cs + CB_OFF_B1, CB_SLAB, p.groups, 1, 0, 0, C1_N, T_L1B, 0, 1.0f);
+  seg(cs + CB_OFF_W2, CB_SLAB, p.groups, 1, 0, 0, KC2 * C2_N, T_L2W, 0, 1.0f);
+  seg(cs + CB_OFF_B2, CB_SLAB, p.groups, 1, 0, 0, C2_N, T_L2B, 0, 1.0f);
+  seg(ws + p.fccol, FC, p.fc_split, 1, 0, 0, FC, T_FCB, 0, 1.0f);
+  seg(ws + p.hgrad, 0, 1, FC, L.zs, 0, L.A, T_HW, L.A, 1.0f);
+  seg(ws + p.hcol, L.zs, p.head_split, 1, 0, 0, L.A, T_HB, 0, 1.0f);
   if (a3c) {
-    seg(ws + p.hgrad, 0, 1, FC, L.zs, L.A, 1, L.off[T_VW], 1, 1.0f);
-    seg(ws + p.hcol, L.zs, p.head_split, 1, 0, L.A, 1, L.off[T_VB], 0, 1.0f);
+    seg(ws + p.hgrad, 0, 1, FC, L.zs, L.A, 1, T_VW, 1, 1.0f);
+    seg(ws + p.hcol, L.zs, p.head_split, 1, 0, L.A, 1, T_VB, 0, 1.0f);
   }
-  hipLaunchKernelGGL(k_finalize, dim3(32, fs.n + 1), dim3(256), 0, s, fs, terms, B, loss_out);
+  int nsumblk = 0;
+  if (sf) {   // every other tensor is final by now (fc weights: reduced above; LSTM: BPTT)
+    fs.part = sf->part;
+    fs.tt = *sf->tt;
+    fs.op = *sf->op;
+    fs.sum_c0[0] = 0;
+    for (int t = 0; t < L.nt; ++t) {
+      if (finalize_tensor(L, t)) continue;
+      if (fs.nsum == 4) return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "fused norms: too many tensors");
+      fs.sum_t[fs.nsum] = t;
+      fs.sum_c0[fs.nsum + 1] = fs.sum_c0[fs.nsum] + fs.tt.pb_count[t];
+      ++fs.nsum;
+    }
+    nsumblk = fs.sum_c0[fs.nsum];
+  }
+  hipLaunchKernelGGL(k_finalize, dim3((unsigned)(FIN_X * fs.n + 1 + nsumblk)), dim3(256), 0, s, fs, terms, B,
+                     loss_out);
   A3C_CHECK(hipGetLastError());
   return 0;
 }

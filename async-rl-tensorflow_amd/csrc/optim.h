@@ -45,6 +45,47 @@ struct OptParams {
 };
 
 int a3c_make_tab(int n, const int64_t* off, const int64_t* size, int64_t total, TensorTab* tt);
+
+// the lr schedule and target-sync decision from the device step counter (one thread; k_sumsq's
+// block 0, or the backward's finalize when it produces the partials itself)
+__device__ inline void opt_schedule(const OptParams& op) {
+  if (!op.sched || !op.step_ptr) return;
+  const int64_t g0 = *op.step_ptr;
+  const double step = op.wstep_ptr ? (double)(*op.wstep_ptr + (*op.tau_ptr - op.tau0) + op.n_step - 1)
+                                   : (double)(g0 + op.step_add);
+  // agent.py:393-395; the reference never trains past max_step (agent.py:46,55-57), so the
+  // schedule is clamped at 0 there instead of turning negative (RMSProp would ascend)
+  const double lr = (double)(op.max_step - step + 1.0) / (double)op.max_step * op.lr0;
+  op.sched[0] = (float)(lr > 0.0 ? lr : 0.0);
+  int copy = 0;
+  if (op.target_period > 0) copy = (g0 + op.step_add + 1) / op.target_period != (g0 + 1) / op.target_period;
+  op.sched[1] = copy ? 1.0f : 0.0f;
+}
+
+// fp64 sum of squares of chunk c (SS_CHUNK elements) of tensor t, by one 256-thread block into
+// part[slot]: float4 body + scalar tail, then a fixed-order tree
+__device__ inline void sumsq_chunk(const float* __restrict__ g, const TensorTab& tt, int t, int64_t c,
+                                   double* __restrict__ part, int slot) {
+  __shared__ double red[256];
+  const int64_t beg = c * SS_CHUNK;
+  const int64_t end = min(tt.size[t], beg + (int64_t)SS_CHUNK);
+  const float* p = g + tt.off[t];
+  double s = 0.0;
+  // tensor offsets are 4-aligned, chunk starts are 4096-aligned
+  const int64_t end4 = beg + ((end - beg) & ~(int64_t)3);
+  for (int64_t j = beg + 4 * threadIdx.x; j < end4; j += 4 * 256) {
+    f32x4 v = *(const f32x4*)(p + j);
+    s += (double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3];
+  }
+  for (int64_t j = end4 + threadIdx.x; j < end; j += 256) s += (double)p[j] * p[j];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[slot] = red[0];
+}
 int a3c_sumsq_launch(const float* grads, const TensorTab& tt, const OptParams& op, double* part, hipStream_t s);
 int a3c_apply_launch(float* w, float* ms, float* mom, float* grads, const TensorTab& tt, const OptParams& op,
                      const double* part, float* sumsq_out, hipStream_t s);
