@@ -691,21 +691,20 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s);
 // Overlapped runs where the backward stream, not the rollout, bounds the iteration: mode M2 (a
 // shorter rollout) and several GPUs (the exchange -- all-to-all, sharded apply, all-gather -- runs on
 // the backward's stream).  There the compact conv backward takes its LDS-lean form (M2: 4.56M ->
-// 4.66-4.76M env-steps/s) and the backward starts right behind the rollout it consumes
-// (rollout_grad); in mode M1 the rollout bounds it and both choices cost the rollout more than
-// they save the backward.
+// 4.66-4.76M env-steps/s), the fc GEMMs their XCD-grouped tile order (4.77-4.83M -> 4.87-4.88M)
+// and the backward starts right behind the rollout it consumes (rollout_grad); in mode M1 the
+// rollout bounds it and each of these costs the rollout more than it saves the backward.
 static bool bwd_bound(const a3c_engine* e) {
   return e->overlap && (e->frame84 || e->cfg.world_size > 1);
 }
-static bool lean_cbwd(const a3c_engine* e) { return bwd_bound(e); }
 static int enqueue_grad(a3c_engine* e, const Slot& sl, hipStream_t s) {
   // overlap: the backward shares CUs with the next rollout -> small-footprint kernel variants
   a3c_set_shared_gpu(e->overlap != 0);
-  a3c_set_lean_cbwd(lean_cbwd(e));
+  a3c_set_bwd_bound(bwd_bound(e));
   mark(2, s);
   int rc = enqueue_grad_impl(e, sl, s);
   a3c_set_shared_gpu(false);
-  a3c_set_lean_cbwd(false);
+  a3c_set_bwd_bound(false);
   return rc;
 }
 
@@ -1000,7 +999,8 @@ static int rollout_grad(a3c_engine* e, hipStream_t s, bool fused) {
   // of k starts with rollout k+1 instead of ~10 us ahead of it, where its GEMMs slow rollout k+1's
   // first steps (M1 4.42-4.53M -> 4.56-4.57M, M2 4.75-4.82M -> 4.50M if used there).
   // Either way rollout k is complete in rs order.
-  const bool late_go = !bwd_bound(e);
+  static const int late_env = getenv("A3C_LATE_GO") ? atoi(getenv("A3C_LATE_GO")) : -1;   // A/B override
+  const bool late_go = late_env >= 0 ? late_env != 0 : !bwd_bound(e);
   auto signal_rollout = [&](int q) -> int {
     if (e->wait_value) {
       A3C_CHECK(hipStreamWriteValue32(e->rs, e->xflags + 1, ++e->r_seq, 0));
@@ -1438,8 +1438,8 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
   const Slot& sl = e->slot[0];
   if (e->rs) A3C_CHECK(hipStreamSynchronize(e->rs));
   a3c_set_shared_gpu(e->overlap != 0);      // time the variants the engine runs
-  a3c_set_lean_cbwd(lean_cbwd(e));
-  struct ResetShared { ~ResetShared() { a3c_set_shared_gpu(false); a3c_set_lean_cbwd(false); } } reset_shared;
+  a3c_set_bwd_bound(bwd_bound(e));
+  struct ResetShared { ~ResetShared() { a3c_set_shared_gpu(false); a3c_set_bwd_bound(false); } } reset_shared;
   if (kernel == A3C_KER_CONV12_FWD || kernel == A3C_KER_FC_FWD || kernel == A3C_KER_HEAD_SCREEN_CONV12) {
     int rc0 = a3c_prep_fwd_launch(L, e->params, sl.prep, s);
     if (rc0) return rc0;

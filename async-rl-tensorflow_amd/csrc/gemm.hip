@@ -230,10 +230,10 @@ int a3c_gemm(bool a_kc, bool b_nc, GemmArgs g, hipStream_t s) {
   int rc = gemm_setup(a_kc, b_nc, g);
   if (rc) return rc;
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, g.nsplit);
-  // (off by default: it halves the backward GEMMs' HBM bytes, 124 -> 73 MB per iteration, but
-  // the overlapped bench drops 4.56M -> 4.05M env-steps/s: tools/ab.sh, profile r3v1)
-  static const int env_xcd = getenv("A3C_GEMM_XCD") ? atoi(getenv("A3C_GEMM_XCD")) : 0;
-  if (g.xcd && env_xcd) {
+  // XCD-grouped order where the caller asks for it (the overlapped backward when it bounds the
+  // iteration): it halves the backward GEMMs' HBM bytes, 124 -> 73 MB per iteration (profile
+  // r3v1), but beside a rollout that bounds the iteration it costs 4.56M -> 4.05M env-steps/s
+  if (g.xcd) {
     const int G = g.xcd == 1 ? (int)(grid.y * grid.z) : (int)(grid.x * grid.z);
     const int J = g.xcd == 1 ? (int)grid.x : (int)grid.y;
     const dim3 g1((unsigned)(8 * ((G + 7) / 8) * J));

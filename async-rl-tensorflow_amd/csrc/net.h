@@ -168,7 +168,7 @@ int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipSt
 bool a3c_shared_gpu();
 void a3c_set_shared_gpu(bool v);
 bool a3c_lean_cbwd();
-void a3c_set_lean_cbwd(bool v);
+void a3c_set_bwd_bound(bool v);
 
 // stage the HIST u8 planes of state b into LDS (HIST x 441 uint4)
 __device__ inline void stage_state(const StateAddr& sa, int64_t b, int64_t tau0, uint8_t* x8) {

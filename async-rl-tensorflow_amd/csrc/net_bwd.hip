@@ -824,6 +824,7 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   return p;
 }
 
+static bool xcd_gemm();   // (below, beside the other mode knobs)
 int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
                         const float* act_l1, const float* act_l2, const float* act_l3,
                         const float* z, const int32_t* actions, const float* target, float beta,
@@ -880,7 +881,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   gf.C = grads + L.off[T_FCW]; gf.ldc = FC;
   gf.M = FLAT; gf.N = FC; gf.K = (int)B;
   gf.epi = EPI_STORE; gf.slab = ws + p.fcslab; gf.nsplit = p.fc_split; gf.colsum = ws + p.fccol;
-  gf.xcd = 1;                           // the 4 column tiles of an l2 strip on one XCD
+  gf.xcd = xcd_gemm() ? 1 : 0;          // the 4 column tiles of an l2 strip on one XCD
   // dl2[B][2592] = (dl3 W^T) * (l2 > 0)
   GemmArgs gd = {};
   gd.A = dh3; gd.lda = FC;               // A(m=b, k) = dl3[b][k]
@@ -888,7 +889,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   gd.C = dl2; gd.ldc = FLAT;
   gd.M = (int)B; gd.N = FLAT; gd.K = FC;
   gd.epi = EPI_MASK; gd.mask = act_l2; gd.ldm = FLAT; gd.nsplit = 1;
-  gd.xcd = 2;                           // the 20 row tiles of a W strip on one XCD
+  gd.xcd = xcd_gemm() ? 2 : 0;          // the 20 row tiles of a W strip on one XCD
   int rc;
   // sync mode: the three GEMMs in one launch (3.32M -> 3.41M env-steps/s); overlapped with the
   // next rollout the 1,420-workgroup launch slows it more than it gains (4.40M -> 4.30M), and so
@@ -992,14 +993,20 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
 static thread_local bool t_shared_gpu = false;
 bool a3c_shared_gpu() { return t_shared_gpu; }
 void a3c_set_shared_gpu(bool v) { t_shared_gpu = v; }
-// the compact conv backward's LDS-lean form (set by the engine where the backward, not the
-// rollout, bounds the overlapped iteration: mode M2); A3C_CB_LEAN=0/1 overrides
-static thread_local bool t_lean_cbwd = false;
+// set by the engine where the backward stream, not the rollout, bounds the overlapped iteration
+// (mode M2, several GPUs): there the compact conv backward takes its LDS-lean form and the fc
+// GEMMs their XCD-grouped tile order; A3C_CB_LEAN=0/1 and A3C_GEMM_XCD=0/1 override each
+static thread_local bool t_bwd_bound = false;
+static int env_knob(const char* name) { return getenv(name) ? atoi(getenv(name)) : -1; }
 bool a3c_lean_cbwd() {
-  static const int env = getenv("A3C_CB_LEAN") ? atoi(getenv("A3C_CB_LEAN")) : -1;
-  return env >= 0 ? env != 0 : t_lean_cbwd;
+  static const int env = env_knob("A3C_CB_LEAN");
+  return env >= 0 ? env != 0 : t_bwd_bound;
 }
-void a3c_set_lean_cbwd(bool v) { t_lean_cbwd = v; }
+static bool xcd_gemm() {
+  static const int env = env_knob("A3C_GEMM_XCD");
+  return env >= 0 ? env != 0 : t_bwd_bound;
+}
+void a3c_set_bwd_bound(bool v) { t_bwd_bound = v; }
 
 int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,
                         const float* dl2, float* ws, hipStream_t s) {
