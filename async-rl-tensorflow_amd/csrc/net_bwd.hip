@@ -176,6 +176,16 @@ constexpr int cb_tail(bool lx) {
 // the backward overlaps the next rollout (engine overlap mode)
 #define CB_SMEM_COMPACT (CB_X8 + cb_tail(false))                                        // 74304
 #define CB_SMEM_COMPACT_LX (CB_X8 + cb_tail(true))                                      // 80480
+// LDS the compact kernels reserve: more than half of the CU's 160 KB, so that two of their
+// workgroups never share a CU -- such a CU has no room left for a rollout workgroup (79.6 KB),
+// and the rollout step then runs a second round of workgroups -- and no more than 160 KB minus
+// the rollout kernel's (A3C_CB_SOLO=0: the kernels' own sizes)
+#define CB_SMEM_SOLO 82944
+static_assert(2 * CB_SMEM_SOLO > 160 * 1024 && CB_SMEM_SOLO >= CB_SMEM_COMPACT_LX, "solo reservation");
+static int cb_smem(int own) {
+  static const bool solo = getenv("A3C_CB_SOLO") ? atoi(getenv("A3C_CB_SOLO")) != 0 : true;
+  return solo ? CB_SMEM_SOLO : own;
+}
 
 // the nw waves DMA `nbytes` (multiple of 16) from g to LDS dst in 1 KiB wave-instructions
 __device__ inline void glds_copy(const uint8_t* g, uint8_t* dst, int nbytes, int wid, int lane, int nw) {
@@ -1020,13 +1030,13 @@ int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa,
   static const int env_nw = getenv("A3C_CB_WAVES") ? atoi(getenv("A3C_CB_WAVES")) : 0;
   const int nw = env_nw ? env_nw : (a3c_shared_gpu() ? 4 : 8);
   if (a3c_shared_gpu() && nw == 4 && a3c_lean_cbwd())
-    hipLaunchKernelGGL((k_conv_bwd<false, 4, true>), dim3((unsigned)p.nwg), dim3(256), CB_SMEM_COMPACT_LX, s, sa, B,
+    hipLaunchKernelGGL((k_conv_bwd<false, 4, true>), dim3((unsigned)p.nwg), dim3(256), cb_smem(CB_SMEM_COMPACT_LX), s, sa, B,
                        p.per_wg, act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
   else if (a3c_shared_gpu() && nw == 4)
-    hipLaunchKernelGGL((k_conv_bwd<false, 4, false>), dim3((unsigned)p.nwg), dim3(256), CB_SMEM_COMPACT, s, sa, B,
+    hipLaunchKernelGGL((k_conv_bwd<false, 4, false>), dim3((unsigned)p.nwg), dim3(256), cb_smem(CB_SMEM_COMPACT), s, sa, B,
                        p.per_wg, act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
   else if (a3c_shared_gpu())
-    hipLaunchKernelGGL((k_conv_bwd<false, 8, true>), dim3((unsigned)p.nwg), dim3(512), CB_SMEM_COMPACT_LX, s, sa, B,
+    hipLaunchKernelGGL((k_conv_bwd<false, 8, true>), dim3((unsigned)p.nwg), dim3(512), cb_smem(CB_SMEM_COMPACT_LX), s, sa, B,
                        p.per_wg, act_l1, dl2, P + L.off[T_L2W], ws + p.cslab);
   else if (nw == 4)
     hipLaunchKernelGGL((k_conv_bwd<true, 4, false>), dim3((unsigned)p.nwg), dim3(256), CB_SMEM_DMA, s, sa, B, p.per_wg,
@@ -1060,7 +1070,7 @@ void a3c_conv_bwd_set_smem() {
   const int a = hipFuncAttributeMaxDynamicSharedMemorySize;
   (void)hipFuncSetAttribute((const void*)k_conv_bwd<true, 4, false>, (hipFuncAttribute)a, CB_SMEM_DMA);
   (void)hipFuncSetAttribute((const void*)k_conv_bwd<true, 8, true>, (hipFuncAttribute)a, CB_SMEM_DMA);
-  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 4, false>, (hipFuncAttribute)a, CB_SMEM_COMPACT);
-  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 4, true>, (hipFuncAttribute)a, CB_SMEM_COMPACT_LX);
-  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 8, true>, (hipFuncAttribute)a, CB_SMEM_COMPACT_LX);
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 4, false>, (hipFuncAttribute)a, cb_smem(CB_SMEM_COMPACT));
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 4, true>, (hipFuncAttribute)a, cb_smem(CB_SMEM_COMPACT_LX));
+  (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 8, true>, (hipFuncAttribute)a, cb_smem(CB_SMEM_COMPACT_LX));
 }

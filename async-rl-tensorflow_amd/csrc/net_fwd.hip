@@ -737,9 +737,15 @@ __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restr
 // are final) plus the screen just computed (kept in LDS).  One kernel boundary and the conv
 // staging latency fewer per rollout step.  LDS: screen scratch (54 KB, later overlaid by l1) |
 // x8 (28 KB).
-#define HSC_X8_OFF (((SCREEN_FRAME_SMEM) + 15) / 16 * 16)
+// The screen's vertical-tap table goes to the x8 region behind the new plane's bf16 copy (free
+// during the screen), which keeps the kernel under 80 KB: a CU holds one of it beside one
+// compact conv backward workgroup (CB_SMEM_SOLO).
+#define HSC_X8_OFF (((SCREEN_FRAME_SMEM_NOKV) + 15) / 16 * 16)
 #define HSC_SMEM (HSC_X8_OFF + HIST * PLANE)
-static_assert(L1S_BYTES <= SCREEN_FRAME_SMEM, "l1 overlays the screen scratch");
+#define HSC_KV_OFF (PLANE * 2)
+static_assert(L1S_BYTES <= SCREEN_FRAME_SMEM_NOKV, "l1 overlays the screen scratch");
+static_assert(HSC_KV_OFF % 16 == 0 && HSC_KV_OFF + SCREEN_KV_BYTES <= HIST * PLANE, "tap table in the x8 region");
+static_assert(HSC_SMEM + 16 <= 160 * 1024 - 82944, "rollout workgroup beside a compact conv backward one");
 // waves_per_eu(4) caps it at 128 VGPRs: with the concurrent k_conv_bwd<false,4> (254 VGPRs,
 // one wave per SIMD) two of its waves per SIMD must fit in the remaining 258
 template <bool SAVE_L1>
@@ -862,7 +868,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
     atari::copy_frame84<512>(sel.pool + (int64_t)frame * PLANE, slot, xnew, conv1_old);
   else
     atari::screen_frame<512>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3), slot, smem, dbg, xnew,
-                             conv1_old);
+                             conv1_old, (int*)(x8 + HSC_KV_OFF));
   if (dbg && threadIdx.x == 0) dbg[9] = __builtin_readcyclecounter();
   uint4 wn[6];
 #pragma unroll

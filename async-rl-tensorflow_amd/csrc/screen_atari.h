@@ -194,7 +194,8 @@ __device__ inline void hpass_seg(const uint8_t* __restrict__ grow, uint8_t* __re
 // horizontal = 16 tasks (column segment, block of 64 rows), lane = row; vertical = 28 tasks
 // of 3 output rows x 21 column quads, lane = (row, quad), taps read from the LDS table.
 #define SCREEN_KV_BYTES (84 * 8 * 4)
-#define SCREEN_FRAME_SMEM (210 * 160 + 210 * 84 + 96 + SCREEN_KV_BYTES)
+#define SCREEN_FRAME_SMEM_NOKV (210 * 160 + 210 * 84 + 96)   // the tap table elsewhere (kvs_at)
+#define SCREEN_FRAME_SMEM (SCREEN_FRAME_SMEM_NOKV + SCREEN_KV_BYTES)
 // 4 u8 pixels (one dword, little-endian) -> 4 bf16 (exact: integers 0..255 are the upper half of
 // their f32)
 __device__ inline uint2 u8x4_to_bf16x4(uint32_t d) {
@@ -212,10 +213,12 @@ struct NoScreenMid {
 // pass writes the scratch (it may use the first 51 KB of smem; it must not wait on vector memory)
 template <int NT, typename Mid = NoScreenMid>
 __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __restrict__ out, uint8_t* smem,
-                                    uint64_t* dbg = nullptr, uint16_t* lds_bf16 = nullptr, Mid mid = Mid()) {
+                                    uint64_t* dbg = nullptr, uint16_t* lds_bf16 = nullptr, Mid mid = Mid(),
+                                    int* kvs_at = nullptr) {
   uint8_t* gray = smem;
   uint8_t* tmp = smem + IH * IW;
-  int* kvs = (int*)(tmp + IH * OW + 96);              // [yy][8]: 7 taps, xmin
+  // [yy][8]: 7 taps, xmin -- after the scratch, or at kvs_at (written after mid())
+  int* kvs = kvs_at ? kvs_at : (int*)(tmp + IH * OW + 96);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr int NWV = NT / 64;
