@@ -130,6 +130,52 @@ __device__ inline const uint8_t* state_plane(const StateAddr& a, int64_t b, int 
 #define WG_T1(dst) ((void)0)
 #endif
 
+// Debug builds only (-DA3C_WGLOG, tools/wglog.py): every workgroup of the instrumented kernels
+// appends (start, end, kind | xcc | workgroup | HW_ID) to a device log, so which workgroups shared
+// a CU, and when, can be read back (a3c_debug_wglog).  Thread 0 logs at its own exit.
+#ifdef A3C_WGLOG
+// no atomics (a single log counter serialised the chip): workgroup b of kind k keeps its own
+// launch counter cnt[k][b] (launches of one kernel are ordered on their stream, and kernel
+// boundaries make the previous launch's store visible) and writes slot e[k][b][cnt % WGL_RING]
+#define WGL_KINDS 16
+#define WGL_MAXWG 4096
+#define WGL_RING 16
+struct WglBuf {
+  unsigned int on, pad[3];
+  unsigned int cnt[WGL_KINDS][WGL_MAXWG];
+  unsigned long long e[WGL_KINDS][WGL_MAXWG][WGL_RING][3];   // start, end, xcc << 32 | HW_ID
+};
+static __device__ WglBuf* g_wgl;   // one per translation unit, bound by its a3c_wglog_bind_* hook
+struct WgLog {
+  unsigned long long t0;
+  unsigned kind, c;
+  WglBuf* b;
+  __device__ explicit WgLog(unsigned k) : t0(__builtin_amdgcn_s_memrealtime()), kind(k), c(0), b(nullptr) {
+    WglBuf* g = g_wgl;
+    if (threadIdx.x == 0 && g && g->on && blockIdx.x < WGL_MAXWG) {
+      b = g;
+      c = g->cnt[k][blockIdx.x];   // (used at the end: the load retires meanwhile)
+    }
+  }
+  __device__ ~WgLog() {
+    if (!b) return;
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    unsigned long long* e = b->e[kind][blockIdx.x][c % WGL_RING];
+    e[0] = t0;
+    e[1] = __builtin_amdgcn_s_memrealtime();
+    e[2] = ((unsigned long long)(xcc & 15) << 32) | hw;
+    b->cnt[kind][blockIdx.x] = c + 1;
+  }
+};
+#define WGLOG(kind) WgLog wgl_(kind)
+#define WGLOG_BIND(name) \
+  void name(WglBuf* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wgl), &p, sizeof(p)); }
+#else
+#define WGLOG(kind) ((void)0)
+#endif
+
 // Stores of activations that the next kernel reads on other XCDs (l1, l2, l3, the frame ring):
 // non-temporal with A3C_NT_STORE (bypass the writing XCD's L2, so the end-of-kernel release has
 // fewer dirty lines to write back) -- an A/B switch.

@@ -676,6 +676,32 @@ extern "C" int a3c_debug_marks(unsigned long long* host, int reset) {
 static void mark(int, hipStream_t) {}
 #endif
 
+#ifdef A3C_WGLOG
+void a3c_wglog_bind_fwd(WglBuf*);
+void a3c_wglog_bind_bwd(WglBuf*);
+void a3c_wglog_bind_gemm(WglBuf*);
+void a3c_wglog_bind_optim(WglBuf*);
+// Debug builds only (tools/wglog.py): on >= 0 switches logging, reset clears the log; the whole
+// WglBuf is copied to host when host != nullptr (after a device sync); returns its size in bytes
+extern "C" int64_t a3c_debug_wglog(void* host, int on, int reset) {
+  static WglBuf* buf = nullptr;
+  if (!buf) {
+    A3C_CHECK(hipMalloc(&buf, sizeof(WglBuf)));
+    A3C_CHECK(hipMemset(buf, 0, sizeof(WglBuf)));
+    a3c_wglog_bind_fwd(buf); a3c_wglog_bind_bwd(buf); a3c_wglog_bind_gemm(buf); a3c_wglog_bind_optim(buf);
+  }
+  A3C_CHECK(hipDeviceSynchronize());
+  if (host) A3C_CHECK(hipMemcpy(host, buf, sizeof(WglBuf), hipMemcpyDeviceToHost));
+  if (reset) A3C_CHECK(hipMemset(buf, 0, sizeof(WglBuf)));
+  if (on >= 0) {
+    const unsigned v = (unsigned)on;
+    A3C_CHECK(hipMemcpy(buf, &v, 4, hipMemcpyHostToDevice));
+  }
+  A3C_CHECK(hipDeviceSynchronize());
+  return (int64_t)sizeof(WglBuf);
+}
+#endif
+
 static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
   mark(0, s);
   int rc = enqueue_rollout_begin(e, sl, s);

@@ -26,6 +26,9 @@ struct GemmArgs {
   // on one XCD (they share the A strip); 2 = the M-tiles of one (N-tile, K-chunk) on one XCD
   // (they share the B strip).  Speed only: every tile computes the same sums in the same order.
   int xcd;
+  // a3c_gemm: at most this many workgroups (0 = one per tile), each looping over tiles id, id +
+  // grid, ... -- fewer GEMM workgroups resident beside a concurrent kernel.  Speed only.
+  int max_wgs;
 };
 
 int a3c_gemm(bool a_kcontig, bool b_ncontig, GemmArgs g, hipStream_t s);

@@ -119,6 +119,7 @@ __device__ inline void gemm_tile_id(const GemmArgs& g, int id, float (&As)[BK][B
 
 template <bool A_KC, bool B_NC>
 __global__ void __launch_bounds__(256) k_gemm_f32(GemmArgs g) {
+  WGLOG(5);
   __shared__ __attribute__((aligned(16))) float As[BK][BM + PAD];
   __shared__ __attribute__((aligned(16))) float Bs[BK][BN + PAD];
   gemm_tile<A_KC, B_NC>(g, blockIdx.x, blockIdx.y, blockIdx.z, As, Bs);
@@ -130,6 +131,7 @@ __global__ void __launch_bounds__(256) k_gemm_f32(GemmArgs g) {
 // Ids past the last group exit at once.
 template <bool A_KC, bool B_NC>
 __global__ void __launch_bounds__(256) k_gemm_f32_x(GemmArgs g, int G, int J) {
+  WGLOG(5);
   __shared__ __attribute__((aligned(16))) float As[BK][BM + PAD];
   __shared__ __attribute__((aligned(16))) float Bs[BK][BN + PAD];
   const int id = blockIdx.x, slot = id >> 3;
@@ -140,11 +142,38 @@ __global__ void __launch_bounds__(256) k_gemm_f32_x(GemmArgs g, int G, int J) {
   else gemm_tile<A_KC, B_NC>(g, grp % gx, j, grp / gx, As, Bs);
 }
 
+// the tiles of a 3-D k_gemm_f32 grid (nb of them) on a capped grid, each workgroup looping over
+// tile ids blockIdx.x, + gridDim.x, ... (gemm_tile's leading barrier guards the LDS reuse)
+template <bool A_KC, bool B_NC>
+__global__ void __launch_bounds__(256) k_gemm_f32_p(GemmArgs g, int nb) {
+  WGLOG(5);
+  __shared__ __attribute__((aligned(16))) float As[BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[BK][BN + PAD];
+  for (int id = blockIdx.x; id < nb; id += gridDim.x) gemm_tile_id<A_KC, B_NC>(g, id, As, Bs);
+}
+
+// k_gemm_f32_x on a capped grid (a multiple of 8, so every id a workgroup visits keeps its XCD)
+template <bool A_KC, bool B_NC>
+__global__ void __launch_bounds__(256) k_gemm_f32_xp(GemmArgs g, int G, int J, int nid) {
+  WGLOG(5);
+  __shared__ __attribute__((aligned(16))) float As[BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[BK][BN + PAD];
+  const int gx = (g.N + BN - 1) / BN, gy = (g.M + BM - 1) / BM;
+  for (int id = blockIdx.x; id < nid; id += gridDim.x) {
+    const int slot = id >> 3;
+    const int grp = 8 * (slot / J) + (id & 7), j = slot % J;
+    if (grp >= G) continue;
+    if (g.xcd == 1) gemm_tile<A_KC, B_NC>(g, j, grp % gy, grp / gy, As, Bs);
+    else gemm_tile<A_KC, B_NC>(g, grp % gx, j, grp / gx, As, Bs);
+  }
+}
+
 // Several independent GEMMs in one launch (the backward's dW_head, dW_fc and dl2 all need only
 // dz / dl3): workgroup ids [0, nb[0]) are GEMM 0's tiles, then GEMM 1's, then GEMM 2's -- one
 // kernel boundary instead of three and one fill/drain tail.  Flavours: (A k-contiguous, B
 // n-contiguous) = (false, true), (false, true), (true, false).
 __global__ void __launch_bounds__(256) k_gemm_multi(GemmArgs g0, GemmArgs g1, GemmArgs g2, int nb0, int nb1) {
+  WGLOG(5);
   __shared__ __attribute__((aligned(16))) float As[BK][BM + PAD];
   __shared__ __attribute__((aligned(16))) float Bs[BK][BN + PAD];
   // (each branch names its own kernel argument: selecting a pointer to one would copy all three
@@ -160,6 +189,7 @@ __global__ void k_reduce_slabs(const float* __restrict__ slab, int nsplit, int M
                                float* __restrict__ C, int64_t ldc, int epi,
                                const float* __restrict__ bias, const float* __restrict__ mask,
                                int64_t ldm) {
+  WGLOG(8);
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t total = (int64_t)M * N;
   if (i >= total) return;
@@ -233,14 +263,34 @@ int a3c_gemm(bool a_kc, bool b_nc, GemmArgs g, hipStream_t s) {
   // XCD-grouped order where the caller asks for it (the overlapped backward when it bounds the
   // iteration): it halves the backward GEMMs' HBM bytes, 124 -> 73 MB per iteration (profile
   // r3v1), but beside a rollout that bounds the iteration it costs 4.56M -> 4.05M env-steps/s
+  const int nb = (int)(grid.x * grid.y * grid.z);
   if (g.xcd) {
     const int G = g.xcd == 1 ? (int)(grid.y * grid.z) : (int)(grid.x * grid.z);
     const int J = g.xcd == 1 ? (int)grid.x : (int)grid.y;
-    const dim3 g1((unsigned)(8 * ((G + 7) / 8) * J));
+    const int nid = 8 * ((G + 7) / 8) * J;
+    if (g.max_wgs > 0 && nid > g.max_wgs) {
+      const dim3 gp((unsigned)(8 * ((g.max_wgs + 7) / 8)));
+      if (a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_xp<true, true>), gp, dim3(256), 0, s, g, G, J, nid);
+      else if (a_kc && !b_nc) hipLaunchKernelGGL((k_gemm_f32_xp<true, false>), gp, dim3(256), 0, s, g, G, J, nid);
+      else if (!a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_xp<false, true>), gp, dim3(256), 0, s, g, G, J, nid);
+      else hipLaunchKernelGGL((k_gemm_f32_xp<false, false>), gp, dim3(256), 0, s, g, G, J, nid);
+      A3C_CHECK(hipGetLastError());
+      return g.defer_reduce ? 0 : a3c_gemm_reduce(g, s);
+    }
+    const dim3 g1((unsigned)nid);
     if (a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_x<true, true>), g1, dim3(256), 0, s, g, G, J);
     else if (a_kc && !b_nc) hipLaunchKernelGGL((k_gemm_f32_x<true, false>), g1, dim3(256), 0, s, g, G, J);
     else if (!a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_x<false, true>), g1, dim3(256), 0, s, g, G, J);
     else hipLaunchKernelGGL((k_gemm_f32_x<false, false>), g1, dim3(256), 0, s, g, G, J);
+    A3C_CHECK(hipGetLastError());
+    return g.defer_reduce ? 0 : a3c_gemm_reduce(g, s);
+  }
+  if (g.max_wgs > 0 && nb > g.max_wgs) {
+    const dim3 gp((unsigned)g.max_wgs);
+    if (a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_p<true, true>), gp, dim3(256), 0, s, g, nb);
+    else if (a_kc && !b_nc) hipLaunchKernelGGL((k_gemm_f32_p<true, false>), gp, dim3(256), 0, s, g, nb);
+    else if (!a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_p<false, true>), gp, dim3(256), 0, s, g, nb);
+    else hipLaunchKernelGGL((k_gemm_f32_p<false, false>), gp, dim3(256), 0, s, g, nb);
     A3C_CHECK(hipGetLastError());
     return g.defer_reduce ? 0 : a3c_gemm_reduce(g, s);
   }
@@ -251,3 +301,7 @@ int a3c_gemm(bool a_kc, bool b_nc, GemmArgs g, hipStream_t s) {
   A3C_CHECK(hipGetLastError());
   return g.defer_reduce ? 0 : a3c_gemm_reduce(g, s);
 }
+
+#ifdef A3C_WGLOG
+WGLOG_BIND(a3c_wglog_bind_gemm)
+#endif

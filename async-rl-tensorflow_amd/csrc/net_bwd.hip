@@ -61,6 +61,7 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ z, i
                                                   int literal, float invB, int64_t B,
                                                   float* __restrict__ dz, float* __restrict__ dh3,
                                                   float* __restrict__ terms, ReturnsArgs ra, int relu) {
+  WGLOG(7);
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
@@ -218,6 +219,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
                                                   const float* __restrict__ dl2,
                                                   const float* __restrict__ W2,
                                                   float* __restrict__ slab) {
+  WGLOG(6);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* x8buf = smem;                                             // [DMA ? 2 : 1][CB_X8]
   uint8_t* l1st = smem + (DMA ? 2 : 1) * CB_X8;
@@ -699,6 +701,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
 // pass 1 of the conv-slab reduction: dst[g][i] = sum of slabs s in group g (fixed order)
 __global__ void __launch_bounds__(256) k_slab_group(const float* __restrict__ src, int nsplit, int per,
                                                     int64_t len, float* __restrict__ dst) {
+  WGLOG(8);
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= len) return;
   const int g = blockIdx.y;
@@ -730,6 +733,7 @@ __device__ void loss_reduce_block(const float* __restrict__ terms, int64_t B, fl
 // the blocks after it sum the other tensors' chunks (fused per-tensor norms, FinalizeSegs)
 __global__ void __launch_bounds__(256) k_finalize(FinalizeSegs fs, const float* __restrict__ terms, int64_t B,
                                                   float* __restrict__ loss_out) {
+  WGLOG(8);
   const int b = blockIdx.x;
   if (b < FIN_X * fs.n) {
     const int y = b / FIN_X, x = b - y * FIN_X;
@@ -900,6 +904,10 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   gd.M = (int)B; gd.N = FLAT; gd.K = FC;
   gd.epi = EPI_MASK; gd.mask = act_l2; gd.ldm = FLAT; gd.nsplit = 1;
   gd.xcd = xcd_gemm() ? 2 : 0;          // the 20 row tiles of a W strip on one XCD
+  {
+    static const int env_wgs = getenv("A3C_GEMM_WGS") ? atoi(getenv("A3C_GEMM_WGS")) : 0;
+    if (a3c_shared_gpu()) gh.max_wgs = gf.max_wgs = gd.max_wgs = env_wgs;
+  }
   int rc;
   // sync mode: the three GEMMs in one launch (3.32M -> 3.41M env-steps/s); overlapped with the
   // next rollout the 1,420-workgroup launch slows it more than it gains (4.40M -> 4.30M), and so
@@ -1074,3 +1082,7 @@ void a3c_conv_bwd_set_smem() {
   (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 4, true>, (hipFuncAttribute)a, cb_smem(CB_SMEM_COMPACT_LX));
   (void)hipFuncSetAttribute((const void*)k_conv_bwd<false, 8, true>, (hipFuncAttribute)a, cb_smem(CB_SMEM_COMPACT_LX));
 }
+
+#ifdef A3C_WGLOG
+WGLOG_BIND(a3c_wglog_bind_bwd)
+#endif

@@ -60,6 +60,7 @@ __global__ void __launch_bounds__(256) k_prep_fwd(const float* __restrict__ W1, 
                                                   const float* __restrict__ W2, uint8_t* __restrict__ prep,
                                                   const int64_t* __restrict__ tau_src, int64_t* __restrict__ tau_dst) {
 #pragma clang fp contract(off)
+  WGLOG(10);
   const int t = blockIdx.x * 256 + threadIdx.x;
   if (t == 0 && tau_dst) *tau_dst = *tau_src;
   if (t < C1_K * 64 * 8) {                                   // (kh, lane, j): conv1 split
@@ -372,6 +373,7 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
                                                     const float* __restrict__ b2,
                                                     float* __restrict__ act_l1,
                                                     float* __restrict__ act_l2) {
+  WGLOG(3);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint16_t* xb = (uint16_t*)smem;
   uint8_t* x8 = smem;
@@ -608,6 +610,7 @@ __global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, 
                                                   const float* __restrict__ Wp, const float* __restrict__ bp,
                                                   const float* __restrict__ Wv, const float* __restrict__ bv,
                                                   int A, int zs, float* __restrict__ z, HeadSelect sel) {
+  WGLOG(4);
   __shared__ __attribute__((aligned(16))) f32x4 l3s[4][64];
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -756,6 +759,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
                                                             const float* __restrict__ bv, int A, int zs,
                                                             float* __restrict__ z, HeadSelect sel,
                                                             Conv12Next nx) {
+  WGLOG(1);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* x8 = smem + HSC_X8_OFF;
   const int64_t b = blockIdx.x;
@@ -1203,6 +1207,7 @@ __device__ inline int fcp_c0(int x) { return (FC_CH * x) / FC_NS; }
 
 __global__ void __launch_bounds__(256) k_fc_part(const float* __restrict__ A, const float* __restrict__ Wp,
                                                  float* __restrict__ part, int M) {
+  WGLOG(2);
   __shared__ __attribute__((aligned(16))) float as[FCP_RB * FCP_LD];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i16 = lane & 15, j4 = lane >> 4;
@@ -1367,3 +1372,7 @@ int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* 
   A3C_CHECK(hipGetLastError());
   return 0;
 }
+
+#ifdef A3C_WGLOG
+WGLOG_BIND(a3c_wglog_bind_fwd)
+#endif

@@ -45,6 +45,7 @@ __global__ void __launch_bounds__(256) k_apply(float* __restrict__ w, float* __r
                                                TensorTab tt, const double* __restrict__ part, OptParams op,
                                                float* __restrict__ sumsq_out) {
 #pragma clang fp contract(off)
+  WGLOG(9);
   __shared__ float cm[A3C_MAX_TENSORS];
   __shared__ float s_lr, s_copy;
   __shared__ double red[4][A3C_MAX_TENSORS];
@@ -328,3 +329,7 @@ extern "C" int a3c_ipc_close(void* p) {
   if (p) A3C_CHECK(hipIpcCloseMemHandle(p));
   return 0;
 }
+
+#ifdef A3C_WGLOG
+WGLOG_BIND(a3c_wglog_bind_optim)
+#endif
