@@ -517,6 +517,22 @@ static const Slot& prev_slot(const a3c_engine* e, const Slot& sl) {
   return e->nslot == 2 ? e->slot[&sl == &e->slot[0] ? 1 : 0] : sl;
 }
 
+// "rollout k done", the go of its backward (rollout_grad): written on the rollout stream right
+// behind rollout k when the backward bounds the iteration; otherwise at the start of rollout
+// k+1, behind its wait for the apply it needs -- then the backward of k starts with rollout k+1
+// instead of ~10 us ahead of it, where its GEMMs slowed rollout k+1's first steps (DESIGN §6;
+// M1 4.42-4.53M -> 4.56-4.57M, M2 4.75-4.82M -> 4.50M if used there), and rollout k+1's prep
+// kernel bumps the sequence itself (kernel_go: no write-value operation on the rollout stream)
+static bool bwd_bound(const a3c_engine* e);
+static bool late_go(const a3c_engine* e) {
+  static const int env = getenv("A3C_LATE_GO") ? atoi(getenv("A3C_LATE_GO")) : -1;   // A/B override
+  return env >= 0 ? env != 0 : !bwd_bound(e);
+}
+static bool kernel_go(const a3c_engine* e) {
+  static const int env = getenv("A3C_KERNEL_GO") ? atoi(getenv("A3C_KERNEL_GO")) : 1;   // A/B override
+  return e->overlap && e->wait_value && late_go(e) && env != 0;
+}
+
 // rollout start: forward weights of the rollout's parameters (+ q: the epsilon schedule)
 static int enqueue_rollout_begin(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
@@ -530,7 +546,7 @@ static int enqueue_rollout_begin(a3c_engine* e, const Slot& sl, hipStream_t s) {
   int rc =
 #endif
   rc = a3c_prep_fwd_launch(e->L, sl.P, sl.prep, s, e->overlap ? e->counters : nullptr,
-                           e->overlap ? sl.tau : nullptr);
+                           e->overlap ? sl.tau : nullptr, kernel_go(e) ? e->xflags + 1 : nullptr);
   if (rc) return rc;
   if (e->L.lstm) {
     rc = a3c_lstm_transpose_launch(sl.P + e->L.off[T_LW], sl.lwt, s);
@@ -1020,13 +1036,8 @@ static int rollout_grad(a3c_engine* e, hipStream_t s, bool fused) {
     A3C_CHECK(hipEventRecord(e->ev_start, s));
     A3C_CHECK(hipStreamWaitEvent(e->rs, e->ev_start, 0));
   }
-  // "rollout k done" (the backward's go): signalled right behind rollout k when the backward bounds
-  // the iteration; otherwise behind the wait for the apply rollout k+1 needs, so that the backward
-  // of k starts with rollout k+1 instead of ~10 us ahead of it, where its GEMMs slow rollout k+1's
-  // first steps (M1 4.42-4.53M -> 4.56-4.57M, M2 4.75-4.82M -> 4.50M if used there).
-  // Either way rollout k is complete in rs order.
-  static const int late_env = getenv("A3C_LATE_GO") ? atoi(getenv("A3C_LATE_GO")) : -1;   // A/B override
-  const bool late_go = late_env >= 0 ? late_env != 0 : !bwd_bound(e);
+  // the go of the backward of rollout k-1 (late_go); in rs order rollout k-1 is complete
+  const bool late = late_go(e);
   auto signal_rollout = [&](int q) -> int {
     if (e->wait_value) {
       A3C_CHECK(hipStreamWriteValue32(e->rs, e->xflags + 1, ++e->r_seq, 0));
@@ -1036,11 +1047,16 @@ static int rollout_grad(a3c_engine* e, hipStream_t s, bool fused) {
     }
     return 0;
   };
-  int rc = late_go && e->iter >= 1 ? signal_rollout(p ^ 1) : 0;
+  int rc = 0;
+  if (kernel_go(e)) {            // the rollout's prep kernel bumps xflags[1] (every rollout)
+    e->roll_seq[p ^ 1] = ++e->r_seq;
+  } else if (late && e->iter >= 1) {
+    rc = signal_rollout(p ^ 1);
+  }
   if (rc) return rc;
   rc = run_graph(e, 1 + p, 1, p, e->rs);   // (its prep kernel snapshots tau into sl.tau)
   if (rc) return rc;
-  rc = late_go ? 0 : signal_rollout(p);
+  rc = late ? 0 : signal_rollout(p);
   if (rc) return rc;
   e->grad_ready = false;
 #ifdef A3C_MARKERS

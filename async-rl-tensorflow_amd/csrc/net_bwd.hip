@@ -839,6 +839,7 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
 }
 
 static bool xcd_gemm();   // (below, beside the other mode knobs)
+static bool dwfc_late_knob();
 int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
                         const float* act_l1, const float* act_l2, const float* act_l3,
                         const float* z, const int32_t* actions, const float* target, float beta,
@@ -939,10 +940,15 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
 #else
     constexpr bool abl_gemm = false;
 #endif
+    // dwfc_late: the fc weight GEMM (+ its fold) behind the conv backward -- only dl2 stands
+    // between the head and the conv
+    const bool dwfc_late = dwfc_late_knob() && !fork;
     rc = abl_gemm ? 0 : a3c_gemm(false, true, gh, ws_s);
     if (rc) return rc;
-    rc = abl_gemm ? 0 : a3c_gemm(false, true, gf, ws_s);
-    if (rc) return rc;
+    if (!dwfc_late) {
+      rc = abl_gemm ? 0 : a3c_gemm(false, true, gf, ws_s);
+      if (rc) return rc;
+    }
     if (fork) A3C_CHECK(hipEventRecord(ev_join, side));
     rc = abl_gemm ? 0 : a3c_gemm(true, false, gd, s);
     if (rc) return rc;
@@ -954,6 +960,10 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
 #ifdef A3C_MARKERS
     a3c_mark(5, s);
 #endif
+    if (dwfc_late) {
+      rc = abl_gemm ? 0 : a3c_gemm(false, true, gf, s);
+      if (rc) return rc;
+    }
   }
 
   FinalizeSegs fs = {};
@@ -1012,8 +1022,9 @@ static thread_local bool t_shared_gpu = false;
 bool a3c_shared_gpu() { return t_shared_gpu; }
 void a3c_set_shared_gpu(bool v) { t_shared_gpu = v; }
 // set by the engine where the backward stream, not the rollout, bounds the overlapped iteration
-// (mode M2, several GPUs): there the compact conv backward takes its LDS-lean form and the fc
-// GEMMs their XCD-grouped tile order; A3C_CB_LEAN=0/1 and A3C_GEMM_XCD=0/1 override each
+// (mode M2, several GPUs): there the compact conv backward takes its LDS-lean form, the fc
+// GEMMs their XCD-grouped tile order and the fc weight GEMM runs behind the conv backward;
+// A3C_CB_LEAN, A3C_GEMM_XCD and A3C_DWFC_LATE (0/1) override each
 static thread_local bool t_bwd_bound = false;
 static int env_knob(const char* name) { return getenv(name) ? atoi(getenv(name)) : -1; }
 bool a3c_lean_cbwd() {
@@ -1022,6 +1033,11 @@ bool a3c_lean_cbwd() {
 }
 static bool xcd_gemm() {
   static const int env = env_knob("A3C_GEMM_XCD");
+  return env >= 0 ? env != 0 : t_bwd_bound;
+}
+// the fc weight GEMM behind the conv backward (M2: 5.15-5.18M -> 5.20-5.22M; M1 neutral)
+static bool dwfc_late_knob() {
+  static const int env = env_knob("A3C_DWFC_LATE");
   return env >= 0 ? env != 0 : t_bwd_bound;
 }
 void a3c_set_bwd_bound(bool v) { t_bwd_bound = v; }

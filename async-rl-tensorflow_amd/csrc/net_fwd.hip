@@ -58,11 +58,15 @@ __device__ inline void split3_bits(float w, uint32_t& h, uint32_t& m, uint32_t& 
 
 __global__ void __launch_bounds__(256) k_prep_fwd(const float* __restrict__ W1, const float* __restrict__ Wfc,
                                                   const float* __restrict__ W2, uint8_t* __restrict__ prep,
-                                                  const int64_t* __restrict__ tau_src, int64_t* __restrict__ tau_dst) {
+                                                  const int64_t* __restrict__ tau_src, int64_t* __restrict__ tau_dst,
+                                                  uint32_t* sig) {
 #pragma clang fp contract(off)
   WGLOG(10);
   const int t = blockIdx.x * 256 + threadIdx.x;
   if (t == 0 && tau_dst) *tau_dst = *tau_src;
+  // the engine's "previous rollout complete" sequence (it precedes this kernel on the stream), in
+  // place of a stream write-value operation: one system-scope atomic, no extra kernel
+  if (t == 0 && sig) (void)__hip_atomic_fetch_add(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (t < C1_K * 64 * 8) {                                   // (kh, lane, j): conv1 split
     uint16_t* w1s = (uint16_t*)prep;
     const int ks = t >> 9, lane = (t >> 3) & 63, j = t & 7;     // ks = 2 cin + h2
@@ -107,10 +111,10 @@ __global__ void __launch_bounds__(256) k_prep_fwd(const float* __restrict__ W1, 
 }
 
 int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s, const int64_t* tau_src,
-                        int64_t* tau_dst) {
+                        int64_t* tau_dst, uint32_t* sig) {
   const int total = C1_K * 64 * 8 + (FC / 16) * FC_CH * 64 + W2F_ELEMS;
   hipLaunchKernelGGL(k_prep_fwd, dim3((total + 255) / 256), dim3(256), 0, s, P + L.off[T_L1W], P + L.off[T_FCW],
-                     P + L.off[T_L2W], prep, tau_src, tau_src ? tau_dst : nullptr);
+                     P + L.off[T_L2W], prep, tau_src, tau_src ? tau_dst : nullptr, sig);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
