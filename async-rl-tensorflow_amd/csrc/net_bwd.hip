@@ -840,6 +840,7 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
 
 static bool xcd_gemm();   // (below, beside the other mode knobs)
 static bool dwfc_late_knob();
+static bool bwd_bound_knob();
 int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
                         const float* act_l1, const float* act_l2, const float* act_l3,
                         const float* z, const int32_t* actions, const float* target, float beta,
@@ -910,12 +911,13 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     if (a3c_shared_gpu()) gh.max_wgs = gf.max_wgs = gd.max_wgs = env_wgs;
   }
   int rc;
-  // sync mode: the three GEMMs in one launch (3.32M -> 3.41M env-steps/s); overlapped with the
-  // next rollout the 1,420-workgroup launch slows it more than it gains (4.40M -> 4.30M), and so
-  // do the folds moved behind the conv backward alone (A3C_FOLD_LATE: 4.36M -> 3.73M)
+  // sync mode: the three GEMMs in one launch (3.32M -> 3.41M env-steps/s), and so where the
+  // overlapped backward bounds the iteration (M2: 5.17-5.22M -> 5.38-5.39M); beside a rollout
+  // that bounds it the 1,420-workgroup launch slows it more than it gains (M1: 4.62M -> 4.45M),
+  // and so do the folds moved behind the conv backward alone (A3C_FOLD_LATE: 4.62M -> 4.45M)
   static const int env_multi = getenv("A3C_GEMM_MULTI") ? atoi(getenv("A3C_GEMM_MULTI")) : -1;
   static const int env_late = getenv("A3C_FOLD_LATE") ? atoi(getenv("A3C_FOLD_LATE")) : -1;
-  const bool multi = env_multi >= 0 ? env_multi != 0 : !a3c_shared_gpu();
+  const bool multi = env_multi >= 0 ? env_multi != 0 : !a3c_shared_gpu() || bwd_bound_knob();
   const bool late = env_late >= 0 ? env_late != 0 : multi;
   if (!fork && (multi || late)) {
     // the weight-gradient split-K folds go after the conv backward (only the clip / apply read
@@ -1022,9 +1024,9 @@ static thread_local bool t_shared_gpu = false;
 bool a3c_shared_gpu() { return t_shared_gpu; }
 void a3c_set_shared_gpu(bool v) { t_shared_gpu = v; }
 // set by the engine where the backward stream, not the rollout, bounds the overlapped iteration
-// (mode M2, several GPUs): there the compact conv backward takes its LDS-lean form, the fc
-// GEMMs their XCD-grouped tile order and the fc weight GEMM runs behind the conv backward;
-// A3C_CB_LEAN, A3C_GEMM_XCD and A3C_DWFC_LATE (0/1) override each
+// (mode M2, several GPUs): there the compact conv backward takes its LDS-lean form and the three
+// weight/input GEMMs run as one launch with their folds behind the conv backward (as in sync
+// mode); A3C_CB_LEAN, A3C_GEMM_MULTI, A3C_GEMM_XCD and A3C_DWFC_LATE (0/1) override the choices
 static thread_local bool t_bwd_bound = false;
 static int env_knob(const char* name) { return getenv(name) ? atoi(getenv(name)) : -1; }
 bool a3c_lean_cbwd() {
@@ -1040,6 +1042,7 @@ static bool dwfc_late_knob() {
   static const int env = env_knob("A3C_DWFC_LATE");
   return env >= 0 ? env != 0 : t_bwd_bound;
 }
+static bool bwd_bound_knob() { return t_bwd_bound; }
 void a3c_set_bwd_bound(bool v) { t_bwd_bound = v; }
 
 int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,
