@@ -538,14 +538,7 @@ static int enqueue_rollout_begin(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
   // params are fixed for the rollout; overlap: the prep kernel also snapshots tau for the slot's
   // backward (sync: the slot's tau is the live counter)
-#ifdef A3C_ABL_PREP
-  static int abl_prep_n = 0;   // measurement only: no forward-weight prep after the first rollouts
-  int rc = 0;
-  if (abl_prep_n++ < 4)
-#else
-  int rc =
-#endif
-  rc = a3c_prep_fwd_launch(e->L, sl.P, sl.prep, s, e->overlap ? e->counters : nullptr,
+  int rc = a3c_prep_fwd_launch(e->L, sl.P, sl.prep, s, e->overlap ? e->counters : nullptr,
                            e->overlap ? sl.tau : nullptr, kernel_go(e) ? e->xflags + 1 : nullptr);
   if (rc) return rc;
   if (e->L.lstm) {
