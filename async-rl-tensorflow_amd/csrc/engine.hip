@@ -517,16 +517,18 @@ static const Slot& prev_slot(const a3c_engine* e, const Slot& sl) {
   return e->nslot == 2 ? e->slot[&sl == &e->slot[0] ? 1 : 0] : sl;
 }
 
-// "rollout k done", the go of its backward (rollout_grad): written on the rollout stream right
-// behind rollout k when the backward bounds the iteration; otherwise at the start of rollout
-// k+1, behind its wait for the apply it needs -- then the backward of k starts with rollout k+1
+// "rollout k done", the go of its backward (rollout_grad): on one GPU at the start of rollout
+// k+1, behind its wait for the apply it needs -- the backward of k then starts with rollout k+1
 // instead of ~10 us ahead of it, where its GEMMs slowed rollout k+1's first steps (DESIGN §6;
-// M1 4.42-4.53M -> 4.56-4.57M, M2 4.75-4.82M -> 4.50M if used there), and rollout k+1's prep
-// kernel bumps the sequence itself (kernel_go: no write-value operation on the rollout stream)
+// M1 4.42-4.53M -> 4.56-4.57M), and rollout k+1's prep kernel bumps the sequence itself
+// (kernel_go: no write-value operation on the rollout stream); with an exchange, right behind
+// rollout k on the rollout stream
 static bool bwd_bound(const a3c_engine* e);
 static bool late_go(const a3c_engine* e) {
   static const int env = getenv("A3C_LATE_GO") ? atoi(getenv("A3C_LATE_GO")) : -1;   // A/B override
-  return env >= 0 ? env != 0 : !bwd_bound(e);
+  // one GPU: M1 and M2 (M2 5.77M -> 5.83M since the conv backward runs one workgroup per CU);
+  // with an exchange the caller stream carries it behind the backward: right behind the rollout
+  return env >= 0 ? env != 0 : e->cfg.world_size == 1;
 }
 static bool kernel_go(const a3c_engine* e) {
   static const int env = getenv("A3C_KERNEL_GO") ? atoi(getenv("A3C_KERNEL_GO")) : 1;   // A/B override
@@ -725,10 +727,10 @@ static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
 static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s);
 // Overlapped runs where the backward stream, not the rollout, bounds the iteration: mode M2 (a
 // shorter rollout) and several GPUs (the exchange -- all-to-all, sharded apply, all-gather -- runs on
-// the backward's stream).  There the compact conv backward takes its LDS-lean form (M2: 4.56M ->
-// 4.66-4.76M env-steps/s), the fc GEMMs their XCD-grouped tile order (4.77-4.83M -> 4.87-4.88M)
-// and the backward starts right behind the rollout it consumes (rollout_grad); in mode M1 the
-// rollout bounds it and each of these costs the rollout more than it saves the backward.
+// the backward's stream).  There the three backward GEMMs run as one launch with their folds
+// behind the conv backward (M2 5.17-5.22M -> 5.36-5.40M env-steps/s); in mode M1 the rollout
+// co-bounds it and the single 1,420-workgroup launch costs the rollout more than it saves
+// (net_bwd.hip's knobs).
 static bool bwd_bound(const a3c_engine* e) {
   return e->overlap && (e->frame84 || e->cfg.world_size > 1);
 }

@@ -225,11 +225,10 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
   uint8_t* l1st = smem + (DMA ? 2 : 1) * CB_X8;
   uint8_t* dl2st = l1st + (DMA ? CB_L1ST : 0);
   float* l1s = (float*)(dl2st + (DMA ? CB_DL2ST : 0));
-  // LX: the LDS-lean layout (above).  The 8-wave kernels always take it; the compact 4-wave kernel
-  // that runs beside the rollout only where the backward is the critical path (a3c_lean_cbwd):
-  // in mode M1 every faster form of it measured slower overlapped (4.45-4.48M vs 4.56M
-  // env-steps/s), the rollout then being the critical path and slower beside the denser
-  // backward; in mode M2 (pre-sized frames, a shorter rollout) it gains 4.56M -> 4.75-4.82M
+  // LX: the LDS-lean layout (above).  The 8-wave kernels always take it, the compact 4-wave one
+  // that runs beside the rollout by default (a3c_lean_cbwd): with 183 workgroups it lost in mode M1
+  // (4.45-4.48M vs 4.56M env-steps/s) and won in M2; with one workgroup per CU on all 256 CUs
+  // (CB_SMEM_SOLO) it wins in both (M1 4.64M -> 4.67M)
   constexpr int L1LD = cb_l1_ld(LX);
   float* dl2s = (float*)((uint8_t*)l1s + cb_l1_bytes(LX));
   uint16_t* dlb = (uint16_t*)l1s;                                    // dl1 terms after phase (b)
@@ -810,7 +809,9 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   // n*E = 1280) 4.37M env-steps/s vs 4.29M for 224 (214 x 6), 4.14M for 160 (160 x 8), 4.00M for 256.
   // The slab workspace is sized for the larger count, so the plan's offsets do not depend on the mode.
   static const int env_nwg = getenv("A3C_CB_NWG") ? atoi(getenv("A3C_CB_NWG")) : 0;
-  const int nwg_shared = env_nwg ? env_nwg : 192, nwg_own = env_nwg ? env_nwg : 256;
+  // Round 3, with one compact workgroup per CU guaranteed (CB_SMEM_SOLO): 256 (5 samples each at
+  // n*E = 1280) -- M2 5.36M -> 5.77M, M1 4.62M -> 4.66M against 183 x 7 (214 x 6: 5.71M / 4.65M)
+  const int nwg_shared = env_nwg ? env_nwg : 256, nwg_own = env_nwg ? env_nwg : 256;
   auto count = [&](int nwg_max, int& per) {
     int nwg = (int)(B < nwg_max ? B : nwg_max);
     if (nwg < 1) nwg = 1;
@@ -1024,14 +1025,14 @@ static thread_local bool t_shared_gpu = false;
 bool a3c_shared_gpu() { return t_shared_gpu; }
 void a3c_set_shared_gpu(bool v) { t_shared_gpu = v; }
 // set by the engine where the backward stream, not the rollout, bounds the overlapped iteration
-// (mode M2, several GPUs): there the compact conv backward takes its LDS-lean form and the three
-// weight/input GEMMs run as one launch with their folds behind the conv backward (as in sync
-// mode); A3C_CB_LEAN, A3C_GEMM_MULTI, A3C_GEMM_XCD and A3C_DWFC_LATE (0/1) override the choices
+// (mode M2, several GPUs): there the three weight/input GEMMs run as one launch with their folds
+// behind the conv backward (as in sync mode); A3C_CB_LEAN, A3C_GEMM_MULTI, A3C_GEMM_XCD and
+// A3C_DWFC_LATE (0/1) override the choices
 static thread_local bool t_bwd_bound = false;
 static int env_knob(const char* name) { return getenv(name) ? atoi(getenv(name)) : -1; }
-bool a3c_lean_cbwd() {
+bool a3c_lean_cbwd() {   // (every overlap mode since the 256-workgroup plan: M1 4.63M -> 4.66M)
   static const int env = env_knob("A3C_CB_LEAN");
-  return env >= 0 ? env != 0 : t_bwd_bound;
+  return env >= 0 ? env != 0 : true;
 }
 static bool xcd_gemm() {
   static const int env = env_knob("A3C_GEMM_XCD");

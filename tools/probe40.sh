@@ -1,0 +1,8 @@
+set -o pipefail
+bash tools/gpu_tests.sh > /dev/null 2>&1; rc=$?; tail -3 gpurun_out/tests/pytest.log; [ $rc -ne 0 ] && { grep -B5 -A30 "FAILED\|Error" gpurun_out/tests/pytest.log | head -80; exit 1; }
+echo "### M1"
+AB_MODES=overlap AB_REPS=2 timeout -k 10 900 bash tools/ab.sh "A3C_X=new" "A3C_CB_LEAN=1" "A3C_LATE_GO=0" 2>&1 | grep -v amdgpu.ids || exit 1
+echo "### M2"
+AB_MODES=overlap AB_REPS=2 AB_ARGS=--frames84 timeout -k 10 900 bash tools/ab.sh "A3C_X=new" "A3C_CB_LEAN=0" "A3C_LATE_GO=1" "A3C_GEMM_MULTI=0" 2>&1 | grep -v amdgpu.ids || exit 1
+echo "### sync"
+AB_MODES=sync AB_REPS=1 timeout -k 10 900 bash tools/ab.sh "A3C_X=new" 2>&1 | grep -v amdgpu.ids || exit 1
