@@ -507,8 +507,10 @@ static OptParams opt_params(const a3c_engine* e, const Slot& sl) {
 static int enqueue_rollout_impl(a3c_engine* e, const Slot& sl, hipStream_t s);
 static int enqueue_rollout(a3c_engine* e, const Slot& sl, hipStream_t s) {
   a3c_set_shared_gpu(e->overlap != 0);
+  a3c_set_fcp_split(e->frame84 ? 2 : 4);
   int rc = enqueue_rollout_impl(e, sl, s);
   a3c_set_shared_gpu(false);
+  a3c_set_fcp_split(2);
   return rc;
 }
 
@@ -1476,7 +1478,10 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
   if (e->rs) A3C_CHECK(hipStreamSynchronize(e->rs));
   a3c_set_shared_gpu(e->overlap != 0);      // time the variants the engine runs
   a3c_set_bwd_bound(bwd_bound(e));
-  struct ResetShared { ~ResetShared() { a3c_set_shared_gpu(false); a3c_set_bwd_bound(false); } } reset_shared;
+  a3c_set_fcp_split(e->frame84 ? 2 : 4);
+  struct ResetShared {
+    ~ResetShared() { a3c_set_shared_gpu(false); a3c_set_bwd_bound(false); a3c_set_fcp_split(2); }
+  } reset_shared;
   if (kernel == A3C_KER_CONV12_FWD || kernel == A3C_KER_FC_FWD || kernel == A3C_KER_HEAD_SCREEN_CONV12) {
     int rc0 = a3c_prep_fwd_launch(L, e->params, sl.prep, s);
     if (rc0) return rc0;

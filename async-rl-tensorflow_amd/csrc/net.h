@@ -161,6 +161,8 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
                        const Conv12Next* next = nullptr, float* fc_part = nullptr);
 // fc layer as FC_NS K-slice partials part[x][M][FC] (folded by k_head_screen_conv12's head)
 int a3c_fc_part_launch(const float* A, const float* Wp, float* part, int64_t M, hipStream_t s);
+int a3c_fcp_split();
+void a3c_set_fcp_split(int ks);
 // tau_src / tau_dst (nullable): *tau_dst = *tau_src as well (the overlap rollout's tau snapshot);
 // sig (nullable): *sig += 1 (a system-scope atomic: the engine's rollout sequence)
 int a3c_prep_fwd_launch(const NetLayout& L, const float* P, uint8_t* prep, hipStream_t s,

@@ -1209,41 +1209,52 @@ __global__ void __launch_bounds__(64 * NW) k_fc_fwd(const float* __restrict__ A,
 #define FCP_SMEM (FCP_RB * FCP_LD * 4)          // 43520
 __device__ inline int fcp_c0(int x) { return (FC_CH * x) / FC_NS; }
 
-__global__ void __launch_bounds__(256) k_fc_part(const float* __restrict__ A, const float* __restrict__ Wp,
-                                                 float* __restrict__ part, int M) {
+// KS > 1: each of the 4 column tiles is split over KS waves by K ranges (chunk ranges of equal
+// length), so each wave's serial MFMA chain is KS times shorter; the waves of ranges 1..KS-1 hand
+// their sums to range 0's wave through LDS, which adds them in range order and stores.  KS = 2:
+// two waves per SIMD at 75 VGPRs, KS = 4: four at <= 64 VGPRs -- beside a compact conv backward
+// workgroup either way.  Measured (M1 / M2 env-steps/s): KS 1 4.67M / 5.82M, KS 2 4.78M / 6.07M.
+template <int KS>
+__global__ void __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(KS == 4 ? 8 : 1)))
+k_fc_part(const float* __restrict__ A, const float* __restrict__ Wp, float* __restrict__ part, int M) {
   WGLOG(2);
   __shared__ __attribute__((aligned(16))) float as[FCP_RB * FCP_LD];
+  constexpr int NT = 256 * KS;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i16 = lane & 15, j4 = lane >> 4;
   const int id = blockIdx.x;
   const int x = id % FC_NS, k = id / FC_NS;
   const int rb = k / (FC / FCP_CB), cb = k % (FC / FCP_CB);
   const int c0 = fcp_c0(x), c1 = fcp_c0(x + 1), nch = c1 - c0;
-  const int m0 = rb * FCP_RB, ct = cb * (FCP_CB / 16) + wid;
+  const int m0 = rb * FCP_RB, ct = cb * (FCP_CB / 16) + (wid & 3);
+  // this wave's K range
+  const int kr = wid >> 2;
+  const int kc0 = (nch * kr) / KS, kc1 = (nch * (kr + 1)) / KS;
+  const int kn = kc1 - kc0;
   // this wave's packed-W chunks (16-byte fragments, 4 MFMAs each), the first D in flight before
-  // the A tile is staged.  D = 8 keeps the kernel at 96 VGPRs: all 21 in flight (152 VGPRs) is
-  // faster alone (6.8 vs 7.4 us) and loses overlapped (3.83M vs 4.09M env-steps/s)
+  // the A tile is staged.  D = 8 keeps the 4-wave kernel at 96 VGPRs: all 21 in flight (152
+  // VGPRs) is faster alone (6.8 vs 7.4 us) and loses overlapped (3.83M vs 4.09M env-steps/s)
 #ifndef FCP_D
 #define FCP_D 8
 #endif
-  constexpr int D = FCP_D;
-  const f32x4* bp = (const f32x4*)Wp + ((int64_t)ct * FC_CH + c0) * 64 + lane;
+  constexpr int D = KS == 4 ? 4 : FCP_D;
+  const f32x4* bp = (const f32x4*)Wp + ((int64_t)ct * FC_CH + c0 + kc0) * 64 + lane;
   f32x4 rb4[D];
 #pragma unroll
-  for (int d = 0; d < D; ++d) rb4[d] = bp[(int64_t)min(d, nch - 1) * 64];
+  for (int d = 0; d < D; ++d) rb4[d] = bp[(int64_t)min(d, kn - 1) * 64];
   // A tile: 32 rows x nch chunks of 16 floats, f32x4 per thread-iteration, all loads issued first
-  constexpr int NA = (FCP_RB * FCP_MAXCH * 4 + 255) / 256;   // 11
+  constexpr int NA = (FCP_RB * FCP_MAXCH * 4 + NT - 1) / NT;   // 11, 6, 3
   f32x4 ra[NA];
   const int q4 = nch * 4;                                    // f32x4 per row
 #pragma unroll
   for (int u = 0; u < NA; ++u) {
-    const int i = min((int)threadIdx.x + 256 * u, FCP_RB * q4 - 1);
+    const int i = min((int)threadIdx.x + NT * u, FCP_RB * q4 - 1);
     const int r = i / q4, q = i - r * q4;
     ra[u] = *(const f32x4*)(A + (int64_t)min(m0 + r, M - 1) * FLAT + 16 * c0 + 4 * q);
   }
 #pragma unroll
   for (int u = 0; u < NA; ++u) {
-    const int i = (int)threadIdx.x + 256 * u;
+    const int i = (int)threadIdx.x + NT * u;
     if (i < FCP_RB * q4) {
       const int r = i / q4, q = i - r * q4;
       *(f32x4*)(as + r * FCP_LD + 4 * q) = ra[u];
@@ -1251,12 +1262,12 @@ __global__ void __launch_bounds__(256) k_fc_part(const float* __restrict__ A, co
   }
   __syncthreads();
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};   // row tiles 0 / 1
-  const float* a0 = as + i16 * FCP_LD + 4 * j4;
+  const float* a0 = as + i16 * FCP_LD + 4 * j4 + 16 * kc0;
   const float* a1 = a0 + 16 * FCP_LD;
-  for (int c = 0; c < nch; c += D) {
+  for (int c = 0; c < kn; c += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      if (c + d < nch) {
+      if (c + d < kn) {
         const f32x4 x0 = *(const f32x4*)(a0 + 16 * (c + d));
         const f32x4 x1 = *(const f32x4*)(a1 + 16 * (c + d));
 #pragma unroll
@@ -1265,8 +1276,23 @@ __global__ void __launch_bounds__(256) k_fc_part(const float* __restrict__ A, co
           acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[c4], rb4[d][c4], acc1, 0, 0, 0);
         }
         const int cn = c + d + D;
-        if (cn < nch) rb4[d] = bp[(int64_t)cn * 64];
+        if (cn < kn) rb4[d] = bp[(int64_t)cn * 64];
       }
+    }
+  }
+  if constexpr (KS > 1) {   // ranges 1.. -> LDS (the A tile is no longer read) -> range 0 adds in order
+    __syncthreads();
+    f32x4* xs = (f32x4*)as;
+    if (kr) {
+      xs[(((kr - 1) * 4 + (wid & 3)) * 2 + 0) * 64 + lane] = acc0;
+      xs[(((kr - 1) * 4 + (wid & 3)) * 2 + 1) * 64 + lane] = acc1;
+    }
+    __syncthreads();
+    if (kr) return;
+#pragma unroll
+    for (int q = 0; q < KS - 1; ++q) {
+      acc0 += xs[((q * 4 + (wid & 3)) * 2 + 0) * 64 + lane];
+      acc1 += xs[((q * 4 + (wid & 3)) * 2 + 1) * 64 + lane];
     }
   }
   // partial tile rows m0 + 16 rt + 4 j4 + r, column 16 ct + i16
@@ -1279,10 +1305,21 @@ __global__ void __launch_bounds__(256) k_fc_part(const float* __restrict__ A, co
   }
 }
 
+// K splits of the partial fc, set by the engine per frame mode (a3c_set_fcp_split; A3C_FCP_KS
+// overrides): M1 4 (4.72-4.75M -> 4.76-4.81M env-steps/s against 2), M2 2 (6.02-6.03M vs 5.99-6.00M)
+static thread_local int t_fcp_split = 2;
+int a3c_fcp_split() { return t_fcp_split; }
+void a3c_set_fcp_split(int ks) { t_fcp_split = ks; }
+
 int a3c_fc_part_launch(const float* A, const float* Wp, float* part, int64_t M, hipStream_t s) {
   if (M <= 0) return 0;
   const int nrb = (int)((M + FCP_RB - 1) / FCP_RB);
-  hipLaunchKernelGGL(k_fc_part, dim3((unsigned)(FC_NS * nrb * (FC / FCP_CB))), dim3(256), 0, s, A, Wp, part, (int)M);
+  static const int env_ks = getenv("A3C_FCP_KS") ? atoi(getenv("A3C_FCP_KS")) : 0;
+  const int ks = env_ks ? env_ks : a3c_fcp_split();
+  const dim3 grid((unsigned)(FC_NS * nrb * (FC / FCP_CB)));
+  if (ks == 4) hipLaunchKernelGGL(k_fc_part<4>, grid, dim3(1024), 0, s, A, Wp, part, (int)M);
+  else if (ks == 2) hipLaunchKernelGGL(k_fc_part<2>, grid, dim3(512), 0, s, A, Wp, part, (int)M);
+  else hipLaunchKernelGGL(k_fc_part<1>, grid, dim3(256), 0, s, A, Wp, part, (int)M);
   A3C_CHECK(hipGetLastError());
   return 0;
 }

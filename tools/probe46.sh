@@ -1,0 +1,6 @@
+set -o pipefail
+A3C_FCP_WAVES=8 bash tools/gpu_tests.sh > /dev/null 2>&1; rc=$?; tail -3 gpurun_out/tests/pytest.log; [ $rc -ne 0 ] && { grep -B5 -A30 "FAILED\|Error" gpurun_out/tests/pytest.log | head -80; exit 1; }
+echo "### M1: 8-wave partial fc"
+AB_MODES=overlap AB_REPS=3 AB_KT=k_fc_part timeout -k 10 900 bash tools/ab.sh "A3C_FCP_WAVES=4" "A3C_FCP_WAVES=8" 2>&1 | grep -v amdgpu.ids || exit 1
+echo "### M2"
+AB_MODES=overlap AB_REPS=2 AB_ARGS=--frames84 timeout -k 10 900 bash tools/ab.sh "A3C_FCP_WAVES=4" "A3C_FCP_WAVES=8" 2>&1 | grep -v amdgpu.ids || exit 1
