@@ -1237,7 +1237,10 @@ k_fc_part(const float* __restrict__ A, const float* __restrict__ Wp, float* __re
 #ifndef FCP_D
 #define FCP_D 8
 #endif
-  constexpr int D = KS == 4 ? 4 : FCP_D;
+#ifndef FCP_D4
+#define FCP_D4 4
+#endif
+  constexpr int D = KS == 4 ? FCP_D4 : FCP_D;
   const f32x4* bp = (const f32x4*)Wp + ((int64_t)ct * FC_CH + c0 + kc0) * 64 + lane;
   f32x4 rb4[D];
 #pragma unroll
