@@ -110,6 +110,108 @@ __device__ inline void gemm_tile(const GemmArgs& g, int bx, int by, int bz, floa
   if (do_colsum && tid < BN && n0 + tid < g.N) g.colsum[(int64_t)ks * g.N + n0 + tid] = csum;
 }
 
+// 128x128 tile of C = A B over all of K (nsplit 1): 4 waves (2 x 2), each a 64x64 block as 2 x 2
+// v_mfma_f32_32x32x2f32 tiles; operands LDS-staged BK = 16 deep with a register prefetch of the
+// next K step, two f32x4 of A and two of B per thread.  The same products as k_gemm_f32 summed in
+// the same K order per output, so the result is bit-identical.
+template <bool A_KC, bool B_NC>
+__global__ void __launch_bounds__(256) k_gemm_f32_big(GemmArgs g) {
+  WGLOG(5);
+  constexpr int TM = 128, TN = 128;
+  __shared__ __attribute__((aligned(16))) float As[BK][TM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[BK][TN + PAD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
+  const int kend = g.K;
+  // per-thread load coordinates of element u = 0, 1
+  auto a_rc = [&](int u, int& r, int& c) {
+    if (A_KC) { r = (tid >> 2) + 64 * u; c = (tid & 3) * 4; }   // row m, k quad
+    else      { r = (tid >> 5) + 8 * u; c = (tid & 31) * 4; }   // row k, m quad
+  };
+  auto b_rc = [&](int u, int& r, int& c) {
+    if (B_NC) { r = (tid >> 5) + 8 * u; c = (tid & 31) * 4; }   // row k, n quad
+    else      { r = (tid >> 2) + 64 * u; c = (tid & 3) * 4; }   // row n, k quad
+  };
+  auto load_a = [&](int k0, int u) -> f32x4 {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    int r, c;
+    a_rc(u, r, c);
+    if (A_KC) {
+      const int m = m0 + r, k = k0 + c;
+      if (m < g.M && k < kend) v = *(const f32x4*)(g.A + (int64_t)m * g.lda + k);
+    } else {
+      const int k = k0 + r, m = m0 + c;
+      if (k < kend && m < g.M) v = *(const f32x4*)(g.A + (int64_t)k * g.lda + m);
+    }
+    return v;
+  };
+  auto load_b = [&](int k0, int u) -> f32x4 {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    int r, c;
+    b_rc(u, r, c);
+    if (B_NC) {
+      const int k = k0 + r, n = n0 + c;
+      if (k < kend && n < g.N) v = *(const f32x4*)(g.B + (int64_t)k * g.ldb + n);
+    } else {
+      const int n = n0 + r, k = k0 + c;
+      if (n < g.N && k < kend) v = *(const f32x4*)(g.B + (int64_t)n * g.ldb + k);
+    }
+    return v;
+  };
+  auto store_a = [&](f32x4 v, int u) {
+    int r, c;
+    a_rc(u, r, c);
+    if (A_KC) { As[c][r] = v[0]; As[c + 1][r] = v[1]; As[c + 2][r] = v[2]; As[c + 3][r] = v[3]; }
+    else      { *(f32x4*)&As[r][c] = v; }
+  };
+  auto store_b = [&](f32x4 v, int u) {
+    int r, c;
+    b_rc(u, r, c);
+    if (B_NC) { *(f32x4*)&Bs[r][c] = v; }
+    else      { Bs[c][r] = v[0]; Bs[c + 1][r] = v[1]; Bs[c + 2][r] = v[2]; Bs[c + 3][r] = v[3]; }
+  };
+  f32x16 acc[2][2] = {};
+  f32x4 ra0 = load_a(0, 0), ra1 = load_a(0, 1), rb0 = load_b(0, 0), rb1 = load_b(0, 1);
+  for (int k0 = 0; k0 < kend; k0 += BK) {
+    __syncthreads();
+    store_a(ra0, 0); store_a(ra1, 1);
+    store_b(rb0, 0); store_b(rb1, 1);
+    __syncthreads();
+    if (k0 + BK < kend) {
+      ra0 = load_a(k0 + BK, 0); ra1 = load_a(k0 + BK, 1);
+      rb0 = load_b(k0 + BK, 0); rb1 = load_b(k0 + BK, 1);
+    }
+    const int kh = lane >> 5, c = lane & 31;
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      const float a0 = As[2 * kk + kh][wm * 64 + c], a1 = As[2 * kk + kh][wm * 64 + 32 + c];
+      const float b0 = Bs[2 * kk + kh][wn * 64 + c], b1 = Bs[2 * kk + kh][wn * 64 + 32 + c];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 64 + 32 * j + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < g.M && col < g.N) {
+          float v = acc[i][j][r];
+          if (g.epi == EPI_BIAS_RELU) v = fmaxf(v + g.bias[col], 0.f);
+          else if (g.epi == EPI_BIAS) v = v + g.bias[col];
+          else if (g.epi == EPI_MASK) v = g.mask[(int64_t)row * g.ldm + col] > 0.f ? v : 0.f;
+          g.C[(int64_t)row * g.ldc + col] = v;
+        }
+      }
+    }
+}
+
 // tile number id of g's (N tiles, M tiles, K-chunks) grid, N fastest (as k_gemm_f32's blockIdx)
 template <bool A_KC, bool B_NC>
 __device__ inline void gemm_tile_id(const GemmArgs& g, int id, float (&As)[BK][BM + PAD], float (&Bs)[BK][BN + PAD]) {
@@ -264,6 +366,15 @@ int a3c_gemm(bool a_kc, bool b_nc, GemmArgs g, hipStream_t s) {
   // iteration): it halves the backward GEMMs' HBM bytes, 124 -> 73 MB per iteration (profile
   // r3v1), but beside a rollout that bounds the iteration it costs 4.56M -> 4.05M env-steps/s
   const int nb = (int)(grid.x * grid.y * grid.z);
+  if (g.big && g.nsplit == 1 && !g.colsum) {
+    const dim3 gb((g.N + 127) / 128, (g.M + 127) / 128);
+    if (a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_big<true, true>), gb, dim3(256), 0, s, g);
+    else if (a_kc && !b_nc) hipLaunchKernelGGL((k_gemm_f32_big<true, false>), gb, dim3(256), 0, s, g);
+    else if (!a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_big<false, true>), gb, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((k_gemm_f32_big<false, false>), gb, dim3(256), 0, s, g);
+    A3C_CHECK(hipGetLastError());
+    return 0;
+  }
   if (g.xcd) {
     const int G = g.xcd == 1 ? (int)(grid.y * grid.z) : (int)(grid.x * grid.z);
     const int J = g.xcd == 1 ? (int)grid.x : (int)grid.y;
