@@ -29,8 +29,8 @@ struct GemmArgs {
   // a3c_gemm: at most this many workgroups (0 = one per tile), each looping over tiles id, id +
   // grid, ... -- fewer GEMM workgroups resident beside a concurrent kernel.  Speed only.
   int max_wgs;
-  // a3c_gemm, nsplit 1 only: 128x128 tiles (k_gemm_f32_big: a quarter of the workgroups, each four
-  // times the work) -- fewer workgroups resident beside a concurrent kernel.  Speed only.
+  // a3c_gemm: 128x128 tiles (k_gemm_f32_big: a quarter of the workgroups, each four times the
+  // work) -- fewer workgroups resident beside a concurrent kernel.  Speed only (bit-identical).
   int big;
 };
 

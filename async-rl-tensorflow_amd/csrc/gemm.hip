@@ -110,10 +110,11 @@ __device__ inline void gemm_tile(const GemmArgs& g, int bx, int by, int bz, floa
   if (do_colsum && tid < BN && n0 + tid < g.N) g.colsum[(int64_t)ks * g.N + n0 + tid] = csum;
 }
 
-// 128x128 tile of C = A B over all of K (nsplit 1): 4 waves (2 x 2), each a 64x64 block as 2 x 2
+// 128x128 tile of C = A B over K-chunk blockIdx.z: 4 waves (2 x 2), each a 64x64 block as 2 x 2
 // v_mfma_f32_32x32x2f32 tiles; operands LDS-staged BK = 16 deep with a register prefetch of the
-// next K step, two f32x4 of A and two of B per thread.  The same products as k_gemm_f32 summed in
-// the same K order per output, so the result is bit-identical.
+// next K step, two f32x4 of A and two of B per thread; split-K partials to the slab and the
+// optional column sums of B as k_gemm_f32.  The same products as k_gemm_f32 summed in the same K
+// order per output, so the result is bit-identical.
 template <bool A_KC, bool B_NC>
 __global__ void __launch_bounds__(256) k_gemm_f32_big(GemmArgs g) {
   WGLOG(5);
@@ -123,7 +124,10 @@ __global__ void __launch_bounds__(256) k_gemm_f32_big(GemmArgs g) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
-  const int kend = g.K;
+  const int ks = blockIdx.z;
+  const int kbeg = ks * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  const bool do_colsum = g.colsum != nullptr && blockIdx.y == 0;
   // per-thread load coordinates of element u = 0, 1
   auto a_rc = [&](int u, int& r, int& c) {
     if (A_KC) { r = (tid >> 2) + 64 * u; c = (tid & 3) * 4; }   // row m, k quad
@@ -172,8 +176,9 @@ __global__ void __launch_bounds__(256) k_gemm_f32_big(GemmArgs g) {
     else      { Bs[c][r] = v[0]; Bs[c + 1][r] = v[1]; Bs[c + 2][r] = v[2]; Bs[c + 3][r] = v[3]; }
   };
   f32x16 acc[2][2] = {};
-  f32x4 ra0 = load_a(0, 0), ra1 = load_a(0, 1), rb0 = load_b(0, 0), rb1 = load_b(0, 1);
-  for (int k0 = 0; k0 < kend; k0 += BK) {
+  float csum = 0.f;
+  f32x4 ra0 = load_a(kbeg, 0), ra1 = load_a(kbeg, 1), rb0 = load_b(kbeg, 0), rb1 = load_b(kbeg, 1);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
     __syncthreads();
     store_a(ra0, 0); store_a(ra1, 1);
     store_b(rb0, 0); store_b(rb1, 1);
@@ -181,6 +186,10 @@ __global__ void __launch_bounds__(256) k_gemm_f32_big(GemmArgs g) {
     if (k0 + BK < kend) {
       ra0 = load_a(k0 + BK, 0); ra1 = load_a(k0 + BK, 1);
       rb0 = load_b(k0 + BK, 0); rb1 = load_b(k0 + BK, 1);
+    }
+    if (do_colsum && tid < TN) {
+#pragma unroll
+      for (int k = 0; k < BK; ++k) csum += Bs[k][tid];
     }
     const int kh = lane >> 5, c = lane & 31;
 #pragma unroll
@@ -201,8 +210,11 @@ __global__ void __launch_bounds__(256) k_gemm_f32_big(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row < g.M && col < g.N) {
-          float v = acc[i][j][r];
+        if (row >= g.M || col >= g.N) continue;
+        float v = acc[i][j][r];
+        if (g.nsplit > 1) {
+          g.slab[(int64_t)ks * g.M * g.N + (int64_t)row * g.N + col] = v;
+        } else {
           if (g.epi == EPI_BIAS_RELU) v = fmaxf(v + g.bias[col], 0.f);
           else if (g.epi == EPI_BIAS) v = v + g.bias[col];
           else if (g.epi == EPI_MASK) v = g.mask[(int64_t)row * g.ldm + col] > 0.f ? v : 0.f;
@@ -210,6 +222,7 @@ __global__ void __launch_bounds__(256) k_gemm_f32_big(GemmArgs g) {
         }
       }
     }
+  if (do_colsum && tid < TN && n0 + tid < g.N) g.colsum[(int64_t)ks * g.N + n0 + tid] = csum;
 }
 
 // tile number id of g's (N tiles, M tiles, K-chunks) grid, N fastest (as k_gemm_f32's blockIdx)
@@ -366,14 +379,14 @@ int a3c_gemm(bool a_kc, bool b_nc, GemmArgs g, hipStream_t s) {
   // iteration): it halves the backward GEMMs' HBM bytes, 124 -> 73 MB per iteration (profile
   // r3v1), but beside a rollout that bounds the iteration it costs 4.56M -> 4.05M env-steps/s
   const int nb = (int)(grid.x * grid.y * grid.z);
-  if (g.big && g.nsplit == 1 && !g.colsum) {
-    const dim3 gb((g.N + 127) / 128, (g.M + 127) / 128);
+  if (g.big) {
+    const dim3 gb((g.N + 127) / 128, (g.M + 127) / 128, g.nsplit);
     if (a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_big<true, true>), gb, dim3(256), 0, s, g);
     else if (a_kc && !b_nc) hipLaunchKernelGGL((k_gemm_f32_big<true, false>), gb, dim3(256), 0, s, g);
     else if (!a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_big<false, true>), gb, dim3(256), 0, s, g);
     else hipLaunchKernelGGL((k_gemm_f32_big<false, false>), gb, dim3(256), 0, s, g);
     A3C_CHECK(hipGetLastError());
-    return 0;
+    return g.defer_reduce ? 0 : a3c_gemm_reduce(g, s);
   }
   if (g.xcd) {
     const int G = g.xcd == 1 ? (int)(grid.y * grid.z) : (int)(grid.x * grid.z);

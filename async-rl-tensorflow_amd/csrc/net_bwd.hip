@@ -912,6 +912,8 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     // M1 4.79-4.81M -> 4.82-4.83M env-steps/s; bit-identical); A3C_GEMM_BIG=0 reverts
     static const int env_big = getenv("A3C_GEMM_BIG") ? atoi(getenv("A3C_GEMM_BIG")) : 1;
     gd.big = a3c_shared_gpu() && env_big != 0;
+    static const int env_bigf = getenv("A3C_GEMM_BIG_FC") ? atoi(getenv("A3C_GEMM_BIG_FC")) : 0;
+    gf.big = a3c_shared_gpu() && env_bigf != 0;
   }
   {
     static const int env_wgs = getenv("A3C_GEMM_WGS") ? atoi(getenv("A3C_GEMM_WGS")) : 0;
