@@ -1,0 +1,4 @@
+set -o pipefail
+bash tools/gpu_tests.sh > /dev/null 2>&1; rc=$?; tail -3 gpurun_out/tests/pytest.log; [ $rc -ne 0 ] && { grep -B5 -A30 "FAILED\|Error" gpurun_out/tests/pytest.log | head -80; exit 1; }
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" 2>&1 | grep -v amdgpu.ids | tail -2 || exit 1
+timeout -k 10 400 python3 bench.py > gpurun_out/final.json 2> gpurun_out/final.err && tail -c 600 gpurun_out/final.json
