@@ -908,9 +908,11 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   gd.epi = EPI_MASK; gd.mask = act_l2; gd.ldm = FLAT; gd.nsplit = 1;
   gd.xcd = xcd_gemm() ? 2 : 0;          // the 20 row tiles of a W strip on one XCD
   {
-    // overlap: 128x128 tiles (210 workgroups instead of 820 fill fewer CUs beside the rollout;
-    // M1 4.79-4.81M -> 4.82-4.83M env-steps/s; bit-identical); A3C_GEMM_BIG=0 reverts
-    static const int env_big = getenv("A3C_GEMM_BIG") ? atoi(getenv("A3C_GEMM_BIG")) : 1;
+    // overlap, A3C_GEMM_BIG=1: 128x128 tiles (210 workgroups instead of 820 beside the rollout;
+    // bit-identical).  Off: +0.5 % on one box (4.79-4.81M -> 4.82-4.83M), -0.8 % on another
+    // (4.80-4.83M -> 4.75-4.79M) -- the tile GEMM takes 62 us instead of ~35 and the caller
+    // stream's loop (go -> backward -> apply -> hop) then bounds M1 again (tools/wglog.py)
+    static const int env_big = getenv("A3C_GEMM_BIG") ? atoi(getenv("A3C_GEMM_BIG")) : 0;
     gd.big = a3c_shared_gpu() && env_big != 0;
     static const int env_bigf = getenv("A3C_GEMM_BIG_FC") ? atoi(getenv("A3C_GEMM_BIG_FC")) : 0;
     gf.big = a3c_shared_gpu() && env_bigf != 0;

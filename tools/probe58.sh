@@ -1,0 +1,4 @@
+set -o pipefail
+A3C_GEMM_BIG=2 bash tools/gpu_tests.sh > /dev/null 2>&1; rc=$?; tail -3 gpurun_out/tests/pytest.log; [ $rc -ne 0 ] && { grep -B5 -A30 "FAILED\|Error" gpurun_out/tests/pytest.log | head -80; exit 1; }
+echo "### M1: dl2 GEMM tiles: 64x64 / 128x128 4 waves / 128x128 8 waves"
+AB_MODES=overlap AB_REPS=3 timeout -k 10 900 bash tools/ab.sh "A3C_GEMM_BIG=0" "A3C_GEMM_BIG=1" "A3C_GEMM_BIG=2" 2>&1 | grep -v amdgpu.ids || exit 1
