@@ -20,5 +20,7 @@ out = dict(method=d['method'],
            source=f'profiles/{rnd}_{tag}_pmc_summary.json (tools/profile_round.sh {tag}: rocprofv3 --pmc FETCH_SIZE '
                   'and --pmc WRITE_SIZE passes of bench.py --steps 10, separate runs)',
            hbm_bytes_per_launch={k: round(v) for k, v in d['hbm_bytes_per_launch'].items()})
-json.dump(out, open(os.path.join(dst, 'pmc_hbm_bytes.json'), 'w'), indent=1)
+# an M2 round (tag ending in m2, bench.py --frames84) feeds the M2 bench line's roofline.traffic
+json.dump(out, open(os.path.join(dst, 'pmc_hbm_bytes_m2.json' if tag.endswith('m2') else 'pmc_hbm_bytes.json'), 'w'),
+          indent=1)
 print(json.dumps(out['hbm_bytes_per_launch'], indent=1))
