@@ -318,6 +318,7 @@ def main():
         dist.barrier()
     if rank == 0:
         steps_total = world * E * n * args.steps
+        coll = 'RCCL' if args.backend == 'nccl' else 'gloo, host-staged'
         line = {
             'metric': METRIC, 'value': round(steps_total / el, 1), 'unit': 'env-steps/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 4),
@@ -337,10 +338,10 @@ def main():
                        'parallelism': (f'dp{world} hogwild: unlocked RMSProp pushes into {world} IPC-mapped HBM '
                                        f'shards over xGMI, pull at rollout start, no collective'
                                        if args.update == 'hogwild' else
-                                       f'dp{world} partitioned PS: RCCL all-to-all of per-worker-clipped grads, '
-                                       f'{world} sequential RMSProp steps per owned shard, RCCL all-gather'
+                                       f'dp{world} partitioned PS: {coll} all-to-all of per-worker-clipped grads, '
+                                       f'{world} sequential RMSProp steps per owned shard, {coll} all-gather'
                                        if args.exchange == 'sequential' else
-                                       f'dp{world} all-reduce (RCCL) of per-worker-clipped grads, one summed step')
+                                       f'dp{world} all-reduce ({coll}) of per-worker-clipped grads, one summed step')
                        if world > 1 else 'dp1', 'hipgraph': args.graph and not args.no_graph,
                        'update': {'overlap': 'overlap: rollout k uses params after update k-2 (A3C stale-1 async), '
                                              'backward+apply of k-1 concurrent with rollout k',
