@@ -171,8 +171,12 @@ __global__ void __launch_bounds__(256) k_commit(const float* __restrict__ src, i
     if (snap) ((f32x4*)snap)[q] = v;
     if (tsync) ((f32x4*)target)[q] = v;
   }
+  // tau only when this pass owns it: in overlap mode (dtau 0) the concurrent rollout stream advances
+  // tau in its bootstrap head, and an unconditional `counters[0] += 0` here is a read-modify-write
+  // that can overwrite that advance (round 3's w4-breakout-overlap divergence: the lost advance
+  // shifted the rank's ring / Philox counters by n steps while the all-gather kept the ranks equal)
   if (blockIdx.x == 0 && threadIdx.x == 0 && counters) {
-    counters[0] += dtau;
+    if (dtau) counters[0] += dtau;
     counters[1] += dstep;
   }
 }
@@ -299,6 +303,20 @@ extern "C" int a3c_rmsprop_range(float* w, float* ms, float* mom, const float* g
 extern "C" int a3c_dev_alloc(int64_t bytes, void** out) {
   if (!out || bytes <= 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_dev_alloc", "bad argument");
   A3C_CHECK(hipMalloc(out, (size_t)bytes));
+  return 0;
+}
+
+// Hogwild shard memory (DESIGN §7 "memory model"): kind 0 coarse-grained (hipMalloc: coherent
+// only at kernel boundaries), 1 fine-grained (coherent at instruction granularity across devices:
+// a peer's RMW over xGMI and the owner's reads meet in memory, no stale L2 line on either side),
+// 2 uncached (every access goes to memory).  All three are VRAM and IPC-exportable.
+extern "C" int a3c_dev_alloc_kind(int64_t bytes, int kind, void** out) {
+  if (!out || bytes <= 0 || kind < 0 || kind > 2) return a3c_set_error(A3C_ERR_INVALID, "a3c_dev_alloc_kind", "bad argument");
+  if (kind == 0) {
+    A3C_CHECK(hipMalloc(out, (size_t)bytes));
+  } else {
+    A3C_CHECK(hipExtMallocWithFlags(out, (size_t)bytes, kind == 1 ? hipDeviceMallocFinegrained : hipDeviceMallocUncached));
+  }
   return 0;
 }
 

@@ -174,7 +174,8 @@ def run_engine(config, flags):
   ps = None
   if flags.update == 'hogwild':
     from src.hogwild import HogwildPS
-    ps = HogwildPS(eng.params, decay=config.decay, momentum=config.momentum, epsilon=config.epsilon)
+    ps = HogwildPS(eng.params, decay=config.decay, momentum=config.momentum, epsilon=config.epsilon,
+                   ms=eng.ms, mom=eng.mom)     # (restored slots, or the TF1 init after reset)
   # the reference's worker loop `for self.step in xrange(self.step, self.max_step)` (agent.py:46,55):
   # each worker -- here each env, all in lock-step -- takes env-steps up to max_step on its own
   # counter; one rollout is n of them, and the overlap pipeline applies one call later
@@ -214,10 +215,12 @@ def run_engine(config, flags):
         print(json.dumps(rec), flush=True)
         log.write(json.dumps(rec) + '\n')
       if _agree(rank == 0 and time.time() - last_save >= flags.save_model_secs, world):
+        _sync_slots(eng, xch, ps)
         C.save_engine(saver, eng, ns, rank, world, barrier=_barrier(world))
         last_save = time.time()
   torch.cuda.synchronize()
   if iterations > 0:
+    _sync_slots(eng, xch, ps)
     C.save_engine(saver, eng, ns, rank, world, barrier=_barrier(world))    # the final state
   if ps is not None:
     ps.close()
@@ -226,6 +229,14 @@ def run_engine(config, flags):
   if log:
     log.close()
   return eng
+
+
+def _sync_slots(eng, xch, ps):
+  """The RMSProp slots a sharded update keeps per owner (partitioned PS ranges, Hogwild shards)
+  into the engine's full ms / mom before a checkpoint."""
+  for x in (xch, ps):
+    if hasattr(x, 'sync_slots'):
+      x.sync_slots(eng)
 
 
 def _barrier(world):

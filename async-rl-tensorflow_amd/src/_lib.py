@@ -134,6 +134,7 @@ SIGNATURES = {
     'a3c_engine_ext_upload': (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     'a3c_hostenv_step_range': (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int]),
     'a3c_dev_alloc': (c_int, [c_i64, ctypes.POINTER(c_void_p)]),
+    'a3c_dev_alloc_kind': (c_int, [c_i64, c_int, ctypes.POINTER(c_void_p)]),
     'a3c_dev_free': (c_int, [c_void_p]),
     'a3c_ipc_handle': (c_int, [c_void_p, c_void_p]),
     'a3c_ipc_open': (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),

@@ -24,7 +24,7 @@ import torch
 from . import kernels as K
 from . import ops
 from . import checkpoint as C
-from .base import BaseModel, load_checkpoint, save_checkpoint
+from .base import BaseModel, copy_named, load_checkpoint, save_checkpoint
 from .distributed import GradExchange, gather_grads
 from .history import History
 from .utils import get_time
@@ -386,10 +386,9 @@ class Agent(BaseModel):
 
   def load(self, path):
     arrays, step = load_checkpoint(path)
-    dst = {C.tf_name(k, 'q'): v for k, v in self.w.items()}
-    dst.update({C.tf_target_name(k): v for k, v in self.t_w.items()})
-    for k, v in arrays.items():
-      if k in dst:
-        dst[k].copy_(torch.as_tensor(v).reshape(dst[k].shape))
+    # TF variable names; round-1/2 files used the raw dict names and 'target/<k>'
+    dst = {'w/' + k: (v, [C.tf_name(k, 'q'), k]) for k, v in self.w.items()}
+    dst.update({'t_w/' + k: (v, [C.tf_target_name(k), 'target/' + k]) for k, v in self.t_w.items()})
+    copy_named(arrays, dst, path)
     self.step_op = step
     return step

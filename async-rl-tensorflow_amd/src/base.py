@@ -71,6 +71,28 @@ def save_checkpoint(path, named_tensors, step):
   return path if path.endswith('.npz') else path + '.npz'
 
 
+def copy_named(arrays, targets, what):
+  """Copy checkpoint arrays into tensors.  targets: {destination tensor name: (tensor, [keys, ...])},
+  the keys tried in order (the TF variable name first, then the raw-dict / ``target/<k>`` names of
+  round-1/2 files).  Raises ValueError when no tensor matched (the file is not a checkpoint of
+  this model) and names the missing ones when only some matched.  Returns the number copied."""
+  import torch
+  found, missing = 0, []
+  for name, (dst, keys) in targets.items():
+    key = next((k for k in keys if k in arrays), None)
+    if key is None:
+      missing.append(name)
+      continue
+    dst.copy_(torch.as_tensor(arrays[key]).reshape(dst.shape))
+    found += 1
+  if not found:
+    raise ValueError('%s: the checkpoint holds none of the expected tensors (%s ...)' % (what, ', '.join(
+        k for _, ks in list(targets.values())[:2] for k in ks[:1])))
+  if missing:
+    print(' [!] %s: checkpoint lacks %s (kept as initialised)' % (what, ', '.join(missing)))
+  return found
+
+
 def load_checkpoint(path):
   with np.load(path, allow_pickle=False) as f:
     key = 'step' if 'step' in f.files else '__step__'     # (files of rounds 1-2)

@@ -36,6 +36,7 @@ import numpy as np
 
 STEP_KEY = 'step'
 STATE_KEY = '__engine_state__'
+WSTEP_KEY = '__worker_step__'
 
 _Q = {'l1_w': 'l1/w', 'l1_b': 'l1/biases', 'l2_w': 'l2/w', 'l2_b': 'l2/biases',
       'l3_w': 'l3/Matrix', 'l3_b': 'l3/bias', 'q_w': 'q/Matrix', 'q_b': 'q/bias',
@@ -87,11 +88,18 @@ class Saver(object):
         p = os.path.join(self.dir, '%s-%d' % (self.basename, int(step)))
         return p + ('.rank%d.npz' % rank if rank else '.npz')
 
+    def _resolve(self, p):
+        """Index entries are file names relative to the index's directory (as tf.train writes
+        them), so a run resumed from another working directory finds them; older indices held
+        paths as built from checkpoint_dir: every checkpoint lives in self.dir, so the base name
+        resolves both."""
+        return os.path.join(self.dir, os.path.basename(p))
+
     def kept(self):
         try:
             with open(self.index_path) as f:
-                return list(json.load(f)['all_model_checkpoint_paths'])
-        except (OSError, ValueError, KeyError):
+                return [self._resolve(p) for p in json.load(f)['all_model_checkpoint_paths']]
+        except (OSError, ValueError, KeyError, TypeError):
             return []
 
     def latest(self):
@@ -124,7 +132,8 @@ class Saver(object):
                     pass
         tmp = self.index_path + '.tmp'
         with open(tmp, 'w') as f:
-            json.dump({'model_checkpoint_path': path, 'all_model_checkpoint_paths': kept}, f)
+            json.dump({'model_checkpoint_path': os.path.basename(path),
+                       'all_model_checkpoint_paths': [os.path.basename(p) for p in kept]}, f)
         os.replace(tmp, self.index_path)
         return path
 
@@ -161,6 +170,11 @@ def engine_arrays(eng, names_shapes, with_state=True):
         for name, _ in names_shapes:
             out[tf_target_name(name)] = T[name]
     out[STEP_KEY] = np.array(int(eng.counters[1].item()), np.int64)
+    if hasattr(eng, 'worker_step'):
+        # the workers' own loop counter (agent.py:55); the reference's Saver keeps only `step` and
+        # resumes every worker at it (agent.py:34,46) -- kept so that a resume without the engine
+        # state (host-stepped envs) continues at the worker step it left
+        out[WSTEP_KEY] = np.array(int(eng.worker_step), np.int64)
     if state is not None:
         out[STATE_KEY] = state
     return out
@@ -170,7 +184,8 @@ def engine_restore(eng, names_shapes, arrays, state=None):
     """Restore into a created engine.  With a state blob of the same configuration: the exact
     state (bit-continuous).  Otherwise the reference's resume: parameters (and whatever of the
     target / RMSProp slots the file has) on freshly reset envs, global and worker step at the
-    restored ``step`` (agent.py:34,46).  Returns the global step."""
+    restored ``step`` (agent.py:34,46) -- the worker step at the saved ``__worker_step__`` when the
+    file has one.  Returns the global step."""
     import torch
     algo = eng.algo
     step = int(arrays[STEP_KEY])
@@ -205,8 +220,9 @@ def engine_restore(eng, names_shapes, arrays, state=None):
     if ms is not None and mom is not None:
         eng.ms.copy_(torch.as_tensor(ms))
         eng.mom.copy_(torch.as_tensor(mom))
-    eng.set_step(step, step)
-    torch.cuda.synchronize()
+    eng.set_step(step, int(arrays.get(WSTEP_KEY, step)))
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     return step
 
 
@@ -227,22 +243,72 @@ def save_engine(saver, eng, names_shapes, rank=0, world=1, barrier=None):
     return step
 
 
+def _collectives(world):
+    """(broadcast_object from rank 0, all-ranks AND of a flag) over torch.distributed, or the
+    one-rank identities."""
+    import torch.distributed as dist
+    if world == 1 or not dist.is_initialized():
+        return (lambda obj: obj), (lambda ok: bool(ok))
+
+    def bcast(obj):
+        box = [obj]
+        dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    def all_ok(ok):
+        box = [None] * dist.get_world_size()
+        dist.all_gather_object(box, bool(ok))
+        return all(box)
+    return bcast, all_ok
+
+
 def restore_engine(saver, eng, names_shapes, rank=0, world=1):
-    """Restore the newest checkpoint of ``saver`` (None if there is none).  Rank r takes its own
-    env shard's state when the checkpoint was written by as many ranks, else resumes from
-    parameters + step like the reference."""
-    path = saver.latest()
-    if path is None:
+    """Restore the newest checkpoint of ``saver`` (None if there is none) on every rank alike.
+
+    Rank 0 picks the checkpoint and the path -- none, the exact engine states (written by as many
+    ranks: each rank takes its own env shard's state), or parameters + step like the reference --
+    and broadcasts it; every rank then checks that it can follow, and the ranks agree on the
+    outcome: a rank that cannot read the parameter file fails every rank together; a rank whose
+    state file is missing or does not load sends every rank to the parameters + step path (the
+    ranks then verify they restored rank 0's parameters bit for bit).  So the ranks never take different paths and their
+    collectives keep matching (the exact path restores the overlap pipeline in flight)."""
+    bcast, all_ok = _collectives(world)
+    plan = None
+    if rank == 0:
+        path = saver.latest()
+        if path is not None:
+            try:
+                w = int(load(path).get('world', -1))
+            except (OSError, ValueError):
+                w = -2
+            plan = (os.path.basename(path), 'exact' if w == world and not eng.external_env else 'params')
+    plan = bcast(plan)
+    if plan is None:
         return None
-    arrays = load(path)
-    state = None
-    # the exact state only if the checkpoint was written by as many ranks (each rank's env shard);
-    # otherwise every rank falls back alike to parameters + step
-    if int(arrays.get('world', -1)) == world:
-        if rank == 0:
-            state = arrays.get(STATE_KEY)
-        else:
-            rp = path[:-4] + '.rank%d.npz' % rank
-            if os.path.exists(rp):
-                state = load(rp).get(STATE_KEY)
-    return engine_restore(eng, names_shapes, arrays, state)
+    path = os.path.join(saver.dir, plan[0])
+    try:
+        arrays = load(path)
+        err = None
+    except (OSError, ValueError) as e:
+        arrays, err = None, e
+    if not all_ok(arrays is not None):
+        raise RuntimeError('restore_engine: a rank cannot read %s (%s)' % (path, err or 'another rank'))
+    if plan[1] == 'exact':
+        ok = False
+        try:
+            state = arrays.get(STATE_KEY) if rank == 0 else load(path[:-4] + '.rank%d.npz' % rank).get(STATE_KEY)
+            if state is not None:
+                eng.reset()
+                eng.load_state(state)
+                ok = True
+        except (OSError, ValueError, RuntimeError):
+            ok = False
+        if all_ok(ok):
+            return int(arrays[STEP_KEY])
+    step = engine_restore(eng, names_shapes, arrays, None)
+    if world > 1:   # every rank read rank 0's file: the replicas must hold rank 0's parameters exactly
+        import hashlib
+        digest = hashlib.sha1(eng.params.detach().cpu().numpy().tobytes()).hexdigest()
+        if not all_ok(digest == bcast(digest)):
+            raise RuntimeError('restore_engine: the ranks restored different parameters from %s' % path)
+    return step

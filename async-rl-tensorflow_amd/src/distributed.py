@@ -115,6 +115,19 @@ class PartitionedPS:
             dist.all_gather_into_tensor(self.gathered, self.w_out, group=self.group)
         return self.gathered
 
+    def sync_slots(self, eng):
+        """Every rank owns (updates) only its range of the RMSProp slots: gather the owned ranges
+        of ms and mom into every replica's full buffers, so that a checkpoint (rank 0 writes the
+        slots under TF1's slot names) holds the true slots of every range.  A collective: every
+        rank calls it at the same point, between iterations."""
+        r = self.rank
+        lo, n = self.lo[r], self.n[r]
+        for t in (eng.ms, eng.mom):
+            self.w_out.zero_()
+            self.w_out[:n].copy_(t[lo:lo + n])
+            self.all_gather()
+            t.copy_(self.gathered[:self.total])
+
     def apply(self, eng):
         r = self.rank
         self.all_to_all(eng.grads)

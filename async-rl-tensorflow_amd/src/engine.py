@@ -169,6 +169,7 @@ class Engine:
             arg = hp.ctypes.data_as(ctypes.c_void_p)
         check(lib().a3c_engine_reset(self._h, arg, _lib.stream_handle()), 'a3c_engine_reset')
         self._ext_began = False
+        self._step0_w = 0
 
     def rollout_grad(self):
         check(lib().a3c_engine_rollout_grad(self._h, _lib.stream_handle()), 'a3c_engine_rollout_grad')
@@ -241,7 +242,11 @@ class Engine:
     # ---------------------------------------------------------------- checkpoint / resume
     @property
     def worker_step(self):
-        """agent.py:55's loop counter (the lr / epsilon schedules' step) at the next rollout."""
+        """agent.py:55's loop counter (the lr / epsilon schedules' step) at the next rollout.
+        Host-stepped engines before their first rollout: the device counters are written by
+        ext_begin, so the step is the one set_step restored (0 on a fresh run)."""
+        if self.external_env and not getattr(self, '_ext_began', False):
+            return int(getattr(self, '_step0_w', 0))
         c = self.counters.cpu()
         return int(c[2]) + int(c[0]) - 3
 
@@ -249,6 +254,7 @@ class Engine:
         """Resume from parameters + step (the reference's Saver, agent.py:29): the global step and
         the workers' loop counter restart there (agent.py:34,46)."""
         w = global_step if worker_step is None else worker_step
+        self._step0_w = int(w)
         check(lib().a3c_engine_set_step(self._h, int(global_step), int(w), _lib.stream_handle()),
               'a3c_engine_set_step')
 
@@ -288,8 +294,10 @@ class Engine:
                                        _lib.i64_array(self.sizes), float(self.cfg.clip_norm), None,
                                        _lib.ptr(self._clip_ws), _lib.stream_handle()), 'a3c_clip_grads')
         ps.push(self.grads, lr_dev=self.sched_ptr)
-        self.advance()
         ps.pull(self.params)
+        # counters, and for q the target copy of the pulled (global) weights when the global step
+        # crossed a multiple of target_q_update_step (agent.py:166-167, 342-344)
+        self.apply_commit(None)
 
     # ---------------------------------------------------------------- host-stepped envs
     def ext_begin(self, rgb):

@@ -15,6 +15,15 @@ MI355X form, one process per GPU:
   rollout (theta' <- theta, network.py:96-107).
 No collective runs on the data path. The only collectives are the handle exchange at setup and
 the barrier at teardown.
+
+Memory model: the shards are allocated FINE-GRAINED by default
+(``memory='fine'``, hipDeviceMallocFinegrained).  Plain hipMalloc memory is coarse-grained: it is
+coherent only at kernel boundaries, and a peer GPU's read-modify-writes over xGMI and the owner's
+L2-cached reads of the same lines are ordered by nothing but those boundaries.  Fine-grained
+memory is coherent at instruction granularity across devices, so every push lands in the owner's
+memory and every pull reads it from there: what remains unordered is exactly Hogwild's element
+interleaving of concurrent unlocked RMWs (the reference's ``use_locking=False`` PS apply,
+main.py:63-65).  ``memory='coarse'`` and ``'uncached'`` remain selectable for measurement.
 """
 import ctypes
 
@@ -26,7 +35,15 @@ from ._lib import check, lib, stream_handle
 
 
 class HogwildPS:
-    def __init__(self, local_params, decay=0.99, momentum=0.0, epsilon=0.1, group=None):
+    MEMORY_KINDS = {'coarse': 0, 'fine': 1, 'uncached': 2}
+
+    def __init__(self, local_params, decay=0.99, momentum=0.0, epsilon=0.1, group=None, memory='fine',
+                 ms=None, mom=None):
+        """local_params (and ms / mom: full RMSProp slots to start from, e.g. restored from a
+        checkpoint; default the TF1 init 1 / 0): this rank's shard is initialised from its range."""
+        if memory not in self.MEMORY_KINDS:
+            raise ValueError(f'memory must be one of {sorted(self.MEMORY_KINDS)}')
+        self.memory = memory
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -38,14 +55,20 @@ class HogwildPS:
         self.lo = [min(total, r * shard) for r in range(self.world)]
         self.n = [max(0, min(total, (r + 1) * shard) - self.lo[r]) for r in range(self.world)]
         base = ctypes.c_void_p()
-        check(lib().a3c_dev_alloc(3 * shard * 4, ctypes.byref(base)), 'a3c_dev_alloc')
+        check(lib().a3c_dev_alloc_kind(3 * shard * 4, self.MEMORY_KINDS[memory], ctypes.byref(base)),
+              'a3c_dev_alloc_kind')
         self._own = base.value
         from .engine import _view
         own = _view(self._own, (3, shard), torch.float32)
         own.zero_()
         r = self.rank
-        own[0, :self.n[r]].copy_(local_params[self.lo[r]:self.lo[r] + self.n[r]])
+        sl = slice(self.lo[r], self.lo[r] + self.n[r])
+        own[0, :self.n[r]].copy_(local_params[sl])
         own[1].fill_(1.0)                              # TF1 rms slot init
+        if ms is not None:
+            own[1, :self.n[r]].copy_(ms[sl])
+        if mom is not None:
+            own[2, :self.n[r]].copy_(mom[sl])
         self.own = own
         h = (ctypes.c_char * 64)()
         check(lib().a3c_ipc_handle(ctypes.c_void_p(self._own), h), 'a3c_ipc_handle')
@@ -97,6 +120,17 @@ class HogwildPS:
                 continue
             check(lib().a3c_copy_params(ctypes.c_void_p(pp + 4 * self.lo[q]), ctypes.c_void_p(self.base[q]),
                                         self.n[q], stream_handle()), 'a3c_copy_params')
+
+    def sync_slots(self, eng):
+        """The shared RMSProp slots (every shard's ms / mom) into the engine's full ms / mom
+        buffers, which Hogwild does not otherwise use: checkpoints then hold the true slots."""
+        for k, dst in ((1, eng.ms), (2, eng.mom)):
+            base = dst.data_ptr()
+            for q in range(self.world):
+                if self.n[q]:
+                    check(lib().a3c_copy_params(ctypes.c_void_p(base + 4 * self.lo[q]),
+                                                ctypes.c_void_p(self.base[q] + 4 * k * self.shard), self.n[q],
+                                                stream_handle()), 'a3c_copy_params')
 
     def gather(self):
         """Current shared parameters as one device tensor (for checks)."""

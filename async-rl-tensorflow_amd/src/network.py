@@ -21,7 +21,7 @@ from . import _lib
 from . import kernels as K
 from . import ops
 from . import checkpoint as C
-from .base import load_checkpoint, save_checkpoint
+from .base import copy_named, load_checkpoint, save_checkpoint
 
 
 def _align(n, a=64):
@@ -208,9 +208,8 @@ class Network(object):
       print(" [!] Load FAILED: %s" % checkpoint_dir)
       return False
     arrays, step = load_checkpoint(files[-1])
-    for name, w in self.w.items():
-      v = arrays.get(C.tf_name(name, 'a3c', self.dqn_type))
-      if v is not None:
-        w.copy_(torch.as_tensor(v).reshape(w.shape))
+    # TF variable names; round-1/2 files used the raw dict names
+    copy_named(arrays, {name: (w, [C.tf_name(name, 'a3c', self.dqn_type), name]) for name, w in self.w.items()},
+               files[-1])
     print(" [*] Load SUCCESS: %s" % files[-1])
     return True

@@ -72,6 +72,8 @@ def parse():
                     help='overlap: rollout k overlaps backward+apply of rollout k-1 (stale-1 async A3C); '
                          'sync: rollout -> backward -> all-reduce -> apply; hogwild: unlocked pushes into a '
                          'sharded IPC parameter server, no collective (BASELINE config 4)')
+    ap.add_argument('--hogwild-memory', default='fine', choices=['fine', 'coarse', 'uncached'],
+                    help='--update hogwild: allocation kind of the IPC-shared shards (DESIGN §7 memory model)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
@@ -89,6 +91,25 @@ def parse():
     return ap.parse_args()
 
 
+def host_cpu():
+    """The box's host CPU as BASELINE.md asks it stated: model name, logical CPUs (nproc) and the
+    CPUs this process may run on (a gpurun box gets a share of a larger host)."""
+    model = None
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = None
+    return dict(model=model, nproc=os.cpu_count(), affinity=allowed)
+
+
 def cpu_baseline(seconds, game, algo, frame84=False):
     """The reference's ps/worker algorithm restated on the CPU (oracle/ps_worker.py: shared-memory
     PS, W worker processes with Hogwild RMSProp, one numpy thread each) on the same synthetic
@@ -97,13 +118,17 @@ def cpu_baseline(seconds, game, algo, frame84=False):
     from oracle import ps_worker
     A, lives = GAMES[game]
     n = 5 if algo == 'a3c' else 32
-    W = max(1, min((os.cpu_count() or 2) - 1, 15))
+    host = host_cpu()
+    # W = nproc - 1 workers, capped by the CPUs this process may use and by the
+    # box's CPU share (16 per GPU on the gpurun pool: nproc reports the whole host)
+    avail = host['affinity'] or host['nproc'] or 2
+    W = max(1, min(avail - 1, 15))
     one = ps_worker.run(seconds=seconds / 2, workers=1, envs_per_worker=8, n_step=n, action_size=A, algo=algo,
                         start_lives=lives, frame84=frame84)
     many = ps_worker.run(seconds=seconds / 2, workers=W, envs_per_worker=8, n_step=n, action_size=A, algo=algo,
                          start_lives=lives, frame84=frame84) if W > 1 else one
     return dict(value=round(many['value'], 2), unit='env-steps/s', cores=W, kind='port',
-                one_worker=round(one['value'], 2),
+                one_worker=round(one['value'], 2), host_cpu=host,
                 sample=f'oracle/ps_worker.py ({algo} ps/worker, shared-memory PS, unlocked RMSProp, numpy fp32, '
                        f'8 envs x n={n} per worker{", pre-sized 84x84 frames" if frame84 else ""}): {W} workers x {many["seconds"]:.1f} s = '
                        f'{many["iterations"]} iterations; 1 ps/1 worker: {one["value"]:.1f} env-steps/s')
@@ -164,7 +189,7 @@ def main():
     ps = None
     if args.update == 'hogwild':
         from src.hogwild import HogwildPS
-        ps = HogwildPS(eng.params)
+        ps = HogwildPS(eng.params, memory=args.hogwild_memory)
 
     def step():
         if hpool is not None:
@@ -336,7 +361,8 @@ def main():
                        'game': args.game, 'head': 'lstm' if args.lstm else 'feed-forward', 'env': args.env, 'envs_per_gpu': E, 'n_step': n, 'action_size': A, 'algo': args.algo,
                        'env_steps_per_step': world * E * n,
                        'parallelism': (f'dp{world} hogwild: unlocked RMSProp pushes into {world} IPC-mapped HBM '
-                                       f'shards over xGMI, pull at rollout start, no collective'
+                                       f'shards ({args.hogwild_memory}-grained) over xGMI, pull at rollout start, '
+                                       f'no collective'
                                        if args.update == 'hogwild' else
                                        f'dp{world} partitioned PS: {coll} all-to-all of per-worker-clipped grads, '
                                        f'{world} sequential RMSProp steps per owned shard, {coll} all-gather'

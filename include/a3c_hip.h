@@ -213,12 +213,16 @@ int a3c_copy_params(float* dst, const float* src, int64_t n, void* stream);
  * shard with an unlocked elementwise RMSProp over xGMI and pull the parameters back
  * at rollout start (theta' <- theta, network.py:96-107).
  *  a3c_dev_alloc/free: plain hipMalloc'd device memory (IPC-exportable base pointer).
+ *  a3c_dev_alloc_kind: the same with kind 0 coarse-grained (= a3c_dev_alloc), 1 fine-grained
+ *                      (hipDeviceMallocFinegrained: peer writes coherent at instruction
+ *                      granularity, the Hogwild shards' default), 2 uncached; free with a3c_dev_free.
  *  a3c_ipc_handle:     64-byte hipIpcMemHandle of such a base pointer.
  *  a3c_ipc_open/close: map a peer's handle (lazy peer access) into this process.
  *  a3c_rmsprop_range:  TF ApplyRMSProp on n elements (w, ms, mom may live on a peer
  *                      GPU); lr read from lr_dev[0] when lr_dev != NULL.
  * -------------------------------------------------------------------------- */
 int a3c_dev_alloc(int64_t bytes, void** out);
+int a3c_dev_alloc_kind(int64_t bytes, int kind, void** out);
 int a3c_dev_free(void* p);
 int a3c_ipc_handle(void* base, void* handle64);
 int a3c_ipc_open(const void* handle64, void** out);

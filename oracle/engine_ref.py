@@ -124,8 +124,10 @@ class EngineRef:
         ee = self.ep_end.astype(np.float64)
         return (ee + np.maximum(0.0, (float(h['ep_start']) - ee) * d / float(h['ep_end_t']))).astype(np.float32)
 
-    def iterate(self, forced_actions=None):
-        """One iteration; returns a dict of everything the GPU engine exposes."""
+    def iterate(self, forced_actions=None, grads=True):
+        """One iteration; returns a dict of everything the GPU engine exposes.  grads=False stops
+        after the rollout and its targets (no batch forward / backward: for callers that
+        back-propagate the engine's own saved activations instead)."""
         E, n, A, h = self.E, self.n, self.A, self.h
         acts = np.zeros((n, E), np.int32)
         sampled = np.zeros((n, E), np.int32)
@@ -170,6 +172,8 @@ class EngineRef:
             target = R.td_target(rewards.reshape(-1), terms.reshape(-1), qn.astype(np.float32),
                                  h['discount']).astype(np.float32)
         out['target'] = target.reshape(n, E)
+        if not grads:
+            return out
         if self.lstm:
             fwd = R.lstm_a3c_forward(self.params, states, n, h0c0[0], h0c0[1], terms, dtype=self.dtype)
             out['lstm'] = fwd['lstm']

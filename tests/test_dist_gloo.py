@@ -94,12 +94,12 @@ def _init(rank, world, port):
     assert (r, w) == (rank, world)
 
 
-def _shared_start(rank, A=6, lstm=False):
+def _shared_start(rank, A=6, lstm=False, algo='a3c'):
     """Every rank starts from rank 0's parameters (broadcast, as main.py / bench.py do)."""
     from src.distributed import broadcast_params
     from src.initializers import init_params
     from src.kernels import param_names_shapes
-    ns = param_names_shapes(A, 'a3c', lstm=lstm)
+    ns = param_names_shapes(A, algo, lstm=lstm)
     p = init_params(ns, seed=5 + rank, stddev=0.08)       # different on purpose: broadcast fixes it
     names = [n for n, _ in ns]
     flat = torch.cat([torch.as_tensor(p[n]).reshape(-1) for n in names])
@@ -112,8 +112,10 @@ def _shared_start(rank, A=6, lstm=False):
 def _ref(p, rank, world, cfg):
     from oracle.engine_ref import EngineRef
     E = cfg.get('E', 3)
-    ref = EngineRef(p, E, 2, cfg.get('A', 6), 'a3c', cfg.get('lives', 0), 16, seed=9, env_id_base=rank * E,
-                    world_size=world, lstm=cfg.get('lstm', False))
+    algo = cfg.get('algo', 'a3c')
+    kw = dict(target_q_update_step=cfg['tq']) if 'tq' in cfg else {}
+    ref = EngineRef(p, E, 2, cfg.get('A', 6), algo, cfg.get('lives', 0), 16, seed=9, env_id_base=rank * E,
+                    world_size=world, lstm=cfg.get('lstm', False), **kw)
     ref.reset()
     return ref
 
@@ -121,7 +123,7 @@ def _ref(p, rank, world, cfg):
 def _worker_partitioned(rank, world, port, out, cfg):
     _init(rank, world, port)
     from src.distributed import PartitionedPS
-    p, ns = _shared_start(rank, cfg.get('A', 6), cfg.get('lstm', False))
+    p, ns = _shared_start(rank, cfg.get('A', 6), cfg.get('lstm', False), cfg.get('algo', 'a3c'))
     ref = _ref(p, rank, world, cfg)
     eng = _CpuShardEngine(ref, ns)
     ps = PartitionedPS(eng.total, device='cpu')
@@ -132,7 +134,7 @@ def _worker_partitioned(rank, world, port, out, cfg):
         mine.append(eng.grads.numpy().copy())
         ps.apply(eng)
     out[rank] = dict(params=eng.flat(ref.params), grads=mine, ms=eng.ms.copy(), lo=ps.lo, n=ps.n,
-                     step=ref.global_step)
+                     step=ref.global_step, target=eng.flat(ref.tparams))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -169,7 +171,7 @@ def _replay(world, iters, combine, cfg=None):
     from src.initializers import init_params
     from src.kernels import param_names_shapes
     cfg = dict(cfg or {})
-    ns = param_names_shapes(cfg.get('A', 6), 'a3c', lstm=cfg.get('lstm', False))
+    ns = param_names_shapes(cfg.get('A', 6), cfg.get('algo', 'a3c'), lstm=cfg.get('lstm', False))
     names = [n for n, _ in ns]
     p = init_params(ns, seed=5, stddev=0.08)               # rank 0's params (broadcast source)
     refs = [_ref(p, r, world, cfg) for r in range(world)]
@@ -194,6 +196,8 @@ def _check_partitioned(world, cfg):
     ref0, ns = _replay(world, cfg.get('iters', 3), sequential, cfg)
     np.testing.assert_array_equal(res[0]['params'], _CpuShardEngine(ref0, ns).flat(ref0.params))
     assert res[0]['step'] == ref0.global_step
+    for r in range(world):      # q: every rank copied its target net at the same global step
+        np.testing.assert_array_equal(res[r]['target'], _CpuShardEngine(ref0, ns).flat(ref0.tparams))
     return res
 
 
@@ -217,6 +221,32 @@ def test_gloo_eight_rank_partitioned_ps_is_the_reference_ps_rule(cfg):
 def test_gloo_four_rank_partitioned_ps_lstm_head():
     """C5 (LSTM head, 1,203,456 floats) through the same exchange at world 4."""
     _check_partitioned(4, dict(A=6, lives=3, lstm=True, iters=2))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('world', [2, 4])
+def test_gloo_partitioned_ps_async_q_learning(world):
+    """The reference's own running path, async one-step Q-learning (agent.py:153-207, main.py:60-66),
+    through the partitioned PS: every rank's clipped TD-loss gradient is its own RMSProp step in
+    rank order, and the target net (agent.py:166-167, 342-344) is copied at the same global step T
+    on every rank (tq 30 with 2 steps x 3 envs x world per update: at update 1 and later)."""
+    cfg = dict(algo='q', A=4, lives=5, tq=30, iters=3)
+    res = _check_partitioned(world, cfg)
+    p0, ns = _shared_start_host(cfg)
+    assert not np.array_equal(res[0]['target'], p0)    # the copy happened
+
+
+def _shared_start_host(cfg):
+    _setup_paths()
+    from src.initializers import init_params
+    from src.kernels import param_names_shapes
+    ns = param_names_shapes(cfg.get('A', 6), cfg.get('algo', 'a3c'))
+    p = init_params(ns, seed=5, stddev=0.08)
+    offs, total = aligned_layout(ns)
+    flat = np.zeros(total, np.float32)
+    for (name, _), off in zip(ns, offs):
+        flat[off:off + p[name].size] = p[name].reshape(-1)
+    return flat, ns
 
 
 @pytest.mark.timeout(300)

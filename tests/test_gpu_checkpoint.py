@@ -75,8 +75,9 @@ def test_resume_is_bit_continuous(mode, tmp_path):
 
 def test_resume_from_params_and_step(tmp_path):
     """Without the engine state (e.g. a checkpoint converted from another run): parameters, target
-    and RMSProp slots come back, and the global and the workers' step restart at `step`
-    (agent.py:34,46: before_train reads step_op into self.T and self.step)."""
+    and RMSProp slots come back, and the global step restarts at `step`; the workers' step at the
+    saved worker step, or at `step` for a file without one (agent.py:34,46: before_train reads
+    step_op into self.T and self.step)."""
     from src import checkpoint as C
     a, ns = _make(MODES[2])                        # q: has a target network
     for _ in range(3):
@@ -92,7 +93,14 @@ def test_resume_from_params_and_step(tmp_path):
     for name in ('params', 'target_params', 'ms', 'mom'):       # every tensor (not the alignment padding)
         for off, sz in zip(a.offsets, a.sizes):
             assert torch.equal(getattr(a, name)[off:off + sz], getattr(c, name)[off:off + sz]), name
-    assert int(c.counters[1].item()) == step and c.worker_step == step
+    # the file keeps the worker step too (host-env resumes continue at it)
+    assert int(c.counters[1].item()) == step and c.worker_step == a.worker_step
+    del arrays[C.WSTEP_KEY]                        # a file with only `step`: the reference's rule
+    saver2 = C.Saver(str(tmp_path / 'ref'))
+    saver2.save(arrays, step)
+    d, _ = _make(MODES[2], seed=5)
+    assert C.restore_engine(saver2, d, ns) == step
+    assert int(d.counters[1].item()) == step and d.worker_step == step
 
 
 def test_state_load_rejects_other_configuration():
@@ -122,6 +130,27 @@ def test_main_engine_resumes_bit_for_bit(tmp_path):
     recs = [json.loads(x) for x in open(tmp_path / 'two' / 'engine.jsonl')]
     assert recs and all(k in recs[-1] for k in ('avg_reward', 'avg_loss', 'avg_q', 'avg_ep_reward', 'max_ep_reward',
                                                 'min_ep_reward', 'num_game', 'learning_rate'))
+
+
+def test_main_engine_host_envs_resume_shortens_the_run(tmp_path):
+    """Host-stepped envs resume from parameters + step (no engine state): the resumed run trains
+    only the worker steps left to max_step (agent.py:46 `xrange(self.step, self.max_step)`), and a
+    fresh run takes exactly ceil(max_step / n) rollouts (the step was read before the
+    host engine had written its counters)."""
+    import main
+    common = ['--mode', 'engine', '--env_name', 'Pong-v0', '--num_envs', '8', '--num_frames', '64', '--envs_on',
+              'host', '--host_threads', '2', '--update', 'sync', '--random_seed', '3', '--max_step', '40']
+    one = main.main(common + ['--iterations', '3', '--logdir', str(tmp_path / 'a')])
+    torch.cuda.synchronize()
+    assert one.worker_step == 15
+    del one
+    two = main.main(common + ['--iterations', '100', '--logdir', str(tmp_path / 'a')])
+    torch.cuda.synchronize()
+    assert two.worker_step == 40                 # 5 more rollouts, not max_step / n + 1 again
+    del two
+    fresh = main.main(common + ['--iterations', '100', '--logdir', str(tmp_path / 'b')])
+    torch.cuda.synchronize()
+    assert fresh.worker_step == 40
 
 
 @pytest.mark.parametrize('algo,A,lives,n', [('a3c', 6, 3, 5), ('q', 4, 5, 8)])

@@ -5,7 +5,8 @@ the engine at the exact shapes the bench times, so the variants it actually laun
 against oracle/engine_ref.py:
   * C2 headline: Pong, 256 envs, n=5, mode M1 (raw RGB + Environment.screen on device), overlap
     pipeline: k_head_screen_conv12 (fused step t head + screen + step t+1 conv1/conv2), k_fc_part
-    over 256 rows with the wave-0 fold, k_conv_bwd<false,4> on 183 workgroups of 7 samples;
+    over 256 rows with the wave-0 fold, k_conv_bwd<false,4> on 256 workgroups of 5 samples (one per
+    CU, the CB_SMEM_SOLO reservation);
     and the synchronous update (k_head_screen, k_conv12_fwd, k_fc_fwd, k_conv_bwd<true,8>);
   * C3 per-GPU shard: Breakout (A=4, 5 lives), 256 envs;
   * C4 per-GPU shard: Pong, 512 envs, sync, overlap and Hogwild at world 1;
