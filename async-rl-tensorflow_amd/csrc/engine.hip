@@ -95,6 +95,10 @@ struct a3c_engine {
   hipStream_t gs;          // backward side stream (weight-gradient GEMMs beside the conv backward)
   hipEvent_t ev_gfork, ev_gjoin;
   hipEvent_t ev_start, ev_roll[2];
+  // split exchange (several GPUs, cfg.split_exchange): ev_head marks the fc / head gradients
+  // clipped, mid-backward; a comm stream waits on it (a3c_engine_wait_grad_head)
+  int split;
+  hipEvent_t ev_head;
   // cross-stream ordering by stream memory operations (hipStreamWriteValue32 / WaitValue32 on
   // monotonic counters in device memory) instead of events: measured 3.6 us per hop against
   // 12-40 us for hipEventRecord + hipStreamWaitEvent (tools/waitvalue_probe.py)
@@ -163,6 +167,7 @@ extern "C" void a3c_engine_config_default(a3c_engine_config* c) {
   c->learn_start = 32;
   c->target_q_update_step = 40000LL;
   c->discount = 0.99;
+  c->split_exchange = 1;   // several GPUs: the fc / head exchange under the conv backward
 }
 
 extern "C" int a3c_engine_destroy(a3c_engine* e) {
@@ -178,6 +183,7 @@ extern "C" int a3c_engine_destroy(a3c_engine* e) {
   if (e->ev_gfork) (void)hipEventDestroy(e->ev_gfork);
   if (e->ev_gjoin) (void)hipEventDestroy(e->ev_gjoin);
   if (e->ev_start) (void)hipEventDestroy(e->ev_start);
+  if (e->ev_head) (void)hipEventDestroy(e->ev_head);
   for (int k = 0; k < 2; ++k) {
     if (e->ev_roll[k]) (void)hipEventDestroy(e->ev_roll[k]);
   }
@@ -315,6 +321,12 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
       a3c_engine_destroy(e);
       return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "stream/event creation failed");
     }
+  }
+  // the split exchange needs eager launches (its event is recorded mid-backward) and a peer
+  e->split = cfg->split_exchange && cfg->world_size > 1 && !cfg->use_graph;
+  if (e->split && hipEventCreateWithFlags(&e->ev_head, hipEventDisableTiming) != hipSuccess) {
+    a3c_engine_destroy(e);
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "event creation failed");
   }
   if (e->overlap) {
     // the rollout is a serial chain of small kernels: give its stream the higher priority so
@@ -878,12 +890,22 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
   // out of the backward's last kernel (k_finalize): no separate k_sumsq launch (round 3)
   OptParams op = opt_params(e, sl);
   const SumsqFused sf = {e->opt_part, &e->tt_f, &op};
+  // split exchange: the backward clips the fc / head range first and records ev_head (SplitBwd)
+  SplitBwd sp = {};
+  if (e->split) {
+    sp.ev_head = e->ev_head;
+    sp.clip = op;
+    sp.clip.mode = OPT_CLIP;
+    sp.sumsq_out = e->sumsq;
+    sp.cut = L.off[T_FCW];
+  }
   rc = a3c_backward_launch(L, sl.P, bsa, e->nE, sl.act_l1, sl.act_l2, sl.act_l3, sl.z,
                            sl.actions, sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra,
-                           fork ? e->gs : nullptr, fork ? e->ev_gfork : nullptr, fork ? e->ev_gjoin : nullptr,
-                           L.lstm ? &lb : nullptr, &sf);
+                           fork && !e->split ? e->gs : nullptr, fork && !e->split ? e->ev_gfork : nullptr,
+                           fork && !e->split ? e->ev_gjoin : nullptr, L.lstm ? &lb : nullptr, &sf,
+                           e->split ? &sp : nullptr);
   if (rc) return rc;
-  if (c.world_size > 1) {
+  if (c.world_size > 1 && !e->split) {
     // multi-GPU: clip this worker's gradient (agent.py:319) before the cross-GPU exchange
     op.mode = OPT_CLIP;
     return a3c_apply_launch(nullptr, nullptr, nullptr, e->grads, e->tt_f, op, e->opt_part, e->sumsq, s);
@@ -1096,6 +1118,24 @@ extern "C" int a3c_engine_iterate(a3c_engine* e, void* stream) {
 }
 
 extern "C" int a3c_engine_grad_ready(a3c_engine* e) { return e && e->grad_ready ? 1 : 0; }
+
+// Split exchange: *cut = the float offset where the fc / head range starts (its gradients are
+// clipped before the conv backward runs), 0 when the engine does not split.
+extern "C" int a3c_engine_exchange_split(a3c_engine* e, int64_t* cut) {
+  if (!e || !cut) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_exchange_split", "null");
+  *cut = e->split ? e->L.off[T_FCW] : 0;
+  return 0;
+}
+
+// `stream` waits until the last rollout_grad's backward has clipped grads[cut:] (ev_head): the
+// exchange of that range can start there, under the conv backward.
+extern "C" int a3c_engine_wait_grad_head(a3c_engine* e, void* stream) {
+  if (!e) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_wait_grad_head", "null");
+  if (!e->split) return a3c_set_error(A3C_ERR_STATE, "a3c_engine_wait_grad_head", "the engine does not split its exchange");
+  if (!e->grad_ready) return a3c_set_error(A3C_ERR_STATE, "a3c_engine_wait_grad_head", "no gradient computed yet");
+  A3C_CHECK(hipStreamWaitEvent((hipStream_t)stream, e->ev_head, 0));
+  return 0;
+}
 
 // RMSProp apply (lr from the schedule computed on device), target sync (q) and the counter
 // advance, all in one launch.  world_size == 1: the per-tensor clip is applied here as well.

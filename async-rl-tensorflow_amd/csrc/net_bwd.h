@@ -34,6 +34,7 @@ struct FinalizeSegs {
   int sum_t[4];           // their indices
   int sum_c0[5];          // prefix sums of their chunk counts
   OptParams op;
+  int no_tail;            // 1: no loss / schedule block (the split backward's second finalize)
 };
 
 // engine form of the per-tensor norms: k_finalize produces the partials (layout tt) and the schedule
@@ -45,6 +46,17 @@ struct SumsqFused {
 // the partial layout SumsqFused expects: FIN_X slots for each tensor a finalize segment writes,
 // SS_CHUNK chunks for the others
 int a3c_fused_tab(const NetLayout& L, TensorTab* tt);
+
+// Split exchange (multi-GPU): the fc / head gradients -- 99 % of the bytes -- are final
+// before the conv backward starts, so the backward finalizes, norms and clips them first, records
+// ev_head (the exchange of that range starts on a comm stream under the conv backward), then the
+// conv tensors.  Bit-identical to the one-pass clip: the same partials, the same clip math.
+struct SplitBwd {
+  hipEvent_t ev_head;     // recorded on the backward's stream once grads[cut:] are clipped
+  OptParams clip;         // the per-worker clip (mode OPT_CLIP), its range set per pass
+  float* sumsq_out;       // per-tensor squared norms (written by the second pass, all tensors)
+  int64_t cut;            // float offset of the fc weights: conv tensors [0, cut), the rest [cut, total)
+};
 
 struct BwdPlan {
   int nwg, per_wg, head_split, fc_split, groups;
@@ -80,7 +92,8 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
                         int literal, float* grads, float* loss_out, float* ws, hipStream_t s,
                         const ReturnsArgs* ra = nullptr,
                         hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr,
-                        const LstmBwd* lb = nullptr, const SumsqFused* sf = nullptr);
+                        const LstmBwd* lb = nullptr, const SumsqFused* sf = nullptr,
+                        const SplitBwd* sp = nullptr);
 int a3c_returns_launch(const float* rewards, const uint8_t* terms, const float* boot, int64_t boot_stride,
                        int n, int64_t E, double gamma, float* R, hipStream_t s);
 int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float* qn, int64_t B, int A,

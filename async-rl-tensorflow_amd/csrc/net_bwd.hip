@@ -758,12 +758,12 @@ __global__ void __launch_bounds__(256) k_finalize(FinalizeSegs fs, const float* 
     }
     return;
   }
-  if (b == FIN_X * fs.n) {
+  if (!fs.no_tail && b == FIN_X * fs.n) {
     if (loss_out) loss_reduce_block(terms, B, loss_out);
     if (fs.part && threadIdx.x == 0) opt_schedule(fs.op);
     return;
   }
-  const int k = b - FIN_X * fs.n - 1;
+  const int k = b - FIN_X * fs.n - (fs.no_tail ? 0 : 1);
   int j = 0;
   while (j + 1 < fs.nsum && k >= fs.sum_c0[j + 1]) ++j;
   const int t = fs.sum_t[j], c = k - fs.sum_c0[j];
@@ -839,6 +839,90 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   return p;
 }
 
+// The split backward (SplitBwd): head and fc weight GEMMs with their folds right behind them, the
+// dl2 GEMM, then [finalize of the fc / head segments + their norms + the schedule + the loss, the clip
+// of grads[cut:], ev_head], then the conv backward, its slab folds + norms and the clip of
+// grads[:cut].  Every fold, partial and clip value is the one-pass path's, so the gradients are
+// bit-identical (tests/test_gpu_multirank.py).
+static int backward_split(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,
+                          float* ws, hipStream_t s, const BwdPlan& p, GemmArgs gh, GemmArgs gf, GemmArgs gd,
+                          float* grads, const float* terms, float* loss_out, const SumsqFused* sf, const SplitBwd* sp) {
+  const bool a3c = L.algo == A3C_ALGO_A3C;
+  gh.defer_reduce = gf.defer_reduce = 0;
+  gh.big = gf.big = gd.big = 0;
+  int rc = a3c_gemm(false, true, gh, s);
+  if (!rc) rc = a3c_gemm(false, true, gf, s);
+  if (!rc) rc = a3c_gemm(true, false, gd, s);
+  if (rc) return rc;
+  auto segs = [&](FinalizeSegs& fs) {
+    fs.dst = grads;
+    fs.part = sf->part;
+    fs.tt = *sf->tt;
+    fs.op = *sf->op;
+    fs.sum_c0[0] = 0;
+  };
+  auto seg = [&](FinalizeSegs& fs, const float* src, int64_t stride, int nsplit, int rows, int src_ld, int col0,
+                 int ncols, int tensor, int dst_ld, float scale) {
+    FinalizeSeg& q = fs.s[fs.n++];
+    q.src = src; q.split_stride = stride; q.nsplit = nsplit; q.rows = rows; q.src_ld = src_ld;
+    q.col0 = col0; q.ncols = ncols; q.dst_off = L.off[tensor]; q.dst_ld = dst_ld; q.scale = scale;
+    q.slot = sf->tt->pb_first[tensor];
+  };
+  // (1) fc / head tensors: segments, chunk sums of the tensors the GEMMs / BPTT wrote whole, the
+  // loss and the schedule
+  {
+    FinalizeSegs fs = {};
+    segs(fs);
+    seg(fs, ws + p.fccol, FC, p.fc_split, 1, 0, 0, FC, T_FCB, 0, 1.0f);
+    seg(fs, ws + p.hgrad, 0, 1, FC, L.zs, 0, L.A, T_HW, L.A, 1.0f);
+    seg(fs, ws + p.hcol, L.zs, p.head_split, 1, 0, 0, L.A, T_HB, 0, 1.0f);
+    if (a3c) {
+      seg(fs, ws + p.hgrad, 0, 1, FC, L.zs, L.A, 1, T_VW, 1, 1.0f);
+      seg(fs, ws + p.hcol, L.zs, p.head_split, 1, 0, L.A, 1, T_VB, 0, 1.0f);
+    }
+    for (int t = 0; t < L.nt; ++t) {
+      if (finalize_tensor(L, t)) continue;
+      if (L.off[t] < sp->cut || fs.nsum == 4)
+        return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "split backward: tensor layout");
+      fs.sum_t[fs.nsum] = t;
+      fs.sum_c0[fs.nsum + 1] = fs.sum_c0[fs.nsum] + fs.tt.pb_count[t];
+      ++fs.nsum;
+    }
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)(FIN_X * fs.n + 1 + fs.sum_c0[fs.nsum])), dim3(256), 0, s, fs,
+                       terms, B, loss_out);
+    A3C_CHECK(hipGetLastError());
+    OptParams op = sp->clip;
+    op.q0 = sp->cut >> 2;
+    op.q1 = L.total >> 2;
+    rc = a3c_apply_launch(nullptr, nullptr, nullptr, grads, *sf->tt, op, sf->part, nullptr, s);
+    if (rc) return rc;
+    A3C_CHECK(hipEventRecord(sp->ev_head, s));
+  }
+  // (2) conv tensors
+  rc = a3c_conv_bwd_launch(L, P, sa, B, act_l1, ws + p.dl2, ws, s);
+  if (rc) return rc;
+  const int per = (p.nwg + p.groups - 1) / p.groups;
+  hipLaunchKernelGGL(k_slab_group, dim3((CB_SLAB + 255) / 256, p.groups), dim3(256), 0, s, ws + p.cslab, p.nwg, per,
+                     (int64_t)CB_SLAB, ws + p.cgroup);
+  A3C_CHECK(hipGetLastError());
+  {
+    FinalizeSegs fs = {};
+    segs(fs);
+    fs.no_tail = 1;
+    const float* cs = ws + p.cgroup;
+    seg(fs, cs + CB_OFF_W1, CB_SLAB, p.groups, 1, 0, 0, KC1 * C1_N, T_L1W, 0, 1.0f / 255.0f);
+    seg(fs, cs + CB_OFF_B1, CB_SLAB, p.groups, 1, 0, 0, C1_N, T_L1B, 0, 1.0f);
+    seg(fs, cs + CB_OFF_W2, CB_SLAB, p.groups, 1, 0, 0, KC2 * C2_N, T_L2W, 0, 1.0f);
+    seg(fs, cs + CB_OFF_B2, CB_SLAB, p.groups, 1, 0, 0, C2_N, T_L2B, 0, 1.0f);
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)(FIN_X * fs.n)), dim3(256), 0, s, fs, terms, B, loss_out);
+    A3C_CHECK(hipGetLastError());
+    OptParams op = sp->clip;
+    op.q0 = 0;
+    op.q1 = sp->cut >> 2;
+    return a3c_apply_launch(nullptr, nullptr, nullptr, grads, *sf->tt, op, sf->part, sp->sumsq_out, s);
+  }
+}
+
 static bool xcd_gemm();   // (below, beside the other mode knobs)
 static bool dwfc_late_knob();
 static bool bwd_bound_knob();
@@ -847,7 +931,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
                         const float* z, const int32_t* actions, const float* target, float beta,
                         int literal, float* grads, float* loss_out, float* ws, hipStream_t s,
                         const ReturnsArgs* ra_in, hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join,
-                        const LstmBwd* lb, const SumsqFused* sf) {
+                        const LstmBwd* lb, const SumsqFused* sf, const SplitBwd* sp) {
   ReturnsArgs ra = {};
   if (ra_in) ra = *ra_in;
   if (B <= 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "B must be > 0");
@@ -922,6 +1006,10 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     if (a3c_shared_gpu()) gh.max_wgs = gf.max_wgs = gd.max_wgs = env_wgs;
   }
   int rc;
+  if (sp) {
+    if (!sf || fork) return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "split backward: fused norms, no fork");
+    return backward_split(L, P, sa, B, act_l1, ws, s, p, gh, gf, gd, grads, terms, loss_out, sf, sp);
+  }
   // sync mode: the three GEMMs in one launch (3.32M -> 3.41M env-steps/s), and so where the
   // overlapped backward bounds the iteration (M2: 5.17-5.22M -> 5.38-5.39M); beside a rollout
   // that bounds it the 1,420-workgroup launch slows it more than it gains (M1: 4.62M -> 4.45M),

@@ -42,6 +42,9 @@ struct OptParams {
   int64_t* counters;      // apply: block 0 advances counters[0] += dtau, counters[1] += step_add
   int64_t dtau;
   float rho, momentum, eps;
+  // apply / clip pass over float4 indices [q0, q1) only (q1 == 0: the whole flat vector) -- the
+  // split exchange clips the fc / head tensors before the conv backward, the conv tensors after
+  int64_t q0, q1;
 };
 
 int a3c_make_tab(int n, const int64_t* off, const int64_t* size, int64_t total, TensorTab* tt);

@@ -81,8 +81,9 @@ __global__ void __launch_bounds__(256) k_apply(float* __restrict__ w, float* __r
   const bool clip = op.clip > 0.f && (op.mode & OPT_CLIP);
   const bool apply = op.mode & OPT_APPLY;
   const float one_m_rho = 1.0f - op.rho;
-  const int64_t n4 = tt.total >> 2;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t qe = op.q1 > 0 ? op.q1 : tt.total >> 2;
+  for (int64_t q = (op.q1 > 0 ? op.q0 : 0) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < qe;
+       q += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = 4 * q;
     int t = 0;
     while (t + 1 < tt.n && i >= tt.off[t + 1]) ++t;     // padding after tensor t has zero grads
@@ -205,7 +206,7 @@ int a3c_sumsq_launch(const float* grads, const TensorTab& tt, const OptParams& o
 
 int a3c_apply_launch(float* w, float* ms, float* mom, float* grads, const TensorTab& tt, const OptParams& op,
                      const double* part, float* sumsq_out, hipStream_t s) {
-  int64_t n4 = tt.total >> 2;
+  const int64_t n4 = op.q1 > 0 ? op.q1 - op.q0 : tt.total >> 2;
   int blocks = (int)((n4 + 255) / 256);
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;

@@ -39,7 +39,7 @@ class EngineConfig(ctypes.Structure):
                 ('clip_norm', c_float), ('literal_adv', c_int), ('ep_start', c_float),
                 ('ep_end', c_float), ('ep_end_t', c_i64), ('learn_start', c_i64),
                 ('target_q_update_step', c_i64), ('discount', c_double), ('overlap', c_int),
-                ('external_env', c_int), ('frame84', c_int)]
+                ('external_env', c_int), ('frame84', c_int), ('split_exchange', c_int)]
 
 
 class EngineBuffers(ctypes.Structure):
@@ -123,6 +123,8 @@ SIGNATURES = {
     'a3c_engine_state_load': (c_int, [c_void_p, c_void_p, c_i64, c_void_p]),
     'a3c_engine_apply_shard': (c_int, [c_void_p, c_void_p, c_int, c_i64, c_i64, c_void_p, c_void_p]),
     'a3c_engine_apply_commit': (c_int, [c_void_p, c_void_p, c_void_p]),
+    'a3c_engine_exchange_split': (c_int, [c_void_p, ctypes.POINTER(c_i64)]),
+    'a3c_engine_wait_grad_head': (c_int, [c_void_p, c_void_p]),
     'a3c_engine_ext_begin': (c_int, [c_void_p, c_void_p, c_void_p]),
     'a3c_hostenv_create': (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_u64, c_int, c_int,
                                    ctypes.POINTER(c_void_p)]),

@@ -129,10 +129,82 @@ class PartitionedPS:
             t.copy_(self.gathered[:self.total])
 
     def apply(self, eng):
+        cut = getattr(eng, 'split_point', 0) if self.world > 1 else 0
+        if cut:
+            return self._apply_split(eng, cut)
         r = self.rank
         self.all_to_all(eng.grads)
         eng.apply_shard(self.recv, self.world, self.lo[r], self.n[r], self.w_out)
         self.all_gather()
+        eng.apply_commit(self.gathered)
+
+    # -------------------------------------------------------------------- split exchange
+    def _split_plan(self, cut):
+        """Each owned range [lo_q, lo_q + n_q) splits at `cut` into its conv part (a prefix of the
+        range: the conv tensors come first in the flat layout) and its fc / head part."""
+        if getattr(self, '_cut', None) != cut:
+            W, lo, n = self.world, self.lo, self.n
+            self._cut = cut
+            self.conv_n = [max(0, min(lo[q] + n[q], cut) - lo[q]) for q in range(W)]
+            self.fc_n = [n[q] - self.conv_n[q] for q in range(W)]
+            self.cmax = max(1, max(self.conv_n))
+            dev = self.recv.device
+            r = self.rank
+            self.recv_fc = torch.zeros(max(1, W * self.fc_n[r]), dtype=torch.float32, device=dev)
+            self.recv_conv = torch.zeros(max(1, W * self.conv_n[r]), dtype=torch.float32, device=dev)
+            self.w_conv = torch.zeros(self.cmax, dtype=torch.float32, device=dev)
+            self.g_conv = torch.zeros(W * self.cmax, dtype=torch.float32, device=dev)
+            self.comm = torch.cuda.Stream(device=dev) if dev.type == 'cuda' else None
+
+    def _a2a(self, out, src, splits_out, splits_in):
+        if _host_staged(src, self.group):
+            h = torch.empty(out.numel(), dtype=torch.float32)
+            dist.all_to_all_single(h, src.cpu(), splits_out, splits_in, group=self.group)
+            out.copy_(h)
+        else:
+            dist.all_to_all_single(out, src, splits_out, splits_in, group=self.group)
+
+    def _ag(self, out, src):
+        if _host_staged(src, self.group):
+            h = torch.empty(out.numel(), dtype=torch.float32)
+            dist.all_gather_into_tensor(h, src.cpu(), group=self.group)
+            out.copy_(h)
+        else:
+            dist.all_gather_into_tensor(out, src, group=self.group)
+
+    def _apply_split(self, eng, cut):
+        """The exchange in two phases (comm on its own stream).  Phase A, on a comm
+        stream that waits only for the backward's clip of grads[cut:] (fc + heads, 99 % of the
+        bytes): all-to-all of that range, the W rank-ordered RMSProp steps of each owned range's fc
+        part, all-gather -- concurrent with the conv backward on the caller's stream.  Phase B, on
+        the caller's stream behind the whole backward: the same for the conv prefix (~50 KB, held by
+        rank 0's range at W <= 8), then the caller joins the comm stream and commits.  The same
+        element math on the same values as the one-phase exchange: bit-identical replicas."""
+        import contextlib
+        self._split_plan(cut)
+        r, W = self.rank, self.world
+        g = eng.grads
+        total = self.total
+        lo_fc = self.lo[r] + self.conv_n[r]
+        ctx = torch.cuda.stream(self.comm) if self.comm is not None else contextlib.nullcontext()
+        with ctx:
+            if self.comm is not None:
+                eng.wait_grad_head()
+            # phase A: fc / head range
+            self._a2a(self.recv_fc[:W * self.fc_n[r]], g[cut:total], [self.fc_n[r]] * W, list(self.fc_n))
+            eng.apply_shard(self.recv_fc, W, lo_fc, self.fc_n[r], self.w_out[self.conv_n[r]:])
+            self._ag(self.gathered, self.w_out)
+        # phase B: conv prefix (caller's stream, after the whole backward)
+        self._a2a(self.recv_conv[:W * self.conv_n[r]], g[:cut], [self.conv_n[r]] * W, list(self.conv_n))
+        if self.conv_n[r]:
+            eng.apply_shard(self.recv_conv, W, self.lo[r], self.conv_n[r], self.w_conv)
+        self._ag(self.g_conv, self.w_conv)
+        if self.comm is not None:
+            torch.cuda.current_stream().wait_stream(self.comm)
+        for q in range(W):
+            if self.conv_n[q]:
+                self.gathered[q * self.shard:q * self.shard + self.conv_n[q]].copy_(
+                    self.g_conv[q * self.cmax:q * self.cmax + self.conv_n[q]])
         eng.apply_commit(self.gathered)
 
 

@@ -181,6 +181,18 @@ class Engine:
     def grad_ready(self):
         return bool(lib().a3c_engine_grad_ready(self._h))
 
+    @property
+    def split_point(self):
+        """Split exchange (several GPUs): the float offset where the fc / head gradients start --
+        clipped before the conv backward, so their exchange can run under it; 0: no split."""
+        cut = _lib.c_i64()
+        check(lib().a3c_engine_exchange_split(self._h, ctypes.byref(cut)), 'a3c_engine_exchange_split')
+        return int(cut.value)
+
+    def wait_grad_head(self):
+        """The current stream waits until the last rollout_grad's grads[split_point:] are clipped."""
+        check(lib().a3c_engine_wait_grad_head(self._h, _lib.stream_handle()), 'a3c_engine_wait_grad_head')
+
     def apply_shard(self, grads_by_rank, nranks, lo, n, w_out):
         """Partitioned PS step 1: nranks sequential RMSProp steps of [lo, lo+n) -> w_out."""
         check(lib().a3c_engine_apply_shard(self._h, _lib.ptr(grads_by_rank), int(nranks), int(lo), int(n),

@@ -361,7 +361,8 @@ def main():
                        'game': args.game, 'head': 'lstm' if args.lstm else 'feed-forward', 'env': args.env, 'envs_per_gpu': E, 'n_step': n, 'action_size': A, 'algo': args.algo,
                        'env_steps_per_step': world * E * n,
                        'parallelism': (f'dp{world} hogwild: unlocked RMSProp pushes into {world} IPC-mapped HBM '
-                                       f'shards ({args.hogwild_memory}-grained) over xGMI, pull at rollout start, '
+                                       f'shards ({dict(fine="fine-grained", coarse="coarse-grained", uncached="uncached")[args.hogwild_memory]}) '
+                                       f'over xGMI, pull at rollout start, '
                                        f'no collective'
                                        if args.update == 'hogwild' else
                                        f'dp{world} partitioned PS: {coll} all-to-all of per-worker-clipped grads, '

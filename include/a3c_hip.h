@@ -294,6 +294,12 @@ typedef struct a3c_engine_config {
                         grey frames (the north star's synthetic 84x84x4 states), so the env
                         step's Environment.screen becomes a 7 KB copy into the history ring.
                         0 (default, M1): raw 210x160x3 RGB frames, screen computed on device. */
+  int split_exchange; /* 1 (world_size > 1, eager launches): the backward clips the fc / head
+                        gradients (99 % of the bytes) before the conv backward and records an
+                        event there, so the partitioned-PS exchange of that range runs on a comm
+                        stream under the conv backward (a3c_engine_wait_grad_head); only the
+                        conv tensors' exchange waits for the whole backward.  Gradients are
+                        bit-identical either way.  Default 1.                                 */
 } a3c_engine_config;
 
 void a3c_engine_config_default(a3c_engine_config* cfg);
@@ -335,6 +341,16 @@ int a3c_engine_advance(a3c_engine* eng, void* stream);
 int a3c_engine_apply_shard(a3c_engine* eng, const float* grads_by_rank, int nranks, int64_t lo, int64_t n,
                            float* w_out, void* stream);
 int a3c_engine_apply_commit(a3c_engine* eng, const float* params_src, void* stream);
+/* Split exchange (cfg.split_exchange, world_size > 1): the backward clips grads[cut:] (fc + heads,
+ * 99 % of the bytes) before the conv backward and marks it; the exchange of that range (all-to-all,
+ * a3c_engine_apply_shard of its part of each owned range, all-gather) then runs on a comm stream
+ * under the conv backward, and only grads[:cut] (the conv tensors, ~50 KB) wait for the whole
+ * backward (src/distributed.py PartitionedPS).  The same apply_shard / apply_commit calls, on the
+ * sub-ranges; results bit-identical to the one-phase exchange.
+ *   a3c_engine_exchange_split: *cut (0: the engine does not split);
+ *   a3c_engine_wait_grad_head: `stream` waits for grads[cut:] of the last rollout_grad. */
+int a3c_engine_exchange_split(a3c_engine* eng, int64_t* cut);
+int a3c_engine_wait_grad_head(a3c_engine* eng, void* stream);
 
 /* ----------------------------------------------------------------------------
  * Summaries: the aggregates train_with_summary logs every test_step

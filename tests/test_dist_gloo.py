@@ -51,9 +51,11 @@ class _CpuShardEngine:
     """The engine's partitioned-PS interface (apply_shard / apply_commit) over an EngineRef:
     flat float32 params / ms / mom in the engine's aligned layout, RMSProp from oracle/ref_cpu."""
 
-    def __init__(self, ref, ns):
+    def __init__(self, ref, ns, split=False):
         self.ref, self.ns = ref, ns
         self.offs, self.total = aligned_layout(ns)
+        # the engine's split exchange: the fc / head range (from the fc weights on) first
+        self.split_point = self.offs[4] if split else 0
         self.ms, self.mom = self.flat(ref.ms, 1.0), self.flat(ref.mom)
         self.grads = None
 
@@ -125,7 +127,7 @@ def _worker_partitioned(rank, world, port, out, cfg):
     from src.distributed import PartitionedPS
     p, ns = _shared_start(rank, cfg.get('A', 6), cfg.get('lstm', False), cfg.get('algo', 'a3c'))
     ref = _ref(p, rank, world, cfg)
-    eng = _CpuShardEngine(ref, ns)
+    eng = _CpuShardEngine(ref, ns, split=cfg.get('split', False))
     ps = PartitionedPS(eng.total, device='cpu')
     mine = []
     for it in range(cfg.get('iters', 3)):
@@ -207,7 +209,16 @@ def test_gloo_two_rank_partitioned_ps_is_the_reference_ps_rule():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize('cfg', [dict(A=6), dict(A=4, lives=5)], ids=['pong', 'breakout'])
+@pytest.mark.parametrize('world', [2, 4])
+def test_gloo_split_exchange_is_the_reference_ps_rule(world):
+    """The two-phase exchange (fc / head range first, then the conv prefix -- held by rank 0's range)
+    gives the same replicas as the one-phase exchange: W sequential oracle RMSProp steps."""
+    _check_partitioned(world, dict(A=6, split=True))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('cfg', [dict(A=6), dict(A=4, lives=5), dict(A=4, lives=5, split=True)],
+                         ids=['pong', 'breakout', 'breakout-split'])
 def test_gloo_eight_rank_partitioned_ps_is_the_reference_ps_rule(cfg):
     """BASELINE configs 3/4 are 8-GPU runs: 8 ranks, 8 sequential RMSProp steps per range, and
     the last 64-aligned range ragged (Pong: 7 x 84,800 + 84,544 of 678,144 floats; Breakout:

@@ -38,7 +38,7 @@ TQ = 2000       # q target period: with 64 envs x 5 steps x 4 ranks (1,280 per u
 
 
 def _cfg(cfg):
-    c = dict(A=A, lives=0, lstm=False, algo='a3c', E=E, n=N, tq=TQ)
+    c = dict(A=A, lives=0, lstm=False, algo='a3c', E=E, n=N, tq=TQ, split=1)
     c.update(cfg or {})
     return c
 
@@ -52,6 +52,7 @@ def _make(rank, world, overlap, cfg=None):
     from src.kernels import param_names_shapes
     c = _cfg(cfg)
     kw = dict(target_q_update_step=c['tq']) if c['algo'] == 'q' else {}
+    kw['split_exchange'] = c['split']      # (several ranks: the two-phase exchange, PartitionedPS)
     eng = Engine(num_envs=c['E'], n_step=c['n'], action_size=c['A'], algo=c['algo'], num_frames=64, seed=11,
                  env_id_base=rank * c['E'], world_size=world, overlap=overlap, start_lives=c['lives'],
                  lstm=c['lstm'], **kw)
@@ -167,6 +168,7 @@ def _pps_worker(rank, world, port, out, overlap, cfg):
     dist.init_process_group('gloo')
     eng = _make(rank, world, overlap, cfg)
     q = _cfg(cfg)['algo'] == 'q'
+    assert (eng.split_point > 0) == bool(_cfg(cfg)['split'])
     ps = PartitionedPS(eng.params.numel())
     recs = []
     for _ in range(ITERS):
@@ -256,13 +258,15 @@ class _Oracle:
 @pytest.mark.parametrize('world,overlap,cfg,oracle', [
     (2, False, {}, False), (2, True, {}, False), (4, False, {}, True), (4, True, {}, False),
     (4, True, dict(A=4, lives=5), True), (4, False, dict(A=6, lives=3, lstm=True, E=16), False),
-    (4, False, dict(algo='q', A=6, lives=3), True), (2, False, dict(algo='q', A=4, lives=5, n=8), False)],
+    (4, False, dict(algo='q', A=6, lives=3), True), (2, False, dict(algo='q', A=4, lives=5, n=8), False),
+    (4, True, dict(split=0), False), (2, False, dict(split=0), False)],
     ids=['w2-sync', 'w2-overlap', 'w4-sync', 'w4-overlap', 'w4-breakout-overlap', 'w4-lstm-sync', 'w4-q-sync',
-         'w2-q-breakout-sync'])
+         'w2-q-breakout-sync', 'w4-overlap-onephase', 'w2-sync-onephase'])
 def test_partitioned_ps_ranks(world, overlap, cfg, oracle):
     """`world` ranks on one GPU (gloo, host-staged collectives) run the default multi-GPU exchange:
     all-to-all of the clipped gradients, each rank's W sequential RMSProp steps on its range,
-    all-gather.  Replicas stay identical; every rank's per-iteration record equals one process
+    all-gather -- by default in two phases (the fc / head range on a comm stream under the conv
+    backward, then the conv prefix: `split`), `onephase` ids after the whole backward.  Replicas stay identical; every rank's per-iteration record equals one process
     driving every shard through the same C-ABI by hand (first divergence named); in sync mode that
     also equals applying every rank's clipped gradient, in rank order, to full copies with
     a3c_rmsprop_range (the reference PS rule, main.py:60-65); `oracle`: the replay against the CPU
