@@ -39,6 +39,7 @@ struct Slot {
   float* z;                // [(n+1)][E][zs]
   float* R_buf;            // [n][E] returns / TD targets
   float *act_l1, *act_l2, *act_l3;
+  uint32_t* l2m;           // act_l2's ReLU mask as bits [n*E][81], written by the forward's conv2
   float *scr_l2, *scr_l3;  // bootstrap / target forward scratch
   uint8_t* prep;           // forward weights of P prepared for the kernels (k_prep_fwd)
   // C5 LSTM head: per step h_t, c_t, masked inputs hp, cp [n][E][U], gates [n][E][4U];
@@ -277,6 +278,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     ALLOC(sl.R_buf, nE * 4);
     ALLOC(sl.act_l1, nE * C1_P * C1_N * 4);
     ALLOC(sl.act_l2, nE * FLAT * 4);
+    ALLOC(sl.l2m, nE * C2_Q * 4);
     ALLOC(sl.act_l3, nE * FC * 4);
     ALLOC(sl.scr_l2, scrB * FLAT * 4);
     ALLOC(sl.scr_l3, scrB * FC * 4);
@@ -628,11 +630,12 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
     nx.act_l1 = nullptr;   // measurement only: the fused rollout kernel saves no conv1 output
 #endif
     nx.act_l2 = t + 1 < n ? sl.act_l2 + (o + E) * FLAT : sl.scr_l2;
+    nx.l2m = t + 1 < n ? sl.l2m + (o + E) * C2_Q : nullptr;
   }
   int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
                               sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s,
                               L.lstm ? &ls : nullptr, fuse && t > 0, has_next ? &nx : nullptr,
-                              fc_split(e) ? e->fcpart : nullptr);
+                              fc_split(e) ? e->fcpart : nullptr, sl.l2m + o * C2_Q);
   if (rc) return rc;
   if (dev_env && !e->fused_screen) {
     rc = a3c_env_screen_launch(E, sl.frames + o, e->pool, e->ring, e->R, e->counters, t, s);
@@ -903,7 +906,7 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
                            sl.actions, sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra,
                            fork && !e->split ? e->gs : nullptr, fork && !e->split ? e->ev_gfork : nullptr,
                            fork && !e->split ? e->ev_gjoin : nullptr, L.lstm ? &lb : nullptr, &sf,
-                           e->split ? &sp : nullptr);
+                           e->split ? &sp : nullptr, sl.l2m);
   if (rc) return rc;
   if (c.world_size > 1 && !e->split) {
     // multi-GPU: clip this worker's gradient (agent.py:319) before the cross-GPU exchange

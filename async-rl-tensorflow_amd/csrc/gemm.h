@@ -4,7 +4,7 @@
 
 
 
-enum { EPI_STORE = 0, EPI_BIAS_RELU = 1, EPI_BIAS = 2, EPI_MASK = 3 };
+enum { EPI_STORE = 0, EPI_BIAS_RELU = 1, EPI_BIAS = 2, EPI_MASK = 3, EPI_MASKBITS = 4 };
 
 // C[M][N] = epi( sum_k A(m,k) * B(k,n) )
 //   A(m,k) = A[m*lda + k] when the template's A_KC (k-contiguous) else A[k*lda + m]
@@ -17,6 +17,9 @@ struct GemmArgs {
   int epi;
   const float* bias;          // EPI_BIAS*, indexed by n
   const float* mask; int64_t ldm;  // EPI_MASK: keep where mask[m*ldm+n] > 0
+  // EPI_MASKBITS: keep where bit n & 31 of maskbits[m*ldm + (n >> 5)] is set (ldm in 32-bit words):
+  // the forward's ReLU mask as bits, 1/32 of the bytes of re-reading the activations
+  const uint32_t* maskbits;
   float* slab;                // split-K partials [nsplit][M][N]
   int nsplit;                 // requested split (effective split may be smaller)
   int kchunk;                 // set by a3c_gemm

@@ -103,6 +103,7 @@ __device__ inline void gemm_tile(const GemmArgs& g, int bx, int by, int bz, floa
         if (g.epi == EPI_BIAS_RELU) v = fmaxf(v + g.bias[col], 0.f);
         else if (g.epi == EPI_BIAS) v = v + g.bias[col];
         else if (g.epi == EPI_MASK) v = g.mask[(int64_t)row * g.ldm + col] > 0.f ? v : 0.f;
+        else if (g.epi == EPI_MASKBITS) v = (g.maskbits[(int64_t)row * g.ldm + (col >> 5)] >> (col & 31)) & 1u ? v : 0.f;
         g.C[(int64_t)row * g.ldc + col] = v;
       }
     }
@@ -218,6 +219,7 @@ __global__ void __launch_bounds__(256) k_gemm_f32_big(GemmArgs g) {
           if (g.epi == EPI_BIAS_RELU) v = fmaxf(v + g.bias[col], 0.f);
           else if (g.epi == EPI_BIAS) v = v + g.bias[col];
           else if (g.epi == EPI_MASK) v = g.mask[(int64_t)row * g.ldm + col] > 0.f ? v : 0.f;
+          else if (g.epi == EPI_MASKBITS) v = (g.maskbits[(int64_t)row * g.ldm + (col >> 5)] >> (col & 31)) & 1u ? v : 0.f;
           g.C[(int64_t)row * g.ldc + col] = v;
         }
       }
@@ -303,7 +305,7 @@ __global__ void __launch_bounds__(256) k_gemm_multi(GemmArgs g0, GemmArgs g1, Ge
 __global__ void k_reduce_slabs(const float* __restrict__ slab, int nsplit, int M, int N,
                                float* __restrict__ C, int64_t ldc, int epi,
                                const float* __restrict__ bias, const float* __restrict__ mask,
-                               int64_t ldm) {
+                               int64_t ldm, const uint32_t* __restrict__ maskbits) {
   WGLOG(8);
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t total = (int64_t)M * N;
@@ -313,6 +315,7 @@ __global__ void k_reduce_slabs(const float* __restrict__ slab, int nsplit, int M
   if (epi == EPI_BIAS_RELU) v = fmaxf(v + bias[col], 0.f);
   else if (epi == EPI_BIAS) v = v + bias[col];
   else if (epi == EPI_MASK) v = mask[(int64_t)row * ldm + col] > 0.f ? v : 0.f;
+  else if (epi == EPI_MASKBITS) v = (maskbits[(int64_t)row * ldm + (col >> 5)] >> (col & 31)) & 1u ? v : 0.f;
   C[(int64_t)row * ldc + col] = v;
 }
 
@@ -343,7 +346,7 @@ static int gemm_setup(bool a_kc, bool b_nc, GemmArgs& g) {
 static void gemm_reduce(const GemmArgs& g, hipStream_t s) {
   const int64_t total = (int64_t)g.M * g.N;
   hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
-                     g.slab, g.nsplit, g.M, g.N, g.C, g.ldc, g.epi, g.bias, g.mask, g.ldm);
+                     g.slab, g.nsplit, g.M, g.N, g.C, g.ldc, g.epi, g.bias, g.mask, g.ldm, g.maskbits);
 }
 
 int a3c_gemm3(GemmArgs& g0, GemmArgs& g1, GemmArgs& g2, hipStream_t s) {

@@ -153,12 +153,13 @@ struct Conv12Next {
   const float* b2;
   float* act_l1;            // nullable: the bootstrap state keeps no l1
   float* act_l2;
+  uint32_t* l2m;            // nullable: act_l2's ReLU mask as bits [b][81] (the backward's dl2 epilogue)
 };
 // ls (LSTM head, C5): the cell step runs on act_l3 and the heads read ls->h
 int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* prep, const StateAddr& sa,
                        int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
                        hipStream_t s, const LstmStep* ls = nullptr, bool skip_conv12 = false,
-                       const Conv12Next* next = nullptr, float* fc_part = nullptr);
+                       const Conv12Next* next = nullptr, float* fc_part = nullptr, uint32_t* l2m = nullptr);
 // fc layer as FC_NS K-slice partials part[x][M][FC] (folded by k_head_screen_conv12's head)
 int a3c_fc_part_launch(const float* A, const float* Wp, float* part, int64_t M, hipStream_t s);
 int a3c_fcp_split();

@@ -93,7 +93,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
                         const ReturnsArgs* ra = nullptr,
                         hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr,
                         const LstmBwd* lb = nullptr, const SumsqFused* sf = nullptr,
-                        const SplitBwd* sp = nullptr);
+                        const SplitBwd* sp = nullptr, const uint32_t* l2m = nullptr);
 int a3c_returns_launch(const float* rewards, const uint8_t* terms, const float* boot, int64_t boot_stride,
                        int n, int64_t E, double gamma, float* R, hipStream_t s);
 int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float* qn, int64_t B, int A,
@@ -106,6 +106,6 @@ int a3c_head_screen_launch(const NetLayout& L, const float* P, const float* act_
 int a3c_head_screen_conv12_launch(const NetLayout& L, const float* P, const float* act_l3, int64_t B, float* z,
                                   const HeadSelect& sel, const Conv12Next& nx, hipStream_t s);
 int a3c_conv12_launch(const NetLayout& L, const float* P, const uint8_t* prep, const StateAddr& sa, int64_t B,
-                      float* act_l1, float* act_l2, hipStream_t s);
+                      float* act_l1, float* act_l2, hipStream_t s, uint32_t* l2m = nullptr);
 int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,
                         const float* dl2, float* ws, hipStream_t s);

@@ -931,7 +931,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
                         const float* z, const int32_t* actions, const float* target, float beta,
                         int literal, float* grads, float* loss_out, float* ws, hipStream_t s,
                         const ReturnsArgs* ra_in, hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join,
-                        const LstmBwd* lb, const SumsqFused* sf, const SplitBwd* sp) {
+                        const LstmBwd* lb, const SumsqFused* sf, const SplitBwd* sp, const uint32_t* l2m) {
   ReturnsArgs ra = {};
   if (ra_in) ra = *ra_in;
   if (B <= 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "B must be > 0");
@@ -990,6 +990,9 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   gd.C = dl2; gd.ldc = FLAT;
   gd.M = (int)B; gd.N = FLAT; gd.K = FC;
   gd.epi = EPI_MASK; gd.mask = act_l2; gd.ldm = FLAT; gd.nsplit = 1;
+  if (l2m) {   // the forward's ReLU bits (engine): 415 KB instead of re-reading l2's 13.3 MB (E=256)
+    gd.epi = EPI_MASKBITS; gd.maskbits = l2m; gd.mask = nullptr; gd.ldm = FLAT / 32;
+  }
   gd.xcd = xcd_gemm() ? 2 : 0;          // the 20 row tiles of a W strip on one XCD
   {
     // overlap, A3C_GEMM_BIG=1: 128x128 tiles (210 workgroups instead of 820 beside the rollout;

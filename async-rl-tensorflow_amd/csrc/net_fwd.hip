@@ -222,7 +222,7 @@ __device__ inline void conv12_finish(f32x4 (&acc)[C1_TILES], float* l1s, int64_t
                                      const uint16_t* __restrict__ w1s, const float* __restrict__ b1,
                                      const float* __restrict__ W2, float* __restrict__ act_l1,
                                      float* __restrict__ act_l2, float (&w2r)[64], float bias2,
-                                     uint64_t* dbg) {
+                                     uint64_t* dbg, uint32_t* __restrict__ l2m = nullptr) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i16 = lane & 15, j4 = lane >> 4;
   const int nt = wid & 1, grp = wid >> 1;          // conv2: M-tiles grp and grp + 4 (when < 6)
@@ -338,7 +338,16 @@ __device__ inline void conv12_finish(f32x4 (&acc)[C1_TILES], float* l1s, int64_t
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int q = 16 * (grp + 4 * mi) + 4 * j4 + r;
-      if (q < C2_Q) st_act(act_l2 + b * FLAT + q * C2_N + 16 * nt + i16, fmaxf(acc2[mi][r] + bias2, 0.f));
+      const float v = fmaxf(acc2[mi][r] + bias2, 0.f);
+      if (q < C2_Q) st_act(act_l2 + b * FLAT + q * C2_N + 16 * nt + i16, v);
+      if (l2m) {
+        // the ReLU mask as bits for the backward's dl2 epilogue: position q's channels 16 nt ..
+        // 16 nt + 15 are the 16 lanes of group j4, so one ballot gives its half word (flat index
+        // q * 32 + c: word q of the row, bit c)
+        const uint64_t bal = __ballot(v > 0.f);
+        if (i16 == 0 && q < C2_Q)
+          ((uint16_t*)l2m)[(b * C2_Q + q) * 2 + nt] = (uint16_t)(bal >> (16 * j4));
+      }
     }
   }
 }
@@ -351,7 +360,7 @@ __device__ inline void conv12_core(const uint8_t* x8, const uint16_t* xb, float*
                                    const uint16_t* __restrict__ w1s, const float* __restrict__ b1,
                                    const float* __restrict__ W2, float* __restrict__ act_l1,
                                    float* __restrict__ act_l2, float (&w2r)[64], float bias2,
-                                   uint64_t* dbg = nullptr) {
+                                   uint64_t* dbg = nullptr, uint32_t* __restrict__ l2m = nullptr) {
   const int lane = threadIdx.x & 63;
   uint4* wl = (uint4*)l1s;
   for (int i = threadIdx.x; i < W1S_ELEMS / 8; i += blockDim.x) wl[i] = ((const uint4*)w1s)[i];
@@ -362,7 +371,7 @@ __device__ inline void conv12_core(const uint8_t* x8, const uint16_t* xb, float*
   for (int i = 0; i < C1_TILES; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   conv1_accum<U8, 0, HIST>(x8, xb, acc, [&](int f) { return __builtin_bit_cast(bf16x8, wl[f * 64 + lane]); });
   lds_only_barrier();                                  // weights read: the l1 region is conv1's output
-  conv12_finish<SAVE_L1, EW>(acc, l1s, b, w1s, b1, W2, act_l1, act_l2, w2r, bias2, dbg);
+  conv12_finish<SAVE_L1, EW>(acc, l1s, b, w1s, b1, W2, act_l1, act_l2, w2r, bias2, dbg, l2m);
 }
 
 
@@ -376,7 +385,8 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
                                                     const float* __restrict__ W2,
                                                     const float* __restrict__ b2,
                                                     float* __restrict__ act_l1,
-                                                    float* __restrict__ act_l2) {
+                                                    float* __restrict__ act_l2,
+                                                    uint32_t* __restrict__ l2m) {
   WGLOG(3);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint16_t* xb = (uint16_t*)smem;
@@ -444,7 +454,7 @@ __global__ void __launch_bounds__(512) k_conv12_fwd(StateAddr sa, int64_t B,
     }
   }
 
-  conv12_core<SAVE_L1, EW, U8>(x8, xb, l1s, b, w1s, b1, W2, act_l1, act_l2, w2r, bias2);
+  conv12_core<SAVE_L1, EW, U8>(x8, xb, l1s, b, w1s, b1, W2, act_l1, act_l2, w2r, bias2, nullptr, l2m);
   WG_T1(act_l2 + b * FLAT);
 }
 
@@ -889,7 +899,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
     return __builtin_bit_cast(bf16x8, wn[f - (HIST - 1) * 6]);
   });
   conv12_finish<SAVE_L1, false>(acc, (float*)smem, b, nx.w1s, nx.b1, nx.W2, SAVE_L1 ? nx.act_l1 : nullptr,
-                                nx.act_l2, w2r, bias2, dbg);
+                                nx.act_l2, w2r, bias2, dbg, nx.l2m);
   span_end(srec);
   if (dbg) {
     __syncthreads();
@@ -918,13 +928,13 @@ int a3c_head_screen_conv12_launch(const NetLayout& L, const float* P, const floa
 int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* prep, const StateAddr& sa,
                        int64_t B, float* act_l1, float* act_l2, float* act_l3, float* z, const HeadSelect& sel,
                        hipStream_t s, const LstmStep* ls, bool skip_conv12, const Conv12Next* next,
-                       float* fc_part) {
+                       float* fc_part, uint32_t* l2m) {
   if (B <= 0) return 0;
   if (L.lstm != (ls != nullptr))
     return a3c_set_error(A3C_ERR_INVALID, "a3c_forward", "the LSTM head needs its recurrent state");
   const float* P = params;
   if (!skip_conv12) {
-    int rc0 = a3c_conv12_launch(L, P, prep, sa, B, act_l1, act_l2, s);
+    int rc0 = a3c_conv12_launch(L, P, prep, sa, B, act_l1, act_l2, s, l2m);
     if (rc0) return rc0;
   }
   // fused overlap rollout: the fc as K-slice partials, folded by the head of k_head_screen_conv12
@@ -1003,14 +1013,14 @@ int a3c_head_screen_conv12_launch(const NetLayout& L, const float* P, const floa
 }
 
 int a3c_conv12_launch(const NetLayout& L, const float* P, const uint8_t* prep, const StateAddr& sa, int64_t B,
-                      float* act_l1, float* act_l2, hipStream_t s) {
+                      float* act_l1, float* act_l2, hipStream_t s, uint32_t* l2m) {
   if (!prep) return a3c_set_error(A3C_ERR_INVALID, "a3c_conv12_launch", "prepared forward weights missing");
   const uint16_t* w1s = (const uint16_t*)prep;
   const bool ew = !a3c_shared_gpu();
   // overlap mode: the 60 KB u8-plane variant (co-resides with the backward's workgroups)
   static const int env_u8 = getenv("A3C_C12_U8") ? atoi(getenv("A3C_C12_U8")) : -1;
   const bool u8 = env_u8 >= 0 ? env_u8 != 0 : !ew;
-#define CONV12_ARGS sa, B, w1s, P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2
+#define CONV12_ARGS sa, B, w1s, P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2, l2m
 #define CONV12_GO(S, E, U) \
   hipLaunchKernelGGL((k_conv12_fwd<S, E, U>), dim3((unsigned)B), dim3(512), U ? CONV12_SMEM_U8 : CONV12_SMEM, s, CONV12_ARGS)
   if (u8) {
