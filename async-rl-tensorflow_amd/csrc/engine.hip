@@ -1371,6 +1371,7 @@ static std::vector<StateRegion> state_regions(const a3c_engine* e) {
       add(sl.terms, nE);
       add(sl.z, (nE + E) * zs * 4); add(sl.R_buf, nE * 4);
       add(sl.act_l1, nE * C1_P * C1_N * 4); add(sl.act_l2, nE * FLAT * 4); add(sl.act_l3, nE * FC * 4);
+      add(sl.l2m, nE * C2_Q * 4);     // (the pending backward's dl2 mask)
     }
     if (e->L.lstm) {
       add(sl.lh, nE * LSTM_U * 4); add(sl.lc, nE * LSTM_U * 4);
@@ -1386,7 +1387,7 @@ static std::vector<StateRegion> state_regions(const a3c_engine* e) {
 
 static StateHeader state_header(const a3c_engine* e) {
   StateHeader h = {};
-  h.magic = STATE_MAGIC; h.version = 1;
+  h.magic = STATE_MAGIC; h.version = 2;   // 2: + the l2 ReLU bits of the rollout in flight
   h.E = e->E; h.n = e->n; h.R = e->R; h.algo = e->L.algo; h.A = e->L.A; h.lstm = e->L.lstm ? 1 : 0;
   h.overlap = e->overlap; h.world = e->cfg.world_size; h.frame84 = e->frame84;
   h.env_id_base = e->cfg.env_id_base; h.seed = e->cfg.seed;   // the env shard and its random streams
