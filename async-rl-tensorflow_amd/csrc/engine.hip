@@ -836,6 +836,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
 }
 #endif
 
+// the dl2 epilogue reads the forward's ReLU bits (A3C_L2BITS=0: re-read l2 itself; an A/B knob)
+static bool l2bits_on() {
+  static const bool on = !getenv("A3C_L2BITS") || atoi(getenv("A3C_L2BITS")) != 0;
+  return on;
+}
+
 static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
 #ifdef A3C_HOG
@@ -906,7 +912,7 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
                            sl.actions, sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra,
                            fork && !e->split ? e->gs : nullptr, fork && !e->split ? e->ev_gfork : nullptr,
                            fork && !e->split ? e->ev_gjoin : nullptr, L.lstm ? &lb : nullptr, &sf,
-                           e->split ? &sp : nullptr, sl.l2m);
+                           e->split ? &sp : nullptr, l2bits_on() ? sl.l2m : nullptr);
   if (rc) return rc;
   if (c.world_size > 1 && !e->split) {
     // multi-GPU: clip this worker's gradient (agent.py:319) before the cross-GPU exchange
