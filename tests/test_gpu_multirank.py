@@ -388,6 +388,7 @@ def test_hogwild_sharded_ps(world, lockstep, cfg):
     for it in range(ITERS):
         for e in engs:          # every engine of an iteration uses the start-of-iteration params
             e.params.copy_(w)
+        for e in engs:
             e.rollout_grad()
             lib().a3c_rmsprop_range(ptr(w), ptr(ms), ptr(mom), ptr(e.grads), w.numel(), ctypes.c_void_p(e.sched_ptr),
                                     0.0, 0.99, 0.0, 0.1, stream_handle())
