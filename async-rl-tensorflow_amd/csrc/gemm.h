@@ -35,6 +35,10 @@ struct GemmArgs {
   // a3c_gemm: 128x128 tiles (k_gemm_f32_big: a quarter of the workgroups, each four times the
   // work) -- fewer workgroups resident beside a concurrent kernel.  Speed only (bit-identical).
   int big;
+  // a3c_gemm: 4 = split K over 4 groups of 4 waves inside each 64x64-tile workgroup
+  // (k_gemm_f32_wks), folded in LDS -- nsplit is then 1 (no slab).  Not bit-identical to the
+  // slab split (another summation grouping), deterministic.
+  int wg_split;
 };
 
 int a3c_gemm(bool a_kcontig, bool b_ncontig, GemmArgs g, hipStream_t s);

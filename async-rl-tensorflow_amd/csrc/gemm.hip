@@ -111,6 +111,106 @@ __device__ inline void gemm_tile(const GemmArgs& g, int bx, int by, int bz, floa
   if (do_colsum && tid < BN && n0 + tid < g.N) g.colsum[(int64_t)ks * g.N + n0 + tid] = csum;
 }
 
+// One 64x64 tile per workgroup with the K range split across KS groups of 4 waves inside the
+// workgroup (256 KS threads): group q accumulates k-tiles [q T, (q+1) T) with its own LDS
+// operand buffers, then the partial tiles are folded through LDS in the fixed order
+// ((acc_0 + acc_1) + acc_2) + ... and group 0 stores C (and the column sums of B) once: split-K
+// without slabs in HBM and without a separate fold kernel (the backward's fc weight GEMM,
+// K = n E = 1280).  Deterministic; every group runs the same trip count (k-tiles past K load zeros,
+// whose products add exact zeros).
+template <bool A_KC, bool B_NC, int KS>
+__global__ void __launch_bounds__(256 * KS) k_gemm_f32_wks(GemmArgs g) {
+  WGLOG(5);
+  __shared__ __attribute__((aligned(16))) float As[KS][BK][BM + PAD];
+  __shared__ __attribute__((aligned(16))) float Bs[KS][BK][BN + PAD];
+  const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int ktiles = (g.K + BK - 1) / BK, per = (ktiles + KS - 1) / KS;
+  const int kbeg = grp * per * BK, kend = min(g.K, kbeg + per * BK);
+  const bool do_colsum = g.colsum != nullptr && blockIdx.y == 0;
+  int a_r, a_c, b_r, b_c;
+  if (A_KC) { a_r = tid >> 2; a_c = (tid & 3) * 4; } else { a_r = tid >> 4; a_c = (tid & 15) * 4; }
+  if (B_NC) { b_r = tid >> 4; b_c = (tid & 15) * 4; } else { b_r = tid >> 2; b_c = (tid & 3) * 4; }
+  auto load_a = [&](int k0) -> f32x4 {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (A_KC) {
+      int m = m0 + a_r, k = k0 + a_c;
+      if (m < g.M && k < kend) v = *(const f32x4*)(g.A + (int64_t)m * g.lda + k);
+    } else {
+      int k = k0 + a_r, m = m0 + a_c;
+      if (k < kend && m < g.M) v = *(const f32x4*)(g.A + (int64_t)k * g.lda + m);
+    }
+    return v;
+  };
+  auto load_b = [&](int k0) -> f32x4 {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (B_NC) {
+      int k = k0 + b_r, n = n0 + b_c;
+      if (k < kend && n < g.N) v = *(const f32x4*)(g.B + (int64_t)k * g.ldb + n);
+    } else {
+      int n = n0 + b_r, k = k0 + b_c;
+      if (n < g.N && k < kend) v = *(const f32x4*)(g.B + (int64_t)n * g.ldb + k);
+    }
+    return v;
+  };
+  float (&as)[BK][BM + PAD] = As[grp];
+  float (&bs)[BK][BN + PAD] = Bs[grp];
+  f32x16 acc = {};
+  float csum = 0.f;
+  f32x4 ra = load_a(kbeg), rb = load_b(kbeg);
+  for (int it = 0; it < per; ++it) {
+    const int k0 = kbeg + it * BK;
+    __syncthreads();
+    if (A_KC) { as[a_c][a_r] = ra[0]; as[a_c + 1][a_r] = ra[1]; as[a_c + 2][a_r] = ra[2]; as[a_c + 3][a_r] = ra[3]; }
+    else      { *(f32x4*)&as[a_r][a_c] = ra; }
+    if (B_NC) { *(f32x4*)&bs[b_r][b_c] = rb; }
+    else      { bs[b_c][b_r] = rb[0]; bs[b_c + 1][b_r] = rb[1]; bs[b_c + 2][b_r] = rb[2]; bs[b_c + 3][b_r] = rb[3]; }
+    __syncthreads();
+    if (it + 1 < per) { ra = load_a(k0 + BK); rb = load_b(k0 + BK); }
+    if (do_colsum && tid < BN) {
+#pragma unroll
+      for (int k = 0; k < BK; ++k) csum += bs[k][tid];
+    }
+    const int kh = lane >> 5, c = lane & 31;
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(as[2 * kk + kh][wm * 32 + c], bs[2 * kk + kh][wn * 32 + c], acc, 0, 0, 0);
+  }
+  // fold the groups' partial tiles in order through LDS (the operand buffers, free now)
+  static_assert(KS * BK * (BM + PAD) >= 16 * 256 + BN, "fold buffer");
+  float* fold = &As[0][0][0];
+  for (int q = 1; q < KS; ++q) {
+    __syncthreads();
+    if (grp == q) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) fold[r * 256 + tid] = acc[r];
+      if (do_colsum && tid < BN) fold[16 * 256 + tid] = csum;
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += fold[r * 256 + tid];
+      if (do_colsum && tid < BN) csum += fold[16 * 256 + tid];
+    }
+  }
+  if (grp != 0) return;
+  const int col = n0 + wn * 32 + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (row < g.M && col < g.N) {
+      float v = acc[r];
+      if (g.epi == EPI_BIAS_RELU) v = fmaxf(v + g.bias[col], 0.f);
+      else if (g.epi == EPI_BIAS) v = v + g.bias[col];
+      else if (g.epi == EPI_MASK) v = g.mask[(int64_t)row * g.ldm + col] > 0.f ? v : 0.f;
+      else if (g.epi == EPI_MASKBITS) v = (g.maskbits[(int64_t)row * g.ldm + (col >> 5)] >> (col & 31)) & 1u ? v : 0.f;
+      g.C[(int64_t)row * g.ldc + col] = v;
+    }
+  }
+  if (do_colsum && tid < BN && n0 + tid < g.N) g.colsum[n0 + tid] = csum;
+}
+
 // 128x128 tile of C = A B over K-chunk blockIdx.z: 4 waves (2 x 2), each a 64x64 block as 2 x 2
 // v_mfma_f32_32x32x2f32 tiles; operands LDS-staged BK = 16 deep with a register prefetch of the
 // next K step, two f32x4 of A and two of B per thread; split-K partials to the slab and the
@@ -375,6 +475,19 @@ int a3c_gemm_reduce(const GemmArgs& g, hipStream_t s) {
 
 int a3c_gemm(bool a_kc, bool b_nc, GemmArgs g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return 0;
+  if (g.wg_split == 4) {   // in-workgroup split-K (k_gemm_f32_wks): no slab, no fold kernel
+    g.nsplit = 1;
+    int rc = gemm_setup(a_kc, b_nc, g);
+    if (rc) return rc;
+    const dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, 1);
+    if (a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_wks<true, true, 4>), grid, dim3(1024), 0, s, g);
+    else if (a_kc && !b_nc) hipLaunchKernelGGL((k_gemm_f32_wks<true, false, 4>), grid, dim3(1024), 0, s, g);
+    else if (!a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_wks<false, true, 4>), grid, dim3(1024), 0, s, g);
+    else hipLaunchKernelGGL((k_gemm_f32_wks<false, false, 4>), grid, dim3(1024), 0, s, g);
+    A3C_CHECK(hipGetLastError());
+    return 0;
+  }
+  if (g.wg_split > 1) return a3c_set_error(A3C_ERR_INVALID, "a3c_gemm", "wg_split: 4 only");
   int rc = gemm_setup(a_kc, b_nc, g);
   if (rc) return rc;
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, g.nsplit);

@@ -796,6 +796,11 @@ int a3c_fused_tab(const NetLayout& L, TensorTab* tt) {
 // ---------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------
+static bool fc_wks_on() {
+  static const bool on = !getenv("A3C_FC_WKS") || atoi(getenv("A3C_FC_WKS")) != 0;
+  return on;
+}
+
 BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   BwdPlan p;
   int64_t o = 0;
@@ -822,7 +827,9 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   const int nwg_alloc = std::max(count(nwg_shared, per_alloc), count(nwg_own, per_alloc));
   p.nwg = count(a3c_shared_gpu() ? nwg_shared : nwg_own, p.per_wg);
   p.head_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FC, L.zs, (int)B, 128));
-  p.fc_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FLAT, FC, (int)B, 512));
+  // the fc weight GEMM (K = B) splits K inside its workgroups (k_gemm_f32_wks): no slab round trip
+  // through HBM and no fold kernel; A3C_FC_WKS=0: the split-K slabs + k_reduce_slabs
+  p.fc_split = fc_wks_on() ? 1 : a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FLAT, FC, (int)B, 512));
   p.dz = take(B * L.zs);
   p.dh3 = take(B * FC);
   p.dl2 = take(B * FLAT);
@@ -982,6 +989,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   gf.C = grads + L.off[T_FCW]; gf.ldc = FC;
   gf.M = FLAT; gf.N = FC; gf.K = (int)B;
   gf.epi = EPI_STORE; gf.slab = ws + p.fcslab; gf.nsplit = p.fc_split; gf.colsum = ws + p.fccol;
+  gf.wg_split = fc_wks_on() ? 4 : 0;
   gf.xcd = xcd_gemm() ? 1 : 0;          // the 4 column tiles of an l2 strip on one XCD
   // dl2[B][2592] = (dl3 W^T) * (l2 > 0)
   GemmArgs gd = {};
@@ -1019,7 +1027,8 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   // and so do the folds moved behind the conv backward alone (A3C_FOLD_LATE: 4.62M -> 4.45M)
   static const int env_multi = getenv("A3C_GEMM_MULTI") ? atoi(getenv("A3C_GEMM_MULTI")) : -1;
   static const int env_late = getenv("A3C_FOLD_LATE") ? atoi(getenv("A3C_FOLD_LATE")) : -1;
-  const bool multi = env_multi >= 0 ? env_multi != 0 : !a3c_shared_gpu() || bwd_bound_knob();
+  // (the in-workgroup split-K fc GEMM is a kernel of its own: no single three-GEMM launch then)
+  const bool multi = (env_multi >= 0 ? env_multi != 0 : !a3c_shared_gpu() || bwd_bound_knob()) && !gf.wg_split;
   const bool late = env_late >= 0 ? env_late != 0 : multi;
   if (!fork && (multi || late)) {
     // the weight-gradient split-K folds go after the conv backward (only the clip / apply read
