@@ -167,6 +167,33 @@ __device__ inline int dl2_col(int co) { return 2 * (co & 15) + (co >> 4); }
 #define CB_DLB_LD 480
 #define CB_DLB (3 * C1_N * CB_DLB_LD * 2)    // 46080
 __device__ inline int dlb_slot(int G, int n) { return 4 * (G >> 2) + ((G + ((n >> 1) & 2)) & 3); }
+// Phase (c)'s schedule of the 60 position blocks G = 3 oy + blk (8 positions ox = 8 blk .. +7 of
+// output row oy) over its 15 K-chunks x 4 lane groups j4 (round 4).  The x-plane reads are
+// ds_read_b32 pairs serviced in lane groups {0-31} (j4 0, 1) and {32-63} (j4 2, 3), bank = dword
+// mod 32; a lane's (cin, kernel row) offsets cover 16 banks, and the other j4 of its group covers
+// the other 16 only if the two blocks sit 16 dwords apart mod 32: row oy's blocks 0 and 2, or block 1
+// of rows 4 apart (the old G = 4 c + j4 paired blocks 8 or 4 dwords apart: every read 2-way
+// conflicted).  28 of the 30 pairs are conflict-free (rows 16-19's block 1 pair up with Delta 20):
+// the x reads' LDS cycles 480 -> 256 per wave and sample (tools/lds_bank_sim.py).  The dl1 terms
+// of block G are stored at slot index cb_fmap(G) = 4 c + j4 of its place in this schedule, so the
+// term reads (ds_read_b128, dlb_slot(4 c + j4, n)) keep their conflict-free pattern.
+__device__ inline void cb_block(int c, int j4, int& oy, int& blk) {
+  if (c < 10) {
+    oy = 2 * c + (j4 >> 1);
+    blk = 2 * (j4 & 1);
+  } else {
+    const int i = c - 10;
+    oy = i < 4 ? 8 * (i >> 1) + 2 * (i & 1) + (j4 >> 1) + 4 * (j4 & 1) : 16 + 2 * (j4 >> 1) + (j4 & 1);
+    blk = 1;
+  }
+}
+__device__ inline int cb_fmap(int G) {      // the inverse of cb_block: 4 c + j4 of block G
+  const int oy = G / 3, blk = G - 3 * oy;
+  if (blk != 1) return 2 * oy + (blk >> 1);
+  if (oy >= 16) return 56 + (oy - 16);
+  const int local = oy & 7, rem = local & 3;
+  return 4 * (10 + 2 * (oy >> 3) + (rem >> 1)) + 2 * (rem & 1) + ((local >> 2) & 1);
+}
 // l1s | dl2s | red, overlaid after phase (b) by dlb
 constexpr int cb_tail(bool lx) {
   return cb_l1_bytes(lx) + CB_DL2 + CB_RED > CB_DLB ? cb_l1_bytes(lx) + CB_DL2 + CB_RED : CB_DLB;
@@ -527,7 +554,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
           const float r1 = v[i] - (float)h;
           const __bf16 m = (__bf16)r1;
           const __bf16 l = (__bf16)(r1 - (float)m);
-          __bf16* d = (__bf16*)dlb + n * CB_DLB_LD + 8 * dlb_slot(k >> 3, n) + (k & 7);
+          __bf16* d = (__bf16*)dlb + n * CB_DLB_LD + 8 * dlb_slot(cb_fmap(k >> 3), n) + (k & 7);
           d[0] = h;
           d[C1_N * CB_DLB_LD] = m;
           d[2 * C1_N * CB_DLB_LD] = l;
@@ -567,7 +594,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
             mm[q] = __builtin_bit_cast(uint16_t, m);
             ll[q] = __builtin_bit_cast(uint16_t, l);
           }
-          uint32_t* d = (uint32_t*)(dlb + n * CB_DLB_LD + 8 * dlb_slot(k >> 3, n) + (k & 7));
+          uint32_t* d = (uint32_t*)(dlb + n * CB_DLB_LD + 8 * dlb_slot(cb_fmap(k >> 3), n) + (k & 7));
           d[0] = hh[0] | (hh[1] << 16);
           d[C1_N * CB_DLB_LD / 2] = mm[0] | (mm[1] << 16);
           d[C1_N * CB_DLB_LD] = ll[0] | (ll[1] << 16);
@@ -577,7 +604,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     // zero padding k = 24 oy + 20..23 (slot 3 oy + 2, elements 4..7) of every term row
     for (int i = tid; i < 3 * C1_N * C1_O; i += NT) {
       const int row = i / C1_O, oy = i - row * C1_O;
-      *(uint2*)(dlb + row * CB_DLB_LD + 8 * dlb_slot(3 * oy + 2, row & 15) + 4) = make_uint2(0u, 0u);
+      *(uint2*)(dlb + row * CB_DLB_LD + 8 * dlb_slot(cb_fmap(3 * oy + 2), row & 15) + 4) = make_uint2(0u, 0u);
     }
     if constexpr (!DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's x8 DMA landed
     lds_barrier();   // dl1 terms complete (and every wave's x8 DMA)
@@ -586,19 +613,19 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     // ---- (c) dW1[(kh,kw,cin)][n] += sum_p x[cin][4oy+kh][4ox+kw] * dl1[p][n]  (x unscaled) ----
     // v_mfma_f32_16x16x32_bf16: a u8 pixel is exact in bf16, dl1 = three bf16 terms, so every
     // product is exact in the fp32 accumulator.  K = 15 chunks of 32 padded positions: lane group
-    // g takes 8 consecutive ox of (oy, ox block) G = 4 chunk + g (oy = G / 3, ox = 8 (G % 3) + j).
+    // g takes 8 consecutive ox of block (oy, blk) = cb_block(chunk, g) (ox = 8 blk + j).
     // One dword of x holds the pixels of kw & 3 = 0..3 for one ox: 8 dwords feed the 4 tiles.
     // operands of chunk c: 8 x dwords and the 3 dl1-term fragments (next chunk's prefetched
     // while this one's MFMAs run)
     auto load_chunk = [&](int c, uint32_t (&d)[8], bf16x8 (&bv)[3]) {
-      const int G = 4 * c + j4;
-      const int oy = G / 3, blk = G - 3 * oy;
+      int oy, blk;
+      cb_block(c, j4, oy, blk);                 // (the bank-spread schedule above)
       const uint32_t* xp = (const uint32_t*)(x8 + xoff_c + 4 * oy * IMG + 32 * blk);
 #pragma unroll
       for (int j = 0; j < 8; ++j) d[j] = xp[j];
 #pragma unroll
       for (int term = 0; term < 3; ++term)
-        bv[term] = *(const bf16x8*)(dlb + (term * C1_N + i16) * CB_DLB_LD + 8 * dlb_slot(G, i16));
+        bv[term] = *(const bf16x8*)(dlb + (term * C1_N + i16) * CB_DLB_LD + 8 * dlb_slot(4 * c + j4, i16));
     };
     auto mma_chunk = [&](const uint32_t (&d)[8], const bf16x8 (&bt)[3]) {
 #pragma unroll

@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""LDS bank-conflict model of k_conv_bwd's phase (c) operand reads (csrc/net_bwd.hip, load_chunk).
+
+Per MI355X_MICROARCH.md §LDS: ds_read_b32 (and each half of ds_read2_b32) is serviced in lane
+groups {0-31}, {32-63} with bank = dword mod 32; ds_read_b128 in the four 16-lane groups listed
+below with bank = dword mod 64; each extra distinct dword on a busy bank adds one cycle.
+
+Prints the LDS-array cycles per wave and sample of the x-plane reads (8 dwords per lane per
+chunk, 15 chunks) and of the dl1-term reads (3 b128 per chunk) for the round-3 schedule
+(block G = 4 c + j4) and the round-4 one (cb_block / cb_fmap): x reads 480 -> 256 cycles, the
+term reads unchanged at the conflict-free 60 per term.
+"""
+import collections
+
+PLANE, IMG = 7056, 84
+B128_GROUPS = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+               list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32)),
+               list(range(32, 36)) + list(range(44, 48)) + list(range(52, 60)),
+               list(range(36, 44)) + list(range(48, 52)) + list(range(60, 64))]
+
+
+def dlb_slot(G, n):
+    return 4 * (G >> 2) + ((G + ((n >> 1) & 2)) & 3)
+
+
+def cycles(addrs, groups, nbanks, width):
+    tot = 0
+    for g in groups:
+        banks = collections.defaultdict(set)
+        for lane in g:
+            for w in range(width):
+                banks[(addrs[lane] + w) % nbanks].add(addrs[lane] + w)
+        tot += max(len(v) for v in banks.values())
+    return tot
+
+
+def x_cycles(block, w4):
+    """x-plane reads of one wave (w4 = wave & 3) over the 15 chunks; block(c, j4) -> G."""
+    tot = 0
+    for c in range(15):
+        for j in range(8):
+            addrs = []
+            for lane in range(64):
+                i16, j4 = lane & 15, lane >> 4
+                oy, blk = divmod(block(c, j4), 3)
+                byte = ((i16 & 3) * PLANE + (4 * (w4 >> 1) + (i16 >> 2)) * IMG + 4 * (w4 & 1) + 4 * oy * IMG
+                        + 32 * blk + 4 * j)
+                addrs.append(byte // 4)
+            tot += cycles(addrs, [range(0, 32), range(32, 64)], 32, 1)
+    return tot
+
+
+def term_cycles(slot_of):
+    """dl1-term b128 reads of one wave for one term; slot_of(c, j4) -> slot index."""
+    tot = 0
+    for c in range(15):
+        addrs = [((lane & 15) * 480 + 8 * dlb_slot(slot_of(c, lane >> 4), lane & 15)) // 2 for lane in range(64)]
+        tot += cycles(addrs, B128_GROUPS, 64, 4)
+    return tot
+
+
+def r4_block(c, j4):          # cb_block
+    if c < 10:
+        return 3 * (2 * c + (j4 >> 1)) + 2 * (j4 & 1)
+    i = c - 10
+    oy = 8 * (i >> 1) + 2 * (i & 1) + (j4 >> 1) + 4 * (j4 & 1) if i < 4 else 16 + 2 * (j4 >> 1) + (j4 & 1)
+    return 3 * oy + 1
+
+
+def r4_fmap(G):               # cb_fmap
+    oy, blk = divmod(G, 3)
+    if blk != 1:
+        return 2 * oy + (blk >> 1)
+    if oy >= 16:
+        return 56 + (oy - 16)
+    local = oy & 7
+    rem = local & 3
+    return 4 * (10 + 2 * (oy >> 3) + (rem >> 1)) + 2 * (rem & 1) + ((local >> 2) & 1)
+
+
+if __name__ == '__main__':
+    old = lambda c, j4: 4 * c + j4                                   # noqa: E731
+    assert sorted(r4_block(c, j) for c in range(15) for j in range(4)) == list(range(60))
+    assert all(r4_fmap(r4_block(c, j)) == 4 * c + j for c in range(15) for j in range(4))
+    print('x-plane reads, LDS cycles per wave per sample (waves 0..3):')
+    print('  round 3 (G = 4c + j4):', [x_cycles(old, w) for w in range(4)], ' conflict-free: 240')
+    print('  round 4 (cb_block):   ', [x_cycles(r4_block, w) for w in range(4)])
+    print('dl1-term reads per term: round 3', term_cycles(old), ', round 4', term_cycles(old),
+          '(slot 4c + j4 in both: the writer stores block G at cb_fmap(G)); conflict-free: 60')
