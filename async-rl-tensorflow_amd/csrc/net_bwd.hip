@@ -178,6 +178,9 @@ __device__ inline int dlb_slot(int G, int n) { return 4 * (G >> 2) + ((G + ((n >
 // of block G are stored at slot index cb_fmap(G) = 4 c + j4 of its place in this schedule, so the
 // term reads (ds_read_b128, dlb_slot(4 c + j4, n)) keep their conflict-free pattern.
 __device__ inline void cb_block(int c, int j4, int& oy, int& blk) {
+#ifdef CB_OLD_SCHED   // (A/B builds only: the round-3 schedule G = 4 c + j4)
+  oy = (4 * c + j4) / 3; blk = 4 * c + j4 - 3 * oy; return;
+#endif
   if (c < 10) {
     oy = 2 * c + (j4 >> 1);
     blk = 2 * (j4 & 1);
@@ -188,6 +191,9 @@ __device__ inline void cb_block(int c, int j4, int& oy, int& blk) {
   }
 }
 __device__ inline int cb_fmap(int G) {      // the inverse of cb_block: 4 c + j4 of block G
+#ifdef CB_OLD_SCHED
+  return G;
+#endif
   const int oy = G / 3, blk = G - 3 * oy;
   if (blk != 1) return 2 * oy + (blk >> 1);
   if (oy >= 16) return 56 + (oy - 16);
