@@ -246,6 +246,16 @@ __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_b
 #define CB_PH_OUT(dst) ((void)0)
 #endif
 
+#ifdef CB_PHB_PERM
+// Phase (b) (LX) position order within each M-tile: MFMA row m of tile mt is position 16 mt +
+// nibble m of cb_phb_perm[mt] (tile 6, which holds positions 96..99 and the clamped duplicates,
+// keeps the identity).  Found by a local search over the per-tile permutations for the fewest
+// LDS-array cycles of the tile's ds_read_b128 operand reads and its epilogue's ReLU-mask reads
+// over the four parity classes (tools/lds_bank_sim.py model): 2064 -> 1648 cycles per sample and
+// wave for tiles 0-5.  Any order is valid: A row m and D row m name the same position.
+__constant__ uint64_t cb_phb_perm[7] = {0x0c2af753d1b9864eull, 0xfa360b2795e48cd1ull, 0xfbe6c29783da1405ull, 0x3645eb1acd8f9072ull, 0xbe47851a63fc902dull, 0xa64893d57fe102bcull, 0xfedcba9876543210ull};
+#endif
+
 template <bool DMA, int NW, bool LX>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) k_conv_bwd(StateAddr sa, int64_t B, int per_wg,
                                                   const float* __restrict__ act_l1,
@@ -434,23 +444,41 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
     for (int u = 0; u < MTB; ++u) {
       const int mt = mt_lo + u;
       if (mt >= mt_hi) break;
+#ifdef CB_PHB_PERM
+      const uint64_t pm = cb_phb_perm[mt];
+      const int pc = 16 * mt + (int)((pm >> (4 * bi16)) & 15);
+#else
       const int pc = 16 * mt + bi16;
+#endif
       const int pcc = pc < 100 ? pc : 99;
       const int ay = pcc / 10, cx = pcc - ay * 10;
       const int base = ay * C2_O + cx;
+      int eo[4];
+      float msk[4];
+#ifdef CB_PHB_PERM
+      bool rv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {          // D row 4 j4 + r: its position's slot (clamped at 99)
+        const int pr = 16 * mt + (int)((pm >> (4 * (4 * bj4 + r))) & 15);
+        const int prc = pr < 100 ? pr : 99;
+        const int ayr = prc / 10, cxr = prc - ayr * 10;
+        eo[r] = ((2 * ayr + py) * C1_O + 2 * cxr + px) * L1LD + bi16;
+        rv[r] = pr < 100;
+        msk[r] = l1s[eo[r]];                    // l1 (the ReLU mask), before any write of the tile
+      }
+#else
       // epilogue slots of rows r = 0..3: p = p0 + 2 rr + 20 [cx0 + rr >= 10], rr = min(r, 99 - prc0)
       const int pr0 = 16 * mt + 4 * bj4;
       const int prc0 = pr0 < 100 ? pr0 : 99;
       const int ay0 = prc0 / 10, cx0 = prc0 - ay0 * 10;
       const int p0 = (2 * ay0 + py) * C1_O + 2 * cx0 + px;
-      int eo[4];
-      float msk[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rr = min(r, 99 - prc0);
         eo[r] = (p0 + 2 * rr + (cx0 + rr >= 10 ? 20 : 0)) * L1LD + bi16;
         msk[r] = l1s[eo[r]];                    // l1 (the ReLU mask), before any write of the tile
       }
+#endif
       int qo[4];
 #pragma unroll
       for (int dy = 0; dy < 2; ++dy)
@@ -483,7 +511,11 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2)
       for (int r = 0; r < 4; ++r) {
         const float g = msk[r] > 0.f ? acc[r] : 0.f;
         l1s[eo[r]] = g;                          // dl1 in place over l1 (this lane's own slot)
+#ifdef CB_PHB_PERM
+        db1acc = rv[r] ? db1acc + g : db1acc;
+#else
         db1acc = pr0 + r < 100 ? db1acc + g : db1acc;
+#endif
       }
     }
     } else {
