@@ -177,8 +177,12 @@ __device__ inline int dlb_slot(int G, int n) { return 4 * (G >> 2) + ((G + ((n >
 // the x reads' LDS cycles 480 -> 256 per wave and sample (tools/lds_bank_sim.py).  The dl1 terms
 // of block G are stored at slot index cb_fmap(G) = 4 c + j4 of its place in this schedule, so the
 // term reads (ds_read_b128, dlb_slot(4 c + j4, n)) keep their conflict-free pattern.
+// Measured (profiles/round4_ab_cbsched.txt, 3 interleaved reps): slower -- conv backward alone
+// 92.4 vs 90.8 us, M1 4.72M vs 4.74M, M2 5.56M vs 5.63M env-steps/s: the x reads are not what
+// bounds phase (c), and the schedule's address math sits in its chain.  Kept behind
+// -DCB_BANK_SCHED; the default is the round-3 schedule (cb_block / cb_fmap the identity).
 __device__ inline void cb_block(int c, int j4, int& oy, int& blk) {
-#ifdef CB_OLD_SCHED   // (A/B builds only: the round-3 schedule G = 4 c + j4)
+#ifndef CB_BANK_SCHED   // default: the round-3 schedule G = 4 c + j4 (measured faster, below)
   oy = (4 * c + j4) / 3; blk = 4 * c + j4 - 3 * oy; return;
 #endif
   if (c < 10) {
@@ -191,7 +195,7 @@ __device__ inline void cb_block(int c, int j4, int& oy, int& blk) {
   }
 }
 __device__ inline int cb_fmap(int G) {      // the inverse of cb_block: 4 c + j4 of block G
-#ifdef CB_OLD_SCHED
+#ifndef CB_BANK_SCHED
   return G;
 #endif
   const int oy = G / 3, blk = G - 3 * oy;

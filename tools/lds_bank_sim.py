@@ -7,8 +7,10 @@ below with bank = dword mod 64; each extra distinct dword on a busy bank adds on
 
 Prints the LDS-array cycles per wave and sample of the x-plane reads (8 dwords per lane per
 chunk, 15 chunks) and of the dl1-term reads (3 b128 per chunk) for the round-3 schedule
-(block G = 4 c + j4) and the round-4 one (cb_block / cb_fmap): x reads 480 -> 256 cycles, the
-term reads unchanged at the conflict-free 60 per term.
+(block G = 4 c + j4) and the round-4 one (cb_block / cb_fmap under -DCB_BANK_SCHED): x reads
+480 -> 256 cycles, the term reads unchanged at the conflict-free 60 per term.  Measured on the
+MI355X the bank-spread schedule ran slower (profiles/round4_ab_cbsched.txt), so the default build
+keeps the round-3 schedule: fewer modelled conflict cycles are not what bounds phase (c).
 """
 import collections
 
