@@ -85,7 +85,7 @@ struct LstmBwd {
   float* ws;                              // a3c_lstm_ws_floats(n, E) floats
 };
 
-BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B);
+BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B, bool wks = false);
 int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr& sa, int64_t B,
                         const float* act_l1, const float* act_l2, const float* act_l3,
                         const float* z, const int32_t* actions, const float* target, float beta,

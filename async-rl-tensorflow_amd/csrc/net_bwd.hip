@@ -870,7 +870,7 @@ static bool fc_wks_on() {
   return on;
 }
 
-BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
+BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B, bool wks) {
   BwdPlan p;
   int64_t o = 0;
   auto take = [&](int64_t floats) { int64_t r = o; o += (floats + 63) & ~(int64_t)63; return r; };
@@ -896,9 +896,11 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   const int nwg_alloc = std::max(count(nwg_shared, per_alloc), count(nwg_own, per_alloc));
   p.nwg = count(a3c_shared_gpu() ? nwg_shared : nwg_own, p.per_wg);
   p.head_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FC, L.zs, (int)B, 128));
-  // the fc weight GEMM (K = B) splits K inside its workgroups (k_gemm_f32_wks): no slab round trip
-  // through HBM and no fold kernel; A3C_FC_WKS=0: the split-K slabs + k_reduce_slabs
-  p.fc_split = fc_wks_on() ? 1 : a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FLAT, FC, (int)B, 512));
+  // wks: the fc weight GEMM (K = B) splits K inside its workgroups (k_gemm_f32_wks) -- no slab
+  // round trip through HBM, no fold kernel; else split-K slabs + k_reduce_slabs.  The slab and column
+  // sum buffers are sized for the slab form either way, so the offsets do not depend on it.
+  const int fc_split_slab = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(FLAT, FC, (int)B, 512));
+  p.fc_split = wks ? 1 : fc_split_slab;
   p.dz = take(B * L.zs);
   p.dh3 = take(B * FC);
   p.dl2 = take(B * FLAT);
@@ -906,8 +908,8 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B) {
   p.hgrad = take((int64_t)FC * L.zs);
   p.hcol = take((int64_t)p.head_split * L.zs);
   p.hslab = take(p.head_split > 1 ? (int64_t)p.head_split * FC * L.zs : 0);
-  p.fccol = take((int64_t)p.fc_split * FC);
-  p.fcslab = take(p.fc_split > 1 ? (int64_t)p.fc_split * FLAT * FC : 0);
+  p.fccol = take((int64_t)fc_split_slab * FC);
+  p.fcslab = take(fc_split_slab > 1 ? (int64_t)fc_split_slab * FLAT * FC : 0);
   p.cslab = take((int64_t)nwg_alloc * CB_SLAB);
   p.groups = p.nwg < 16 ? p.nwg : 16;
   p.cgroup = take((int64_t)16 * CB_SLAB);    // groups <= 16 in either mode
@@ -1011,7 +1013,16 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   ReturnsArgs ra = {};
   if (ra_in) ra = *ra_in;
   if (B <= 0) return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "B must be > 0");
-  const BwdPlan p = a3c_bwd_plan(L, B);
+  // sync mode: the three GEMMs in one launch (3.32M -> 3.41M env-steps/s), and so where the
+  // overlapped backward bounds the iteration (M2: 5.17-5.22M -> 5.38-5.39M); beside a rollout
+  // that bounds it the 1,420-workgroup launch slows it more than it gains (M1: 4.62M -> 4.45M),
+  // and so do the folds moved behind the conv backward alone (A3C_FOLD_LATE: 4.62M -> 4.45M)
+  static const int env_multi = getenv("A3C_GEMM_MULTI") ? atoi(getenv("A3C_GEMM_MULTI")) : -1;
+  const bool multi0 = env_multi >= 0 ? env_multi != 0 : !a3c_shared_gpu() || bwd_bound_knob();
+  // the in-workgroup split-K fc weight GEMM where its launch stands alone anyway: the M1 overlap
+  // backward and the split backward (several GPUs), not in the single three-GEMM launch
+  const bool wks = fc_wks_on() && (sp != nullptr || !multi0);
+  const BwdPlan p = a3c_bwd_plan(L, B, wks);
   const float* P = params;
   float* dz = ws + p.dz;
   float* dh3 = ws + p.dh3;
@@ -1058,7 +1069,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   gf.C = grads + L.off[T_FCW]; gf.ldc = FC;
   gf.M = FLAT; gf.N = FC; gf.K = (int)B;
   gf.epi = EPI_STORE; gf.slab = ws + p.fcslab; gf.nsplit = p.fc_split; gf.colsum = ws + p.fccol;
-  gf.wg_split = fc_wks_on() ? 4 : 0;
+  gf.wg_split = wks ? 4 : 0;
   gf.xcd = xcd_gemm() ? 1 : 0;          // the 4 column tiles of an l2 strip on one XCD
   // dl2[B][2592] = (dl3 W^T) * (l2 > 0)
   GemmArgs gd = {};
@@ -1090,14 +1101,8 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     if (!sf || fork) return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "split backward: fused norms, no fork");
     return backward_split(L, P, sa, B, act_l1, ws, s, p, gh, gf, gd, grads, terms, loss_out, sf, sp);
   }
-  // sync mode: the three GEMMs in one launch (3.32M -> 3.41M env-steps/s), and so where the
-  // overlapped backward bounds the iteration (M2: 5.17-5.22M -> 5.38-5.39M); beside a rollout
-  // that bounds it the 1,420-workgroup launch slows it more than it gains (M1: 4.62M -> 4.45M),
-  // and so do the folds moved behind the conv backward alone (A3C_FOLD_LATE: 4.62M -> 4.45M)
-  static const int env_multi = getenv("A3C_GEMM_MULTI") ? atoi(getenv("A3C_GEMM_MULTI")) : -1;
   static const int env_late = getenv("A3C_FOLD_LATE") ? atoi(getenv("A3C_FOLD_LATE")) : -1;
-  // (the in-workgroup split-K fc GEMM is a kernel of its own: no single three-GEMM launch then)
-  const bool multi = (env_multi >= 0 ? env_multi != 0 : !a3c_shared_gpu() || bwd_bound_knob()) && !gf.wg_split;
+  const bool multi = multi0 && !wks;
   const bool late = env_late >= 0 ? env_late != 0 : multi;
   if (!fork && (multi || late)) {
     // the weight-gradient split-K folds go after the conv backward (only the clip / apply read

@@ -162,8 +162,8 @@ def lib():
             raise RuntimeError(f'{LIB_PATH} not built: run __graft_entry__.build() or make -C csrc')
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            if name in MEASUREMENT_ONLY and not hasattr(L, name):
-                continue          # (an older build selected by A3C_LIB for an A/B: no span dumps)
+            if (name in MEASUREMENT_ONLY or os.environ.get('A3C_LIB')) and not hasattr(L, name):
+                continue          # (an older build selected by A3C_LIB for an A/B: no span dumps, ...)
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
