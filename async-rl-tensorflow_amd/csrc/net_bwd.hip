@@ -926,7 +926,12 @@ static int backward_split(const NetLayout& L, const float* P, const StateAddr& s
                           float* ws, hipStream_t s, const BwdPlan& p, GemmArgs gh, GemmArgs gf, GemmArgs gd,
                           float* grads, const float* terms, float* loss_out, const SumsqFused* sf, const SplitBwd* sp) {
   const bool a3c = L.algo == A3C_ALGO_A3C;
-  gh.defer_reduce = gf.defer_reduce = 0;
+  // the head weight GEMM's split-K partials are folded by the finalize segments (the same
+  // sum_strided order as k_reduce_slabs: bit-identical, one kernel fewer)
+  const float* hsrc = p.head_split > 1 ? ws + p.hslab : ws + p.hgrad;
+  const int64_t hstride = (int64_t)FC * L.zs;
+  gh.defer_reduce = 1;        // (the finalize folds the head slabs itself: hsrc below)
+  gf.defer_reduce = 0;
   gh.big = gf.big = gd.big = 0;
   int rc = a3c_gemm(false, true, gh, s);
   if (!rc) rc = a3c_gemm(false, true, gf, s);
@@ -952,10 +957,10 @@ static int backward_split(const NetLayout& L, const float* P, const StateAddr& s
     FinalizeSegs fs = {};
     segs(fs);
     seg(fs, ws + p.fccol, FC, p.fc_split, 1, 0, 0, FC, T_FCB, 0, 1.0f);
-    seg(fs, ws + p.hgrad, 0, 1, FC, L.zs, 0, L.A, T_HW, L.A, 1.0f);
+    seg(fs, hsrc, hstride, p.head_split, FC, L.zs, 0, L.A, T_HW, L.A, 1.0f);
     seg(fs, ws + p.hcol, L.zs, p.head_split, 1, 0, 0, L.A, T_HB, 0, 1.0f);
     if (a3c) {
-      seg(fs, ws + p.hgrad, 0, 1, FC, L.zs, L.A, 1, T_VW, 1, 1.0f);
+      seg(fs, hsrc, hstride, p.head_split, FC, L.zs, L.A, 1, T_VW, 1, 1.0f);
       seg(fs, ws + p.hcol, L.zs, p.head_split, 1, 0, L.A, 1, T_VB, 0, 1.0f);
     }
     for (int t = 0; t < L.nt; ++t) {
@@ -1062,6 +1067,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   gh.C = ws + p.hgrad; gh.ldc = L.zs;
   gh.M = FC; gh.N = L.zs; gh.K = (int)B;
   gh.epi = EPI_STORE; gh.slab = ws + p.hslab; gh.nsplit = p.head_split; gh.colsum = ws + p.hcol;
+  gh.defer_reduce = 1;                 // its split-K fold is the finalize's (segments over the slab)
   // fc weights: dW[2592][256] = l2^T dl3 -> grads directly ; db = colsum(dl3)
   GemmArgs gf = {};
   gf.A = act_l2; gf.lda = FLAT;
@@ -1118,8 +1124,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     if (rc) return rc;
     rc = a3c_conv_bwd_launch(L, P, sa, B, act_l1, dl2, ws, s);
     if (rc) return rc;
-    rc = a3c_gemm_reduce(gh, s);
-    if (!rc) rc = a3c_gemm_reduce(gf, s);
+    rc = a3c_gemm_reduce(gf, s);       // (gh: folded by the finalize)
     if (rc) return rc;
   } else {
 #ifdef A3C_MARKERS
@@ -1174,10 +1179,13 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   seg(cs + CB_OFF_W2, CB_SLAB, p.groups, 1, 0, 0, KC2 * C2_N, T_L2W, 0, 1.0f);
   seg(cs + CB_OFF_B2, CB_SLAB, p.groups, 1, 0, 0, C2_N, T_L2B, 0, 1.0f);
   seg(ws + p.fccol, FC, p.fc_split, 1, 0, 0, FC, T_FCB, 0, 1.0f);
-  seg(ws + p.hgrad, 0, 1, FC, L.zs, 0, L.A, T_HW, L.A, 1.0f);
+  // the head weight GEMM's split-K partials folded here (gh.defer_reduce): one kernel fewer
+  const float* hsrc = p.head_split > 1 ? ws + p.hslab : ws + p.hgrad;
+  const int64_t hstride = (int64_t)FC * L.zs;
+  seg(hsrc, hstride, p.head_split, FC, L.zs, 0, L.A, T_HW, L.A, 1.0f);
   seg(ws + p.hcol, L.zs, p.head_split, 1, 0, 0, L.A, T_HB, 0, 1.0f);
   if (a3c) {
-    seg(ws + p.hgrad, 0, 1, FC, L.zs, L.A, 1, T_VW, 1, 1.0f);
+    seg(hsrc, hstride, p.head_split, FC, L.zs, L.A, 1, T_VW, 1, 1.0f);
     seg(ws + p.hcol, L.zs, p.head_split, 1, 0, L.A, 1, T_VB, 0, 1.0f);
   }
   int nsumblk = 0;
