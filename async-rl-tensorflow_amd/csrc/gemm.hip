@@ -125,10 +125,21 @@ __global__ void __launch_bounds__(256 * KS) k_gemm_f32_wks(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float Bs[KS][BK][BN + PAD];
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (g.xcd == 1) {
+    // 1-D grid, XCD-grouped (speed only): the N tiles of M tile t get ids with id % 8 == t % 8, so
+    // under round-robin dispatch one XCD's L2 fetches the tile's A strip (the n E x 64 block of l2)
+    // for all of them instead of each N tile's XCD fetching it again; ids past the last tile exit
+    const int gx = (g.N + BN - 1) / BN, gy = (g.M + BM - 1) / BM;
+    const int id = blockIdx.x, slot = id >> 3;
+    by = 8 * (slot / gx) + (id & 7);
+    bx = slot % gx;
+    if (by >= gy) return;
+  }
+  const int m0 = by * BM, n0 = bx * BN;
   const int ktiles = (g.K + BK - 1) / BK, per = (ktiles + KS - 1) / KS;
   const int kbeg = grp * per * BK, kend = min(g.K, kbeg + per * BK);
-  const bool do_colsum = g.colsum != nullptr && blockIdx.y == 0;
+  const bool do_colsum = g.colsum != nullptr && by == 0;
   int a_r, a_c, b_r, b_c;
   if (A_KC) { a_r = tid >> 2; a_c = (tid & 3) * 4; } else { a_r = tid >> 4; a_c = (tid & 15) * 4; }
   if (B_NC) { b_r = tid >> 4; b_c = (tid & 15) * 4; } else { b_r = tid >> 2; b_c = (tid & 3) * 4; }
@@ -479,7 +490,10 @@ int a3c_gemm(bool a_kc, bool b_nc, GemmArgs g, hipStream_t s) {
     g.nsplit = 1;
     int rc = gemm_setup(a_kc, b_nc, g);
     if (rc) return rc;
-    const dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, 1);
+    const int gx = (g.N + BN - 1) / BN, gy = (g.M + BM - 1) / BM;
+    // g.xcd == 1: XCD-grouped 1-D grid (the kernel maps ids to tiles), else the plain 2-D grid
+    const dim3 grid = g.xcd == 1 ? dim3((unsigned)(8 * ((gy + 7) / 8) * gx)) : dim3(gx, gy, 1);
+    if (g.xcd != 0 && g.xcd != 1) return a3c_set_error(A3C_ERR_INVALID, "a3c_gemm", "wg_split: xcd 0 or 1");
     if (a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_wks<true, true, 4>), grid, dim3(1024), 0, s, g);
     else if (a_kc && !b_nc) hipLaunchKernelGGL((k_gemm_f32_wks<true, false, 4>), grid, dim3(1024), 0, s, g);
     else if (!a_kc && b_nc) hipLaunchKernelGGL((k_gemm_f32_wks<false, true, 4>), grid, dim3(1024), 0, s, g);
