@@ -203,7 +203,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   e->cfg = *cfg;
   if (a3c_make_layout(&cfg->net, &e->L) || cfg->num_envs < 1 || cfg->n_step < 1 || cfg->n_step > 64 ||
       cfg->num_frames < 1 || cfg->random_start < 1 || cfg->action_repeat < 1 || cfg->world_size < 1 ||
-      (cfg->overlap && cfg->net.algo != A3C_ALGO_A3C) || (cfg->overlap && cfg->external_env) ||
+      (cfg->overlap && cfg->external_env) || (cfg->overlap && cfg->net.lstm_units && cfg->net.algo != A3C_ALGO_A3C) ||
       (cfg->net.lstm_units && !cfg->overlap && cfg->n_step < 2)) {   // sync n=1 would read and
                                                                        // write one state buffer
     delete e;

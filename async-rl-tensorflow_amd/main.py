@@ -145,9 +145,9 @@ def run_engine(config, flags):
   host = flags.envs_on != 'device'
   if host and flags.update == 'hogwild':
     raise ValueError('--envs_on host/gym drives a synchronous engine; use --update sync or overlap')
-  overlap = flags.update == 'overlap' and flags.algo == 'a3c' and not host
+  overlap = flags.update == 'overlap' and not host
   if flags.update == 'overlap' and not overlap and rank == 0:
-    print('main.py: --update overlap needs the a3c algo and device envs; running the synchronous engine',
+    print('main.py: --update overlap needs device envs; running the synchronous engine',
           file=sys.stderr, flush=True)
   pool = make_host_pool(config, flags, E, A, lives, rank) if host else None
   eng = Engine(num_envs=E, n_step=flags.n_step, action_size=A, algo=flags.algo, start_lives=lives,

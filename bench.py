@@ -164,8 +164,6 @@ def main():
 
     A, lives = GAMES[args.game]
     E, n = args.envs, args.n_step
-    if args.algo == 'q' and args.update == 'overlap':
-        args.update = 'sync'              # the stale-1 pipeline is an A3C (policy-gradient) mode
     if args.lstm and args.algo != 'a3c':
         raise SystemExit('--lstm is an a3c head')
     host = args.env == 'host'

@@ -282,7 +282,7 @@ typedef struct a3c_engine_config {
   float ep_start, ep_end; int64_t ep_end_t, learn_start;  /* config.py:18-25         */
   int64_t target_q_update_step;   /* config.py:10 (4e4)                               */
   double discount;                /* config.py:9                                      */
-  int overlap;        /* 1 (a3c only): rollout k runs on an engine stream while the backward +
+  int overlap;        /* 1 (a3c, q; not with host envs): rollout k runs on an engine stream while the backward +
                         apply of rollout k-1 run on the caller's stream; rollout k uses the
                         parameters after update k-2 (A3C stale-parameter asynchrony, fixed
                         staleness 1).  0: synchronous rollout -> grad -> apply.          */

@@ -149,6 +149,16 @@ def test_overlap_stale_semantics_match_oracle(E, frame84):
     check_overlap_vs_oracle(6, E, 5, 0, rollouts=5, seed=77, learning_rate=3e-3, frame84=frame84)
 
 
+@pytest.mark.parametrize('E,tq', [(8, 100), (37, 2000)])
+def test_q_overlap_stale_semantics_match_oracle(E, tq):
+    """Async Q-learning on the stale-1 pipeline: rollout k acts epsilon-greedily with the
+    parameters after update k-2, and rollout k-1's TD targets are formed by its backward (after
+    rollout k) with the target network as it stands then; the target copy follows the apply's
+    global step (agent.py:166-167).  tq=100 at 40 env steps per update syncs on irregular updates."""
+    check_overlap_vs_oracle(6, E, 5, 0, rollouts=6, seed=55, learning_rate=3e-3, algo='q',
+                            target_q_update_step=tq)
+
+
 def test_stream_ordering_modes_are_bit_identical(monkeypatch):
     """Overlap pipeline: ordering the rollout and backward streams by stream wait-value operations
     on device counters (default) or by HIP events gives the same training, bit for bit."""

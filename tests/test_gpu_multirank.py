@@ -208,6 +208,8 @@ class _Oracle:
             acts = sl['actions'].cpu().numpy()
             out = ref.iterate(forced_actions=acts, grads=False)
             planes = rollout_planes(ref, c['n'])
+            if overlap and c['algo'] == 'q':      # s_{t+1} planes for the backward-time TD targets
+                out['next_states'] = np.concatenate([ref.states(ref.tau + t + 1) for t in range(c['n'])])
             if overlap:
                 ref.tau += c['n']                 # the rollout owns tau in overlap mode
             assert np.array_equal(sl['rewards'].cpu().numpy(), out['rewards']), (k, r)
@@ -226,7 +228,12 @@ class _Oracle:
             Pj, planes, out = self.hist[r][j]
             sl = eng.slot(j & 1) if overlap else eng
             ret = (sl['returns'] if overlap else sl.returns).cpu().numpy()
-            np.testing.assert_allclose(ret, out['target'], rtol=1e-5, atol=1e-5)
+            want = out['target']
+            if 'next_states' in out:              # q overlap: the target net of backward time
+                qn = Rc.forward(self.refs[r].tparams, out['next_states'], 'q', keep=False)['z']
+                want = Rc.td_target(out['rewards'].reshape(-1), out['terminals'].reshape(-1), qn.astype(np.float32),
+                                    self.refs[r].h['discount']).astype(np.float32).reshape(c['n'], c['E'])
+            np.testing.assert_allclose(ret, want, rtol=1e-5, atol=1e-5)
             losses, g = same_act_grads(sl, planes, Pj, c['algo'], c['A'], c['n'], c['E'], ret)
             assert_losses(eng.loss.cpu().numpy(), losses, c['algo'], (j, r))
             clipped = {kk: Rc.clip_by_norm(v, 40.0) for kk, v in g.items()}
@@ -259,9 +266,10 @@ class _Oracle:
     (2, False, {}, False), (2, True, {}, False), (4, False, {}, True), (4, True, {}, False),
     (4, True, dict(A=4, lives=5), True), (4, False, dict(A=6, lives=3, lstm=True, E=16), False),
     (4, False, dict(algo='q', A=6, lives=3), True), (2, False, dict(algo='q', A=4, lives=5, n=8), False),
-    (4, True, dict(split=0), False), (2, False, dict(split=0), False)],
+    (4, True, dict(split=0), False), (2, False, dict(split=0), False),
+    (2, True, dict(algo='q', A=6, lives=3, tq=700), True), (4, True, dict(algo='q', A=4, lives=5, tq=700), False)],
     ids=['w2-sync', 'w2-overlap', 'w4-sync', 'w4-overlap', 'w4-breakout-overlap', 'w4-lstm-sync', 'w4-q-sync',
-         'w2-q-breakout-sync', 'w4-overlap-onephase', 'w2-sync-onephase'])
+         'w2-q-breakout-sync', 'w4-overlap-onephase', 'w2-sync-onephase', 'w2-q-overlap', 'w4-q-breakout-overlap'])
 def test_partitioned_ps_ranks(world, overlap, cfg, oracle):
     """`world` ranks on one GPU (gloo, host-staged collectives) run the default multi-GPU exchange:
     all-to-all of the clipped gradients, each rank's W sequential RMSProp steps on its range,
