@@ -342,16 +342,17 @@ def main():
     if rank == 0:
         steps_total = world * E * n * args.steps
         coll = 'RCCL' if args.backend == 'nccl' else 'gloo, host-staged'
+        NETNAME = 'A3C' if args.algo == 'a3c' else 'one-step Q'
         line = {
             'metric': METRIC, 'value': round(steps_total / el, 1), 'unit': 'env-steps/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 4),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
             'data': (f'synthetic: HBM-resident hashed {"pre-sized 84x84 grey" if args.frames84 else "RGB 210x160x3"} '
                      f'frame pool ({args.frames} frames) stepped by the on-device synthetic Atari env; random-init '
-                     f'NIPS A3C conv net' if not host else
+                     f'NIPS {NETNAME} conv net' if not host else
                      f'synthetic: host-stepped emulator ({args.host_threads} threads, a3c_hostenv) writing raw RGB '
                      f'210x160x3 frames into pinned buffers, PCIe H2D every step (PCIe-inclusive); random-init '
-                     f'NIPS A3C conv net'),
+                     f'NIPS {NETNAME} conv net'),
             'config': {'workload': f'{args.game}, {E} envs batched per MI355X, n-step={n}, '
                                    f'{"A3C" if args.algo == "a3c" else "one-step Q"} conv net (nips trunk'
                                    f'{" + 256-cell LSTM head" if args.lstm else ""})',
@@ -368,7 +369,7 @@ def main():
                                        if args.exchange == 'sequential' else
                                        f'dp{world} all-reduce ({coll}) of per-worker-clipped grads, one summed step')
                        if world > 1 else 'dp1', 'hipgraph': args.graph and not args.no_graph,
-                       'update': {'overlap': 'overlap: rollout k uses params after update k-2 (A3C stale-1 async), '
+                       'update': {'overlap': 'overlap: rollout k uses params after update k-2 (stale-1 async), '
                                              'backward+apply of k-1 concurrent with rollout k',
                                   'sync': 'synchronous: rollout -> backward -> apply',
                                   'hogwild': 'hogwild: sharded lock-free parameter server (reference PS semantics)'
