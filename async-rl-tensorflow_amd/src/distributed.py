@@ -78,8 +78,12 @@ class PartitionedPS:
 
     owns_apply = True
 
-    def __init__(self, total, group=None, device='cuda'):
+    def __init__(self, total, group=None, device='cuda', split=None):
+        """split: run the two-phase exchange when the engine offers a split point (True), never
+        (False), or (None) only where the collectives run on the device -- host-staged gloo
+        collectives block the host at every staging copy, so two phases there only add stalls."""
         self.group = group
+        self.split = split
         self.world, self.rank = _world(group), _rank(group)
         self.total = int(total)
         self.shard, self.lo, self.n = shard_ranges(self.total, self.world)
@@ -130,7 +134,9 @@ class PartitionedPS:
 
     def apply(self, eng):
         cut = getattr(eng, 'split_point', 0) if self.world > 1 else 0
-        if cut:
+        if cut and self.split is None:
+            cut = 0 if _host_staged(eng.grads, self.group) else cut
+        if cut and self.split is not False:
             return self._apply_split(eng, cut)
         r = self.rank
         self.all_to_all(eng.grads)

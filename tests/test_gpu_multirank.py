@@ -169,7 +169,7 @@ def _pps_worker(rank, world, port, out, overlap, cfg):
     eng = _make(rank, world, overlap, cfg)
     q = _cfg(cfg)['algo'] == 'q'
     assert (eng.split_point > 0) == bool(_cfg(cfg)['split'])
-    ps = PartitionedPS(eng.params.numel())
+    ps = PartitionedPS(eng.params.numel(), split=True)     # two phases on host-staged gloo too
     recs = []
     for _ in range(ITERS):
         eng.iterate(exchange=ps)
