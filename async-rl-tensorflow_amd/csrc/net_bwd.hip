@@ -1076,13 +1076,13 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   gf.M = FLAT; gf.N = FC; gf.K = (int)B;
   gf.epi = EPI_STORE; gf.slab = ws + p.fcslab; gf.nsplit = p.fc_split; gf.colsum = ws + p.fccol;
   gf.wg_split = wks ? 4 : 0;
+  gf.xcd = xcd_gemm() ? 1 : 0;          // the 4 column tiles of an l2 strip on one XCD
   // the in-workgroup split-K form takes the XCD-grouped order by default (its 4 N tiles share
-  // the 64-row strip of l2: 58.5 -> ? MB per launch, PMC); A3C_WKS_XCD=0: the plain grid
+  // the 64-row strip of l2); A3C_WKS_XCD=0: the plain grid
   if (wks) {
     static const int env_wx = getenv("A3C_WKS_XCD") ? atoi(getenv("A3C_WKS_XCD")) : 1;
     gf.xcd = env_wx ? 1 : 0;
   }
-  gf.xcd = xcd_gemm() ? 1 : 0;          // the 4 column tiles of an l2 strip on one XCD
   // dl2[B][2592] = (dl3 W^T) * (l2 > 0)
   GemmArgs gd = {};
   gd.A = dh3; gd.lda = FC;               // A(m=b, k) = dl3[b][k]
