@@ -278,7 +278,6 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     ALLOC(sl.R_buf, nE * 4);
     ALLOC(sl.act_l1, nE * C1_P * C1_N * 4);
     ALLOC(sl.act_l2, nE * FLAT * 4);
-    ALLOC(sl.l2m, nE * C2_Q * 4);
     ALLOC(sl.act_l3, nE * FC * 4);
     ALLOC(sl.scr_l2, scrB * FLAT * 4);
     ALLOC(sl.scr_l3, scrB * FC * 4);
@@ -310,6 +309,8 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   ALLOC(e->sched, 64);
   ALLOC(e->stats, A3C_STATS_N * 8);
   ALLOC(e->ep_acc, E * 8);
+  // last: the other buffers keep the placement they had before the ReLU bits existed
+  for (int k = 0; k < e->nslot; ++k) ALLOC(e->slot[k].l2m, nE * C2_Q * 4);
 #undef ALLOC
   if (a3c_make_tab(L.nt, L.off, L.size, L.total, &e->tt) || a3c_fused_tab(L, &e->tt_f)) {
     a3c_engine_destroy(e);
@@ -569,6 +570,7 @@ static int enqueue_rollout_begin(a3c_engine* e, const Slot& sl, hipStream_t s) {
 // rollout step t: forward of s_{tau+t}, action draw (agent.py:141-151 / network.py:65-72) and,
 // with the device env, act + observe clip + Environment.screen of the new frame into the ring
 // (external envs: the host steps them between a3c_engine_ext_act and a3c_engine_ext_observe).
+static bool l2bits_on();
 static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
   const NetLayout& L = e->L;
@@ -630,12 +632,12 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
     nx.act_l1 = nullptr;   // measurement only: the fused rollout kernel saves no conv1 output
 #endif
     nx.act_l2 = t + 1 < n ? sl.act_l2 + (o + E) * FLAT : sl.scr_l2;
-    nx.l2m = t + 1 < n ? sl.l2m + (o + E) * C2_Q : nullptr;
+    nx.l2m = t + 1 < n && l2bits_on() ? sl.l2m + (o + E) * C2_Q : nullptr;
   }
   int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
                               sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s,
                               L.lstm ? &ls : nullptr, fuse && t > 0, has_next ? &nx : nullptr,
-                              fc_split(e) ? e->fcpart : nullptr, sl.l2m + o * C2_Q);
+                              fc_split(e) ? e->fcpart : nullptr, l2bits_on() ? sl.l2m + o * C2_Q : nullptr);
   if (rc) return rc;
   if (dev_env && !e->fused_screen) {
     rc = a3c_env_screen_launch(E, sl.frames + o, e->pool, e->ring, e->R, e->counters, t, s);
@@ -836,7 +838,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
 }
 #endif
 
-// the dl2 epilogue reads the forward's ReLU bits (A3C_L2BITS=0: re-read l2 itself; an A/B knob)
+// the dl2 epilogue reads the forward's ReLU bits (A3C_L2BITS=0: the forward writes none and the
+// epilogue re-reads l2 itself; an A/B knob)
 static bool l2bits_on() {
   static const bool on = !getenv("A3C_L2BITS") || atoi(getenv("A3C_L2BITS")) != 0;
   return on;

@@ -103,7 +103,11 @@ __device__ inline void gemm_tile(const GemmArgs& g, int bx, int by, int bz, floa
         if (g.epi == EPI_BIAS_RELU) v = fmaxf(v + g.bias[col], 0.f);
         else if (g.epi == EPI_BIAS) v = v + g.bias[col];
         else if (g.epi == EPI_MASK) v = g.mask[(int64_t)row * g.ldm + col] > 0.f ? v : 0.f;
-        else if (g.epi == EPI_MASKBITS) v = (g.maskbits[(int64_t)row * g.ldm + (col >> 5)] >> (col & 31)) & 1u ? v : 0.f;
+#ifndef A3C_NO_MASKBITS
+  #ifndef A3C_NO_MASKBITS
+      else if (g.epi == EPI_MASKBITS) v = (g.maskbits[(int64_t)row * g.ldm + (col >> 5)] >> (col & 31)) & 1u ? v : 0.f;
+#endif
+#endif
         g.C[(int64_t)row * g.ldc + col] = v;
       }
     }
@@ -215,7 +219,9 @@ __global__ void __launch_bounds__(256 * KS) k_gemm_f32_wks(GemmArgs g) {
       if (g.epi == EPI_BIAS_RELU) v = fmaxf(v + g.bias[col], 0.f);
       else if (g.epi == EPI_BIAS) v = v + g.bias[col];
       else if (g.epi == EPI_MASK) v = g.mask[(int64_t)row * g.ldm + col] > 0.f ? v : 0.f;
+#ifndef A3C_NO_MASKBITS
       else if (g.epi == EPI_MASKBITS) v = (g.maskbits[(int64_t)row * g.ldm + (col >> 5)] >> (col & 31)) & 1u ? v : 0.f;
+#endif
       g.C[(int64_t)row * g.ldc + col] = v;
     }
   }
@@ -330,7 +336,11 @@ __global__ void __launch_bounds__(256) k_gemm_f32_big(GemmArgs g) {
           if (g.epi == EPI_BIAS_RELU) v = fmaxf(v + g.bias[col], 0.f);
           else if (g.epi == EPI_BIAS) v = v + g.bias[col];
           else if (g.epi == EPI_MASK) v = g.mask[(int64_t)row * g.ldm + col] > 0.f ? v : 0.f;
-          else if (g.epi == EPI_MASKBITS) v = (g.maskbits[(int64_t)row * g.ldm + (col >> 5)] >> (col & 31)) & 1u ? v : 0.f;
+  #ifndef A3C_NO_MASKBITS
+  #ifndef A3C_NO_MASKBITS
+      else if (g.epi == EPI_MASKBITS) v = (g.maskbits[(int64_t)row * g.ldm + (col >> 5)] >> (col & 31)) & 1u ? v : 0.f;
+#endif
+#endif
           g.C[(int64_t)row * g.ldc + col] = v;
         }
       }
@@ -426,7 +436,9 @@ __global__ void k_reduce_slabs(const float* __restrict__ slab, int nsplit, int M
   if (epi == EPI_BIAS_RELU) v = fmaxf(v + bias[col], 0.f);
   else if (epi == EPI_BIAS) v = v + bias[col];
   else if (epi == EPI_MASK) v = mask[(int64_t)row * ldm + col] > 0.f ? v : 0.f;
+#ifndef A3C_NO_MASKBITS
   else if (epi == EPI_MASKBITS) v = (maskbits[(int64_t)row * ldm + (col >> 5)] >> (col & 31)) & 1u ? v : 0.f;
+#endif
   C[(int64_t)row * ldc + col] = v;
 }
 

@@ -340,6 +340,7 @@ __device__ inline void conv12_finish(f32x4 (&acc)[C1_TILES], float* l1s, int64_t
       const int q = 16 * (grp + 4 * mi) + 4 * j4 + r;
       const float v = fmaxf(acc2[mi][r] + bias2, 0.f);
       if (q < C2_Q) st_act(act_l2 + b * FLAT + q * C2_N + 16 * nt + i16, v);
+#ifndef A3C_NO_L2M_FWD   // (measurement only: the ballot compiled out)
       if (l2m) {
         // the ReLU mask as bits for the backward's dl2 epilogue: position q's channels 16 nt ..
         // 16 nt + 15 are the 16 lanes of group j4, so one ballot gives its half word (flat index
@@ -348,6 +349,7 @@ __device__ inline void conv12_finish(f32x4 (&acc)[C1_TILES], float* l1s, int64_t
         if (i16 == 0 && q < C2_Q)
           ((uint16_t*)l2m)[(b * C2_Q + q) * 2 + nt] = (uint16_t)(bal >> (16 * j4));
       }
+#endif
     }
   }
 }
