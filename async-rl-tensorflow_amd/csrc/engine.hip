@@ -100,6 +100,7 @@ struct a3c_engine {
   // clipped, mid-backward; a comm stream waits on it (a3c_engine_wait_grad_head)
   int split;
   hipEvent_t ev_head;
+  int l2bits;              // the forward writes act_l2's ReLU bits and the dl2 epilogue reads them
   // cross-stream ordering by stream memory operations (hipStreamWriteValue32 / WaitValue32 on
   // monotonic counters in device memory) instead of events: measured 3.6 us per hop against
   // 12-40 us for hipEventRecord + hipStreamWaitEvent (tools/waitvalue_probe.py)
@@ -195,6 +196,7 @@ extern "C" int a3c_engine_destroy(a3c_engine* e) {
 
 static int frame_bytes(const a3c_engine* e) { return e->frame84 ? PLANE : SCREEN_H * SCREEN_W * 3; }
 
+static int l2bits_choice(const a3c_engine* e);
 extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out) {
   if (!cfg || !out) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "null");
   *out = nullptr;
@@ -327,6 +329,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   }
   // the split exchange needs eager launches (its event is recorded mid-backward) and a peer
   e->split = cfg->split_exchange && cfg->world_size > 1 && !cfg->use_graph;
+  e->l2bits = l2bits_choice(e);
   if (e->split && hipEventCreateWithFlags(&e->ev_head, hipEventDisableTiming) != hipSuccess) {
     a3c_engine_destroy(e);
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "event creation failed");
@@ -570,7 +573,8 @@ static int enqueue_rollout_begin(a3c_engine* e, const Slot& sl, hipStream_t s) {
 // rollout step t: forward of s_{tau+t}, action draw (agent.py:141-151 / network.py:65-72) and,
 // with the device env, act + observe clip + Environment.screen of the new frame into the ring
 // (external envs: the host steps them between a3c_engine_ext_act and a3c_engine_ext_observe).
-static bool l2bits_on();
+static bool l2bits_on(const a3c_engine* e);
+static int l2bits_choice(const a3c_engine* e);
 static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
   const NetLayout& L = e->L;
@@ -632,12 +636,12 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
     nx.act_l1 = nullptr;   // measurement only: the fused rollout kernel saves no conv1 output
 #endif
     nx.act_l2 = t + 1 < n ? sl.act_l2 + (o + E) * FLAT : sl.scr_l2;
-    nx.l2m = t + 1 < n && l2bits_on() ? sl.l2m + (o + E) * C2_Q : nullptr;
+    nx.l2m = t + 1 < n && l2bits_on(e) ? sl.l2m + (o + E) * C2_Q : nullptr;
   }
   int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
                               sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s,
                               L.lstm ? &ls : nullptr, fuse && t > 0, has_next ? &nx : nullptr,
-                              fc_split(e) ? e->fcpart : nullptr, l2bits_on() ? sl.l2m + o * C2_Q : nullptr);
+                              fc_split(e) ? e->fcpart : nullptr, l2bits_on(e) ? sl.l2m + o * C2_Q : nullptr);
   if (rc) return rc;
   if (dev_env && !e->fused_screen) {
     rc = a3c_env_screen_launch(E, sl.frames + o, e->pool, e->ring, e->R, e->counters, t, s);
@@ -838,11 +842,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
 }
 #endif
 
-// the dl2 epilogue reads the forward's ReLU bits (A3C_L2BITS=0: the forward writes none and the
-// epilogue re-reads l2 itself; an A/B knob)
-static bool l2bits_on() {
-  static const bool on = !getenv("A3C_L2BITS") || atoi(getenv("A3C_L2BITS")) != 0;
-  return on;
+// The ReLU bits of act_l2 (the forward's conv2 epilogue ballots them, the backward's dl2 GEMM
+// epilogue reads 1/32 of the bytes of re-reading l2) where the backward bounds the overlapped
+// iteration (bwd_bound: M2, several GPUs): M2 6.03M vs 6.00M env-steps/s.  Where the rollout bounds
+// it (M1, C5 LSTM, 1024 envs) the ballot costs the rollout more than the bytes save the backward
+// (M1 4.85M vs 4.86M, and the rollout kernel without the ballot compiled in: C5 +0.9 %).
+// A3C_L2BITS=0/1 overrides.
+static bool l2bits_on(const a3c_engine* e) { return e->l2bits != 0; }
+static int l2bits_choice(const a3c_engine* e) {   // at create (a test compares the two forms)
+  const char* v = getenv("A3C_L2BITS");
+  return v ? atoi(v) != 0 : bwd_bound(e);
 }
 
 static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
@@ -915,7 +924,7 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
                            sl.actions, sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra,
                            fork && !e->split ? e->gs : nullptr, fork && !e->split ? e->ev_gfork : nullptr,
                            fork && !e->split ? e->ev_gjoin : nullptr, L.lstm ? &lb : nullptr, &sf,
-                           e->split ? &sp : nullptr, l2bits_on() ? sl.l2m : nullptr);
+                           e->split ? &sp : nullptr, l2bits_on(e) ? sl.l2m : nullptr);
   if (rc) return rc;
   if (c.world_size > 1 && !e->split) {
     // multi-GPU: clip this worker's gradient (agent.py:319) before the cross-GPU exchange

@@ -217,7 +217,9 @@ __device__ inline void conv1_accum(const uint8_t* x8, const uint16_t* xb, f32x4 
 
 // conv1 bias + relu of the accumulated tiles -> l1s as three bf16 terms (and act_l1), then conv2
 // (bf16x6 MFMA) + relu -> act_l2 for state b.
-template <bool SAVE_L1, bool EW>
+// L2M: the epilogue can write the ReLU bits (when l2m is set); false compiles the ballot out --
+// the fused rollout kernel runs measurably faster without it where the bits are not used
+template <bool SAVE_L1, bool EW, bool L2M = true>
 __device__ inline void conv12_finish(f32x4 (&acc)[C1_TILES], float* l1s, int64_t b,
                                      const uint16_t* __restrict__ w1s, const float* __restrict__ b1,
                                      const float* __restrict__ W2, float* __restrict__ act_l1,
@@ -340,8 +342,7 @@ __device__ inline void conv12_finish(f32x4 (&acc)[C1_TILES], float* l1s, int64_t
       const int q = 16 * (grp + 4 * mi) + 4 * j4 + r;
       const float v = fmaxf(acc2[mi][r] + bias2, 0.f);
       if (q < C2_Q) st_act(act_l2 + b * FLAT + q * C2_N + 16 * nt + i16, v);
-#ifndef A3C_NO_L2M_FWD   // (measurement only: the ballot compiled out)
-      if (l2m) {
+      if (L2M && l2m) {
         // the ReLU mask as bits for the backward's dl2 epilogue: position q's channels 16 nt ..
         // 16 nt + 15 are the 16 lanes of group j4, so one ballot gives its half word (flat index
         // q * 32 + c: word q of the row, bit c)
@@ -349,7 +350,6 @@ __device__ inline void conv12_finish(f32x4 (&acc)[C1_TILES], float* l1s, int64_t
         if (i16 == 0 && q < C2_Q)
           ((uint16_t*)l2m)[(b * C2_Q + q) * 2 + nt] = (uint16_t)(bal >> (16 * j4));
       }
-#endif
     }
   }
 }
@@ -767,7 +767,7 @@ static_assert(HSC_KV_OFF % 16 == 0 && HSC_KV_OFF + SCREEN_KV_BYTES <= HIST * PLA
 static_assert(HSC_SMEM + 16 <= 160 * 1024 - 82944, "rollout workgroup beside a compact conv backward one");
 // waves_per_eu(4) caps it at 128 VGPRs: with the concurrent k_conv_bwd<false,4> (254 VGPRs,
 // one wave per SIMD) two of its waves per SIMD must fit in the remaining 258
-template <bool SAVE_L1>
+template <bool SAVE_L1, bool L2M>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k_head_screen_conv12(const float* __restrict__ h3,
                                                             const float* __restrict__ Wp,
                                                             const float* __restrict__ bp,
@@ -900,7 +900,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   conv1_accum<false, HIST - 1, HIST>(nullptr, xnew - (HIST - 1) * PLANE, acc, [&](int f) {
     return __builtin_bit_cast(bf16x8, wn[f - (HIST - 1) * 6]);
   });
-  conv12_finish<SAVE_L1, false>(acc, (float*)smem, b, nx.w1s, nx.b1, nx.W2, SAVE_L1 ? nx.act_l1 : nullptr,
+  conv12_finish<SAVE_L1, false, L2M>(acc, (float*)smem, b, nx.w1s, nx.b1, nx.W2, SAVE_L1 ? nx.act_l1 : nullptr,
                                 nx.act_l2, w2r, bias2, dbg, nx.l2m);
   span_end(srec);
   if (dbg) {
@@ -1004,12 +1004,13 @@ int a3c_head_screen_conv12_launch(const NetLayout& L, const float* P, const floa
   const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
   if (!nx.sa.tau_ptr || !sel.tau_ptr)
     return a3c_set_error(A3C_ERR_INVALID, "a3c_head_screen_conv12", "device tau counters required");
-  if (nx.act_l1)
-    hipLaunchKernelGGL(k_head_screen_conv12<true>, dim3((unsigned)B), dim3(512), HSC_SMEM, s, act_l3,
-                       P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel, nx);
-  else
-    hipLaunchKernelGGL(k_head_screen_conv12<false>, dim3((unsigned)B), dim3(512), HSC_SMEM, s, act_l3,
-                       P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel, nx);
+#define HSC_GO(S, M) hipLaunchKernelGGL((k_head_screen_conv12<S, M>), dim3((unsigned)B), dim3(512), HSC_SMEM, s, act_l3, \
+                                        P + L.off[T_HW], P + L.off[T_HB], Wv, bv, L.A, L.zs, z, sel, nx)
+  if (nx.act_l1 && nx.l2m) HSC_GO(true, true);
+  else if (nx.act_l1) HSC_GO(true, false);
+  else if (nx.l2m) HSC_GO(false, true);
+  else HSC_GO(false, false);
+#undef HSC_GO
   A3C_CHECK(hipGetLastError());
   return 0;
 }
@@ -1056,9 +1057,13 @@ void a3c_conv12_set_smem() {
   C12_SMEM(true, true, false); C12_SMEM(true, false, false); C12_SMEM(false, true, false); C12_SMEM(false, false, false);
   C12_SMEM(true, true, true); C12_SMEM(true, false, true); C12_SMEM(false, true, true); C12_SMEM(false, false, true);
 #undef C12_SMEM
-  (void)hipFuncSetAttribute((const void*)k_head_screen_conv12<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)k_head_screen_conv12<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             HSC_SMEM);
-  (void)hipFuncSetAttribute((const void*)k_head_screen_conv12<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)k_head_screen_conv12<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            HSC_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_head_screen_conv12<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            HSC_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_head_screen_conv12<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             HSC_SMEM);
   (void)hipFuncSetAttribute((const void*)k_head_screen<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             SCREEN_FRAME_SMEM);

@@ -175,6 +175,24 @@ def test_stream_ordering_modes_are_bit_identical(monkeypatch):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
 
 
+@pytest.mark.parametrize('frame84', [0, 1])
+def test_relu_bits_equal_l2_reread(monkeypatch, frame84):
+    """The dl2 GEMM's ReLU mask from the forward's ballot bits (EPI_MASKBITS, the default where the
+    backward bounds: M2) and from re-reading l2 (EPI_MASK, the default in M1) train bit for bit
+    alike: the same mask, the same sums."""
+    engs = []
+    for bits in ('1', '0'):
+        monkeypatch.setenv('A3C_L2BITS', bits)
+        engs.append(build('a3c', 6, 64, 5, 0, seed=23, overlap=True, frames=256, frame84=frame84)[0])
+    a, b = engs
+    for _ in range(5):
+        a.iterate()
+        b.iterate()
+    torch.cuda.synchronize()
+    for name in ('params', 'ms', 'mom', 'grads', 'loss', 'actions', 'z'):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+
+
 @pytest.mark.parametrize('overlap,frame84', [(False, 0), (True, 0), (True, 1)])
 def test_bench_shape_is_deterministic(overlap, frame84):
     """At the bench configuration (Pong, 256 envs, n=5) two engines from the same seed train bit for
