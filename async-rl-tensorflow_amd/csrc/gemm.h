@@ -17,9 +17,6 @@ struct GemmArgs {
   int epi;
   const float* bias;          // EPI_BIAS*, indexed by n
   const float* mask; int64_t ldm;  // EPI_MASK: keep where mask[m*ldm+n] > 0
-  // EPI_MASKBITS: keep where bit n & 31 of maskbits[m*ldm + (n >> 5)] is set (ldm in 32-bit words):
-  // the forward's ReLU mask as bits, 1/32 of the bytes of re-reading the activations
-  const uint32_t* maskbits;
   float* slab;                // split-K partials [nsplit][M][N]
   int nsplit;                 // requested split (effective split may be smaller)
   int kchunk;                 // set by a3c_gemm
@@ -39,6 +36,9 @@ struct GemmArgs {
   // (k_gemm_f32_wks), folded in LDS -- nsplit is then 1 (no slab).  Not bit-identical to the
   // slab split (another summation grouping), deterministic.
   int wg_split;
+  // EPI_MASKBITS: keep where bit n & 31 of maskbits[m*ldm + (n >> 5)] is set (ldm in 32-bit words):
+  // the forward's ReLU mask as bits, 1/32 of the bytes of re-reading the activations
+  const uint32_t* maskbits;
 };
 
 int a3c_gemm(bool a_kcontig, bool b_ncontig, GemmArgs g, hipStream_t s);
