@@ -865,9 +865,15 @@ int a3c_fused_tab(const NetLayout& L, TensorTab* tt) {
 // ---------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------
-static bool fc_wks_on() {
+// The in-workgroup split-K fc weight GEMM (k_gemm_f32_wks) up to K = B = A3C_FC_WKS_MAXB samples
+// (default 2560: M1 +1.1 %, 512 envs 5.38M vs 5.35M).  Its workgroups each walk a quarter of K per
+// group, so at B = 5120 (1024 envs) it runs 176 us beside the rollout and the slab form wins
+// (5.77M vs 5.64M env-steps/s); with the LSTM head the slab form wins too (3.19M vs 3.16M).
+// A3C_FC_WKS=0 turns it off.
+static bool fc_wks_on(int64_t B) {
   static const bool on = !getenv("A3C_FC_WKS") || atoi(getenv("A3C_FC_WKS")) != 0;
-  return on;
+  static const int64_t maxb = getenv("A3C_FC_WKS_MAXB") ? atoll(getenv("A3C_FC_WKS_MAXB")) : 2560;
+  return on && B <= maxb;
 }
 
 BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B, bool wks) {
@@ -1026,7 +1032,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   const bool multi0 = env_multi >= 0 ? env_multi != 0 : !a3c_shared_gpu() || bwd_bound_knob();
   // the in-workgroup split-K fc weight GEMM where its launch stands alone anyway: the M1 overlap
   // backward and the split backward (several GPUs), not in the single three-GEMM launch
-  const bool wks = fc_wks_on() && (sp != nullptr || !multi0);
+  const bool wks = fc_wks_on(B) && !L.lstm && (sp != nullptr || !multi0);
   const BwdPlan p = a3c_bwd_plan(L, B, wks);
   const float* P = params;
   float* dz = ws + p.dz;
