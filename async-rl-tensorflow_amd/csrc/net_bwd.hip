@@ -1120,6 +1120,12 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     return backward_split(L, P, sa, B, act_l1, ws, s, p, gh, gf, gd, grads, terms, loss_out, sf, sp);
   }
   static const int env_late = getenv("A3C_FOLD_LATE") ? atoi(getenv("A3C_FOLD_LATE")) : -1;
+  // The head weight GEMM folds its own split-K slabs (k_reduce_slabs behind it) instead of the
+  // finalize with the LSTM head (C5 3.19M vs 3.18M env-steps/s), not without it (M1 4.81M vs
+  // 4.87M); A3C_HEAD_FOLD=0/1 overrides.  Separate-launch path below only.
+  static const int env_hfold_knob = getenv("A3C_HEAD_FOLD") ? atoi(getenv("A3C_HEAD_FOLD")) : -1;
+  const bool env_hfold = env_hfold_knob >= 0 ? env_hfold_knob != 0 : lb != nullptr;
+  bool hfold = false;
   const bool multi = multi0 && !wks;
   const bool late = env_late >= 0 ? env_late != 0 : multi;
   if (!fork && (multi || late)) {
@@ -1147,6 +1153,8 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     // dwfc_late: the fc weight GEMM (+ its fold) behind the conv backward -- only dl2 stands
     // between the head and the conv
     const bool dwfc_late = dwfc_late_knob() && !fork;
+    hfold = env_hfold && p.head_split > 1;
+    if (hfold) gh.defer_reduce = 0;
     rc = abl_gemm ? 0 : a3c_gemm(false, true, gh, ws_s);
     if (rc) return rc;
     if (!dwfc_late) {
@@ -1192,12 +1200,13 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   seg(cs + CB_OFF_B2, CB_SLAB, p.groups, 1, 0, 0, C2_N, T_L2B, 0, 1.0f);
   seg(ws + p.fccol, FC, p.fc_split, 1, 0, 0, FC, T_FCB, 0, 1.0f);
   // the head weight GEMM's split-K partials folded here (gh.defer_reduce): one kernel fewer
-  const float* hsrc = p.head_split > 1 ? ws + p.hslab : ws + p.hgrad;
+  const float* hsrc = p.head_split > 1 && !hfold ? ws + p.hslab : ws + p.hgrad;
   const int64_t hstride = (int64_t)FC * L.zs;
-  seg(hsrc, hstride, p.head_split, FC, L.zs, 0, L.A, T_HW, L.A, 1.0f);
+  const int hsplit = hfold ? 1 : p.head_split;
+  seg(hsrc, hstride, hsplit, FC, L.zs, 0, L.A, T_HW, L.A, 1.0f);
   seg(ws + p.hcol, L.zs, p.head_split, 1, 0, 0, L.A, T_HB, 0, 1.0f);
   if (a3c) {
-    seg(hsrc, hstride, p.head_split, FC, L.zs, L.A, 1, T_VW, 1, 1.0f);
+    seg(hsrc, hstride, hsplit, FC, L.zs, L.A, 1, T_VW, 1, 1.0f);
     seg(ws + p.hcol, L.zs, p.head_split, 1, 0, L.A, 1, T_VB, 0, 1.0f);
   }
   int nsumblk = 0;
