@@ -10,7 +10,8 @@ parameter-server apply of main.py:60-66.
 ``overlap=True`` pipelines the engine: rollout k runs on an engine-owned stream with the
 parameters after update k-2 while the backward, exchange and apply of rollout k-1 run on the
 caller's stream (A3C's stale-parameter asynchrony at a fixed staleness of one update).  Rollout
-k's buffers are ``slot(k & 1)``.
+k's buffers are ``slot(k & 1)``.  With ``algo='q'`` rollout k-1's TD targets are formed by its
+backward, with the target network as it stands then (agent.py:169-190 at the same staleness).
 
 Kernels are launched eagerly by default; ``use_graph=True`` captures each engine call into
 hipGraphs and replays them (bit-identical, measured slower on MI355X: DESIGN.md §6).
