@@ -18,6 +18,23 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // Error reporting (defined in capi.cpp).
 extern "C" int a3c_set_error(int code, const char* what, const char* detail);
 
+// Environment switches.  A release build reads only the documented, tested ones (A3C_KNOB:
+// A3C_WAIT_VALUE, A3C_L2BITS, A3C_FC_SPLIT, A3C_FUSE_CONV, A3C_FUSED_SCREEN, A3C_SPANS; bench.py
+// records every A3C_* variable that is set).  The A/B knobs of measured-and-rejected variants
+// (A3C_AB_KNOB) compile to their defaults unless the library is built with -DA3C_KNOBS
+// (tools/build_variant.sh), so a stray variable cannot change a release run's summation order.
+#include <cstdlib>
+inline long long a3c_env_ll(const char* name, long long dflt) {
+  const char* v = getenv(name);
+  return v ? atoll(v) : dflt;
+}
+#define A3C_KNOB(name, dflt) a3c_env_ll(name, dflt)
+#ifdef A3C_KNOBS
+#define A3C_AB_KNOB(name, dflt) a3c_env_ll(name, dflt)
+#else
+#define A3C_AB_KNOB(name, dflt) ((void)(name), (long long)(dflt))
+#endif
+
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al. 2011) -- bit-identical to oracle/philox.py.
 // ---------------------------------------------------------------------------

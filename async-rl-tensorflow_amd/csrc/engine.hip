@@ -211,6 +211,10 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     delete e;
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "bad config");
   }
+  if (cfg->double_q && cfg->net.algo != A3C_ALGO_Q) {
+    delete e;
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "double_q is a Q-learning option (agent.py:176-184)");
+  }
   a3c_init_once();
   const NetLayout& L = e->L;
   e->E = cfg->num_envs;
@@ -219,14 +223,14 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   e->ext = cfg->external_env ? 1 : 0;
   if (e->ext) e->cfg.num_frames = cfg->num_envs;   // the pool is the host frames' staging buffer
   e->fused_screen = 1;
-  if (const char* v = getenv("A3C_FUSED_SCREEN")) e->fused_screen = atoi(v) != 0;
+  e->fused_screen = A3C_KNOB("A3C_FUSED_SCREEN", e->fused_screen) != 0;
   // overlap mode only: measured on MI355X (Pong, 256 envs) 3.65M -> 3.84M env-steps/s overlapped,
   // but 3.25M -> 3.08M in sync mode, where the unfused kernels run their bigger variants
   // (1024-thread screen, early-W2 conv12) with the GPU to themselves
   e->fuse_conv = e->overlap;
-  if (const char* v = getenv("A3C_FUSE_CONV")) e->fuse_conv = atoi(v) != 0;
+  e->fuse_conv = A3C_KNOB("A3C_FUSE_CONV", e->fuse_conv) != 0;
   e->fc_split = 1;
-  if (const char* v = getenv("A3C_FC_SPLIT")) e->fc_split = atoi(v) != 0;
+  e->fc_split = A3C_KNOB("A3C_FC_SPLIT", e->fc_split) != 0;
   e->frame84 = cfg->frame84 ? 1 : 0;
   if (e->frame84 && (e->ext || !e->fused_screen)) {   // the copy lives in the fused head kernels
     delete e;
@@ -340,13 +344,12 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     int lo_prio = 0, hi_prio = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
     int prio = hi_prio;
-    if (const char* v = getenv("A3C_ROLLOUT_PRIO")) prio = atoi(v) ? hi_prio : lo_prio;
+    if (!A3C_AB_KNOB("A3C_ROLLOUT_PRIO", 1)) prio = lo_prio;
     // the cross-stream events order two streams of this device and the host never inspects
     // them: no system-scope fence (measured: 4.54M vs 4.47M env-steps/s with events, on par with
     // the wait-value hop; A3C_DEVICE_EVENTS=0 restores the default events)
     unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;
-    if (const char* v = getenv("A3C_DEVICE_EVENTS"))
-      if (!atoi(v)) evf = hipEventDisableTiming;
+    if (!A3C_AB_KNOB("A3C_DEVICE_EVENTS", 1)) evf = hipEventDisableTiming;
     bool ok = hipStreamCreateWithPriority(&e->rs, hipStreamNonBlocking, prio) == hipSuccess &&
               hipEventCreateWithFlags(&e->ev_start, evf) == hipSuccess;
     for (int k = 0; k < 2 && ok; ++k)
@@ -354,7 +357,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     // (one GPU: with an exchange the collectives' own stream synchronisation sits between the
     // graphs, a combination the pool has not run on several GPUs -- events there)
     e->wait_value = e->cfg.world_size == 1;
-    if (const char* v = getenv("A3C_WAIT_VALUE")) e->wait_value = atoi(v) != 0;
+    e->wait_value = A3C_KNOB("A3C_WAIT_VALUE", e->wait_value) != 0;
 
     if (!ok) {
       a3c_engine_destroy(e);
@@ -485,7 +488,7 @@ static StateAddr ring_addr(const a3c_engine* e, int tau_offset, const int64_t* t
 
 // live launch-span stamps in k_conv_bwd / k_head_screen_conv12 (A3C_SPANS=0 turns them off)
 static bool spans_on() {
-  static const bool on = !getenv("A3C_SPANS") || atoi(getenv("A3C_SPANS")) != 0;
+  static const bool on = A3C_KNOB("A3C_SPANS", 1) != 0;
   return on;
 }
 // conv fusion (k_head_screen_conv12) runs with the device envs and the fused screen
@@ -545,13 +548,13 @@ static const Slot& prev_slot(const a3c_engine* e, const Slot& sl) {
 // rollout k on the rollout stream
 static bool bwd_bound(const a3c_engine* e);
 static bool late_go(const a3c_engine* e) {
-  static const int env = getenv("A3C_LATE_GO") ? atoi(getenv("A3C_LATE_GO")) : -1;   // A/B override
+  static const int env = (int)A3C_AB_KNOB("A3C_LATE_GO", -1);   // A/B override
   // one GPU: M1 and M2 (M2 5.77M -> 5.83M since the conv backward runs one workgroup per CU);
   // with an exchange the caller stream carries it behind the backward: right behind the rollout
   return env >= 0 ? env != 0 : e->cfg.world_size == 1;
 }
 static bool kernel_go(const a3c_engine* e) {
-  static const int env = getenv("A3C_KERNEL_GO") ? atoi(getenv("A3C_KERNEL_GO")) : 1;   // A/B override
+  static const int env = (int)A3C_AB_KNOB("A3C_KERNEL_GO", 1);   // A/B override
   return e->overlap && e->wait_value && late_go(e) && env != 0;
 }
 
@@ -850,8 +853,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
 // A3C_L2BITS=0/1 overrides.
 static bool l2bits_on(const a3c_engine* e) { return e->l2bits != 0; }
 static int l2bits_choice(const a3c_engine* e) {   // at create (a test compares the two forms)
-  const char* v = getenv("A3C_L2BITS");
-  return v ? atoi(v) != 0 : bwd_bound(e);
+  return A3C_KNOB("A3C_L2BITS", bwd_bound(e) ? 1 : 0) != 0;
 }
 
 static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
@@ -883,12 +885,22 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
     HeadSelect none = {};
     none.mode = -1;
     none.E = E;
+    const float* qsel = nullptr;
+    if (c.double_q) {
+      // double Q (agent.py:176-184): the online net's q of s_{t+1} -- rows t+1 of the rollout's own
+      // q (the slot's parameters, those the loss is taken at), and for t = n-1 one forward of s_n
+      // with them into the slot's bootstrap row block
+      rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, n, sl.tau), E, nullptr, sl.scr_l2, sl.scr_l3,
+                              sl.z + e->nE * zs, none, s);
+      if (rc) return rc;
+      qsel = sl.z + (int64_t)E * zs;
+    }
     rc = a3c_prep_fwd_launch(L, e->tparams, e->prep_t, s);
     if (rc) return rc;
     rc = a3c_forward_launch(L, e->tparams, e->prep_t, ring_addr(e, 1, sl.tau), e->nE, nullptr, sl.scr_l2,
                             sl.scr_l3, e->zt, none, s);
     if (rc) return rc;
-    rc = a3c_td_target_launch(sl.rewards, sl.terms, e->zt, e->nE, L.A, zs, c.discount, sl.R_buf, s);
+    rc = a3c_td_target_launch(sl.rewards, sl.terms, e->zt, e->nE, L.A, zs, c.discount, sl.R_buf, s, qsel);
     if (rc) return rc;
   }
   ReturnsArgs ra = {};
@@ -896,7 +908,7 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
     ra.rewards = sl.rewards; ra.terms = sl.terms; ra.boot = sl.z + e->nE * zs + L.A; ra.boot_stride = zs;
     ra.n = n; ra.E = E; ra.gamma = c.gamma; ra.R_out = sl.R_buf;
   }
-  static const bool fork_env = getenv("A3C_BWD_FORK") ? atoi(getenv("A3C_BWD_FORK")) != 0 : false;  // measured slower
+  static const bool fork_env = A3C_AB_KNOB("A3C_BWD_FORK", 0) != 0;  // measured slower
   const bool fork = fork_env && !L.lstm;
   LstmBwd lb = {};
   if (L.lstm) {
@@ -1364,6 +1376,7 @@ struct StateHeader {
   int64_t total, bytes, iter;
   uint64_t seed;
   int32_t grad_ready, grad_applied;
+  int32_t l2bits, pad;   // whether the rollout in flight wrote the l2 ReLU bits its backward reads
 };
 constexpr uint32_t STATE_MAGIC = 0x53433341u;   // "A3CS"
 }
@@ -1405,11 +1418,12 @@ static std::vector<StateRegion> state_regions(const a3c_engine* e) {
 
 static StateHeader state_header(const a3c_engine* e) {
   StateHeader h = {};
-  h.magic = STATE_MAGIC; h.version = 2;   // 2: + the l2 ReLU bits of the rollout in flight
+  h.magic = STATE_MAGIC; h.version = 3;   // 2: + the l2 ReLU bits of the rollout in flight; 3: + l2bits
   h.E = e->E; h.n = e->n; h.R = e->R; h.algo = e->L.algo; h.A = e->L.A; h.lstm = e->L.lstm ? 1 : 0;
   h.overlap = e->overlap; h.world = e->cfg.world_size; h.frame84 = e->frame84;
   h.env_id_base = e->cfg.env_id_base; h.seed = e->cfg.seed;   // the env shard and its random streams
   h.total = e->L.total;
+  h.l2bits = l2bits_on(e) ? 1 : 0;
   int64_t b = sizeof(StateHeader);
   for (const StateRegion& x : state_regions(e)) b += (int64_t)x.bytes;
   h.bytes = b;
@@ -1466,7 +1480,7 @@ extern "C" int a3c_engine_state_load(a3c_engine* e, const void* host, int64_t by
   if (h.E != want.E || h.n != want.n || h.R != want.R || h.algo != want.algo || h.A != want.A ||
       h.lstm != want.lstm || h.overlap != want.overlap || h.world != want.world || h.frame84 != want.frame84 ||
       h.env_id_base != want.env_id_base || h.seed != want.seed || h.total != want.total || h.bytes != want.bytes ||
-      bytes != want.bytes)
+      h.l2bits != want.l2bits || bytes != want.bytes)
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_state_load", "state of a different engine configuration");
   hipStream_t s = (hipStream_t)stream;
   A3C_CHECK(hipStreamSynchronize(s));

@@ -104,9 +104,7 @@ __device__ inline void gemm_tile(const GemmArgs& g, int bx, int by, int bz, floa
         else if (g.epi == EPI_BIAS) v = v + g.bias[col];
         else if (g.epi == EPI_MASK) v = g.mask[(int64_t)row * g.ldm + col] > 0.f ? v : 0.f;
 #ifndef A3C_NO_MASKBITS
-  #ifndef A3C_NO_MASKBITS
       else if (g.epi == EPI_MASKBITS) v = (g.maskbits[(int64_t)row * g.ldm + (col >> 5)] >> (col & 31)) & 1u ? v : 0.f;
-#endif
 #endif
         g.C[(int64_t)row * g.ldc + col] = v;
       }
@@ -336,10 +334,8 @@ __global__ void __launch_bounds__(256) k_gemm_f32_big(GemmArgs g) {
           if (g.epi == EPI_BIAS_RELU) v = fmaxf(v + g.bias[col], 0.f);
           else if (g.epi == EPI_BIAS) v = v + g.bias[col];
           else if (g.epi == EPI_MASK) v = g.mask[(int64_t)row * g.ldm + col] > 0.f ? v : 0.f;
-  #ifndef A3C_NO_MASKBITS
-  #ifndef A3C_NO_MASKBITS
+#ifndef A3C_NO_MASKBITS
       else if (g.epi == EPI_MASKBITS) v = (g.maskbits[(int64_t)row * g.ldm + (col >> 5)] >> (col & 31)) & 1u ? v : 0.f;
-#endif
 #endif
           g.C[(int64_t)row * g.ldc + col] = v;
         }

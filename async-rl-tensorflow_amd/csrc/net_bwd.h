@@ -96,8 +96,9 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
                         const SplitBwd* sp = nullptr, const uint32_t* l2m = nullptr);
 int a3c_returns_launch(const float* rewards, const uint8_t* terms, const float* boot, int64_t boot_stride,
                        int n, int64_t E, double gamma, float* R, hipStream_t s);
+// qsel != nullptr: double Q-learning -- the value of qn's row at qsel's row argmax (agent.py:176-184)
 int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float* qn, int64_t B, int A,
-                         int zs, double discount, float* target, hipStream_t s);
+                         int zs, double discount, float* target, hipStream_t s, const float* qsel = nullptr);
 int a3c_select_launch(const float* z, int64_t B, int zs, int A, const HeadSelect& sel, hipStream_t s);
 void a3c_conv12_set_smem();
 void a3c_conv_bwd_set_smem();

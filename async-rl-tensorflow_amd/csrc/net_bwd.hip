@@ -38,14 +38,26 @@ __global__ void k_returns(const float* __restrict__ rewards, const uint8_t* __re
   }
 }
 
+// agent.py:186-190 (max_a Q'(s')), or with qsel the double-Q form agent.py:176-184: the target
+// net's value at the online net's argmax (tf.argmax: the first maximum)
 __global__ void k_td_target(const float* __restrict__ rewards, const uint8_t* __restrict__ terms,
                             const float* __restrict__ qn, int64_t B, int A, int zs, double discount,
-                            float* __restrict__ target) {
+                            float* __restrict__ target, const float* __restrict__ qsel) {
 #pragma clang fp contract(off)
   int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   float m = qn[b * zs];
-  for (int j = 1; j < A; ++j) m = fmaxf(m, qn[b * zs + j]);
+  if (qsel) {
+    float best = qsel[b * zs];
+    int arg = 0;
+    for (int j = 1; j < A; ++j) {
+      const float v = qsel[b * zs + j];
+      if (v > best) { best = v; arg = j; }
+    }
+    m = qn[b * zs + arg];
+  } else {
+    for (int j = 1; j < A; ++j) m = fmaxf(m, qn[b * zs + j]);
+  }
   double t = terms[b] ? 1.0 : 0.0;
   double v = (1.0 - t) * discount * (double)m + (double)rewards[b];
   target[b] = (float)v;
@@ -221,7 +233,7 @@ constexpr int cb_tail(bool lx) {
 #define CB_SMEM_SOLO 82944
 static_assert(2 * CB_SMEM_SOLO > 160 * 1024 && CB_SMEM_SOLO >= CB_SMEM_COMPACT_LX, "solo reservation");
 static int cb_smem(int own) {
-  static const bool solo = getenv("A3C_CB_SOLO") ? atoi(getenv("A3C_CB_SOLO")) != 0 : true;
+  static const bool solo = A3C_AB_KNOB("A3C_CB_SOLO", 1) != 0;
   return solo ? CB_SMEM_SOLO : own;
 }
 
@@ -871,8 +883,8 @@ int a3c_fused_tab(const NetLayout& L, TensorTab* tt) {
 // (5.77M vs 5.64M env-steps/s); with the LSTM head the slab form wins too (3.19M vs 3.16M).
 // A3C_FC_WKS=0 turns it off.
 static bool fc_wks_on(int64_t B) {
-  static const bool on = !getenv("A3C_FC_WKS") || atoi(getenv("A3C_FC_WKS")) != 0;
-  static const int64_t maxb = getenv("A3C_FC_WKS_MAXB") ? atoll(getenv("A3C_FC_WKS_MAXB")) : 2560;
+  static const bool on = A3C_AB_KNOB("A3C_FC_WKS", 1) != 0;
+  static const int64_t maxb = (int)A3C_AB_KNOB("A3C_FC_WKS_MAXB", 2560);
   return on && B <= maxb;
 }
 
@@ -888,7 +900,7 @@ BwdPlan a3c_bwd_plan(const NetLayout& L, int64_t B, bool wks) {
   // for the rollout).  Round 2, with the partial fc: 192 (-> 183 workgroups of 7 samples at
   // n*E = 1280) 4.37M env-steps/s vs 4.29M for 224 (214 x 6), 4.14M for 160 (160 x 8), 4.00M for 256.
   // The slab workspace is sized for the larger count, so the plan's offsets do not depend on the mode.
-  static const int env_nwg = getenv("A3C_CB_NWG") ? atoi(getenv("A3C_CB_NWG")) : 0;
+  static const int env_nwg = (int)A3C_AB_KNOB("A3C_CB_NWG", 0);
   // Round 3, with one compact workgroup per CU guaranteed (CB_SMEM_SOLO): 256 (5 samples each at
   // n*E = 1280) -- M2 5.36M -> 5.77M, M1 4.62M -> 4.66M against 183 x 7 (214 x 6: 5.71M / 4.65M)
   const int nwg_shared = env_nwg ? env_nwg : 256, nwg_own = env_nwg ? env_nwg : 256;
@@ -1028,11 +1040,14 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   // overlapped backward bounds the iteration (M2: 5.17-5.22M -> 5.38-5.39M); beside a rollout
   // that bounds it the 1,420-workgroup launch slows it more than it gains (M1: 4.62M -> 4.45M),
   // and so do the folds moved behind the conv backward alone (A3C_FOLD_LATE: 4.62M -> 4.45M)
-  static const int env_multi = getenv("A3C_GEMM_MULTI") ? atoi(getenv("A3C_GEMM_MULTI")) : -1;
+  static const int env_multi = (int)A3C_AB_KNOB("A3C_GEMM_MULTI", -1);
   const bool multi0 = env_multi >= 0 ? env_multi != 0 : !a3c_shared_gpu() || bwd_bound_knob();
-  // the in-workgroup split-K fc weight GEMM where its launch stands alone anyway: the M1 overlap
-  // backward and the split backward (several GPUs), not in the single three-GEMM launch
-  const bool wks = fc_wks_on(B) && !L.lstm && (sp != nullptr || !multi0);
+  // the in-workgroup split-K fc weight GEMM where its launch stands alone anyway (the M1 overlap
+  // backward), not in the single three-GEMM launch.  The split backward (SplitBwd) takes the form
+  // the one-phase backward of the same configuration takes (multi0 does not depend on sp), so the
+  // two exchanges sum the fc weight gradient in one order and stay bit-identical
+  // (test_gpu_multirank.py::test_split_exchange_equals_one_phase)
+  const bool wks = fc_wks_on(B) && !L.lstm && !multi0;
   const BwdPlan p = a3c_bwd_plan(L, B, wks);
   const float* P = params;
   float* dz = ws + p.dz;
@@ -1086,7 +1101,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   // A3C_WKS_XCD=1: the in-workgroup split-K form in XCD-grouped order (its 4 N tiles share the
   // 64-row strip of l2): M1 4.84M vs 4.85M with the plain grid (3 interleaved reps), so off
   if (wks) {
-    static const int env_wx = getenv("A3C_WKS_XCD") ? atoi(getenv("A3C_WKS_XCD")) : 0;
+    static const int env_wx = (int)A3C_AB_KNOB("A3C_WKS_XCD", 0);
     gf.xcd = env_wx ? 1 : 0;
   }
   // dl2[B][2592] = (dl3 W^T) * (l2 > 0)
@@ -1105,13 +1120,13 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     // bit-identical).  Off: +0.5 % on one box (4.79-4.81M -> 4.82-4.83M), -0.8 % on another
     // (4.80-4.83M -> 4.75-4.79M) -- the tile GEMM takes 62 us instead of ~35 and the caller
     // stream's loop (go -> backward -> apply -> hop) then bounds M1 again (tools/wglog.py)
-    static const int env_big = getenv("A3C_GEMM_BIG") ? atoi(getenv("A3C_GEMM_BIG")) : 0;
+    static const int env_big = (int)A3C_AB_KNOB("A3C_GEMM_BIG", 0);
     gd.big = a3c_shared_gpu() && env_big != 0;
-    static const int env_bigf = getenv("A3C_GEMM_BIG_FC") ? atoi(getenv("A3C_GEMM_BIG_FC")) : 0;
+    static const int env_bigf = (int)A3C_AB_KNOB("A3C_GEMM_BIG_FC", 0);
     gf.big = a3c_shared_gpu() && env_bigf != 0;
   }
   {
-    static const int env_wgs = getenv("A3C_GEMM_WGS") ? atoi(getenv("A3C_GEMM_WGS")) : 0;
+    static const int env_wgs = (int)A3C_AB_KNOB("A3C_GEMM_WGS", 0);
     if (a3c_shared_gpu()) gh.max_wgs = gf.max_wgs = gd.max_wgs = env_wgs;
   }
   int rc;
@@ -1119,11 +1134,11 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     if (!sf || fork) return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "split backward: fused norms, no fork");
     return backward_split(L, P, sa, B, act_l1, ws, s, p, gh, gf, gd, grads, terms, loss_out, sf, sp);
   }
-  static const int env_late = getenv("A3C_FOLD_LATE") ? atoi(getenv("A3C_FOLD_LATE")) : -1;
+  static const int env_late = (int)A3C_AB_KNOB("A3C_FOLD_LATE", -1);
   // The head weight GEMM folds its own split-K slabs (k_reduce_slabs behind it) instead of the
   // finalize with the LSTM head (C5 3.19M vs 3.18M env-steps/s), not without it (M1 4.81M vs
   // 4.87M); A3C_HEAD_FOLD=0/1 overrides.  Separate-launch path below only.
-  static const int env_hfold_knob = getenv("A3C_HEAD_FOLD") ? atoi(getenv("A3C_HEAD_FOLD")) : -1;
+  static const int env_hfold_knob = (int)A3C_AB_KNOB("A3C_HEAD_FOLD", -1);
   const bool env_hfold = env_hfold_knob >= 0 ? env_hfold_knob != 0 : lb != nullptr;
   bool hfold = false;
   const bool multi = multi0 && !wks;
@@ -1268,7 +1283,7 @@ int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa,
 #endif
   // sync: the DMA-prefetching kernel at 8 waves (2 per SIMD) owns the GPU; overlap: the compact
   // 4-wave kernel leaves registers and LDS for the concurrent rollout (measured, tools/ab.sh)
-  static const int env_nw = getenv("A3C_CB_WAVES") ? atoi(getenv("A3C_CB_WAVES")) : 0;
+  static const int env_nw = (int)A3C_AB_KNOB("A3C_CB_WAVES", 0);
   const int nw = env_nw ? env_nw : (a3c_shared_gpu() ? 4 : 8);
   if (a3c_shared_gpu() && nw == 4 && a3c_lean_cbwd())
     hipLaunchKernelGGL((k_conv_bwd<false, 4, true>), dim3((unsigned)p.nwg), dim3(256), cb_smem(CB_SMEM_COMPACT_LX), s, sa, B,
@@ -1299,10 +1314,10 @@ int a3c_returns_launch(const float* rewards, const uint8_t* terms, const float* 
 }
 
 int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float* qn, int64_t B, int A,
-                         int zs, double discount, float* target, hipStream_t s) {
+                         int zs, double discount, float* target, hipStream_t s, const float* qsel) {
   if (B <= 0) return 0;
   hipLaunchKernelGGL(k_td_target, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, rewards, terms, qn,
-                     B, A, zs, discount, target);
+                     B, A, zs, discount, target, qsel);
   A3C_CHECK(hipGetLastError());
   return 0;
 }

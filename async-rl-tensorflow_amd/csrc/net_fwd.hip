@@ -986,7 +986,7 @@ int a3c_head_screen_launch(const NetLayout& L, const float* P, const float* act_
   const float* Wv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VW] : nullptr;
   const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
   // 1024 threads when the step owns the GPU; 512 leave room for the concurrent backward
-  static const int env_t = getenv("A3C_HS_THREADS") ? atoi(getenv("A3C_HS_THREADS")) : 0;
+  static const int env_t = (int)A3C_AB_KNOB("A3C_HS_THREADS", 0);
   const int nt = env_t ? env_t : (a3c_shared_gpu() ? 512 : 1024);
   if (nt == 1024)
     hipLaunchKernelGGL(k_head_screen<1024>, dim3((unsigned)B), dim3(1024), SCREEN_FRAME_SMEM, s, act_l3,
@@ -1021,7 +1021,7 @@ int a3c_conv12_launch(const NetLayout& L, const float* P, const uint8_t* prep, c
   const uint16_t* w1s = (const uint16_t*)prep;
   const bool ew = !a3c_shared_gpu();
   // overlap mode: the 60 KB u8-plane variant (co-resides with the backward's workgroups)
-  static const int env_u8 = getenv("A3C_C12_U8") ? atoi(getenv("A3C_C12_U8")) : -1;
+  static const int env_u8 = (int)A3C_AB_KNOB("A3C_C12_U8", -1);
   const bool u8 = env_u8 >= 0 ? env_u8 != 0 : !ew;
 #define CONV12_ARGS sa, B, w1s, P + L.off[T_L1B], P + L.off[T_L2W], P + L.off[T_L2B], act_l1, act_l2, l2m
 #define CONV12_GO(S, E, U) \
@@ -1334,7 +1334,7 @@ void a3c_set_fcp_split(int ks) { t_fcp_split = ks; }
 int a3c_fc_part_launch(const float* A, const float* Wp, float* part, int64_t M, hipStream_t s) {
   if (M <= 0) return 0;
   const int nrb = (int)((M + FCP_RB - 1) / FCP_RB);
-  static const int env_ks = getenv("A3C_FCP_KS") ? atoi(getenv("A3C_FCP_KS")) : 0;
+  static const int env_ks = (int)A3C_AB_KNOB("A3C_FCP_KS", 0);
   const int ks = env_ks ? env_ks : a3c_fcp_split();
   const dim3 grid((unsigned)(FC_NS * nrb * (FC / FCP_CB)));
   if (ks == 4) hipLaunchKernelGGL(k_fc_part<4>, grid, dim3(1024), 0, s, A, Wp, part, (int)M);
@@ -1413,13 +1413,13 @@ int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* 
   static const bool ablate = getenv("A3C_ABL_FC") != nullptr;   // measurement only: no fc
   if (ablate) return 0;
 #endif
-  static const int env_nw = getenv("A3C_FC_WAVES") ? atoi(getenv("A3C_FC_WAVES")) : -1;
+  static const int env_nw = (int)A3C_AB_KNOB("A3C_FC_WAVES", -1);
   const int nw = env_nw >= 0 ? env_nw : (a3c_shared_gpu() ? 4 : 8);
   if (nw == 0 && Wrows)
     hipLaunchKernelGGL(k_fc_fwd_rows, dim3(FC / 16, (unsigned)((M + 15) / 16)), dim3(256), 0, s, A, Wrows, bias, C,
                        (int)M);
   else {
-    static const int env_x = getenv("A3C_FC_XCD") ? atoi(getenv("A3C_FC_XCD")) : 0;
+    static const int env_x = (int)A3C_AB_KNOB("A3C_FC_XCD", 0);
     const int mt = (int)((M + 15) / 16), ntiles = mt * (FC / 16);
     const int xr = env_x == 2 ? (M % 128 == 0 ? 2 : 0) : (env_x && ntiles % 8 == 0);
     const dim3 grid = xr ? dim3((unsigned)ntiles) : dim3(FC / 16, (unsigned)mt);

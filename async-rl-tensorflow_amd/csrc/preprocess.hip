@@ -61,8 +61,7 @@ extern "C" int a3c_luminance_u8(const uint8_t* rgb, int64_t npix, uint8_t* out, 
 
 int a3c_screen_rows() {
   static int rows = [] {
-    const char* v = getenv("A3C_PRE_ROWS");    // tuning knob (tools/microbench_preprocess.py); default 14
-    int r = v ? atoi(v) : 14;
+    int r = (int)A3C_AB_KNOB("A3C_PRE_ROWS", 14);    // tuning knob (tools/microbench_preprocess.py)
     return (r == 7 || r == 12 || r == 14 || r == 21 || r == 28 || r == 42) ? r : 14;
   }();
   return rows;
@@ -107,8 +106,7 @@ int a3c_launch_preprocess(const uint8_t* rgb, const int32_t* frame_idx, int64_t 
 // output bands per frame for the standalone C-ABI path (A3C_PRE_PARTS overrides: tuning knob)
 PreGeom a3c_make_geom(int in_h, int in_w, int out_h, int out_w) {
   static int parts = [] {
-    const char* v = getenv("A3C_PRE_PARTS");
-    int p = v ? atoi(v) : 8;
+    int p = (int)A3C_AB_KNOB("A3C_PRE_PARTS", 8);
     return p > 0 ? p : 8;
   }();
   return a3c_make_geom_parts(in_h, in_w, out_h, out_w, parts);

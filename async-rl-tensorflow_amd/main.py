@@ -77,8 +77,32 @@ def parse_flags(argv=None):
                  help='multi-GPU sync/overlap exchange: sequential = partitioned PS applying every '
                       "worker's clipped gradient as its own RMSProp step in rank order (the reference "
                       'PS semantics); sum = one all-reduce, one RMSProp step of the summed gradients')
+  p.add_argument('--lstm', type=str2bool, default=False,
+                 help='engine mode, a3c: the 256-cell LSTM policy head (BASELINE config 5, DESIGN §4b)')
+  p.add_argument('--dqn_type', choices=['nips', 'nature'], default='nips',
+                 help="conv trunk of network.py:30-50 (Network(DQN_type=...)); the engine fuses the nips "
+                      "trunk, nature runs through src/network.Network only")
   p.add_argument('--logdir', default='./logs')
   return p.parse_args(argv)
+
+
+def engine_options(flags):
+  """The reference options of --mode engine: each one either reaches the Engine or is rejected,
+  so no option is silently dropped (agent.py:176-184 double-Q, :234-249 dueling, network.py:30-42
+  nature trunk).  Returns the Engine keyword arguments the flags select."""
+  if flags.dueling:
+    raise ValueError('--dueling (agent.py:234-249) is not fused into the engine: use --mode agent')
+  if flags.dqn_type != 'nips':
+    raise ValueError('--dqn_type %s: the engine fuses the nips trunk (network.py:43-50); the nature trunk '
+                     'runs through src/network.Network' % flags.dqn_type)
+  if flags.double_q and flags.algo != 'q':
+    raise ValueError('--double_q is a Q-learning option (agent.py:176-184): use it with --algo q')
+  if flags.lstm and flags.algo != 'a3c':
+    raise ValueError('--lstm is an A3C policy head: use it with --algo a3c')
+  kw = dict(lstm=bool(flags.lstm))
+  if flags.double_q:
+    kw['double_q'] = True
+  return kw
 
 
 def initial_params(eng, action_size, algo, seed):
@@ -136,6 +160,7 @@ def run_engine(config, flags):
   torch.cuda.set_device(local)
   A, lives = game_spec(config.env_name)
   E = flags.num_envs
+  net_kw = engine_options(flags)
   opts = dict(gamma=config.discount, discount=config.discount, beta=config.beta, learning_rate=config.learning_rate,
               max_step=config.max_step, decay=config.decay, momentum=config.momentum, epsilon=config.epsilon,
               clip_norm=config.clip_norm, literal_adv=int(config.literal_adv), ep_start=config.ep_start,
@@ -145,14 +170,15 @@ def run_engine(config, flags):
   host = flags.envs_on != 'device'
   if host and flags.update == 'hogwild':
     raise ValueError('--envs_on host/gym drives a synchronous engine; use --update sync or overlap')
-  overlap = flags.update == 'overlap' and not host
+  # hogwild overlaps the push / pull of rollout k-1 with rollout k (src/engine.py iterate_hogwild)
+  overlap = flags.update in ('overlap', 'hogwild') and not host
   if flags.update == 'overlap' and not overlap and rank == 0:
     print('main.py: --update overlap needs device envs; running the synchronous engine',
           file=sys.stderr, flush=True)
   pool = make_host_pool(config, flags, E, A, lives, rank) if host else None
   eng = Engine(num_envs=E, n_step=flags.n_step, action_size=A, algo=flags.algo, start_lives=lives,
                num_frames=1 if host else flags.num_frames, seed=flags.random_seed, env_id_base=rank * E,
-               world_size=world, overlap=overlap, external_env=host, **opts)
+               world_size=world, overlap=overlap, external_env=host, **net_kw, **opts)
   ns = param_names_shapes(A, flags.algo, lstm=eng.lstm)
   # checkpoints: <logdir>/<model_dir> as the Supervisor's logdir (main.py:75), Saver max_to_keep
   # (agent.py:29); restored at start as managed_session does (main.py:90)
@@ -282,6 +308,7 @@ def main(argv=None):
     config.max_step = flags.max_step
   config.algo, config.n_step, config.num_envs = flags.algo, flags.n_step, flags.num_envs
   if flags.mode == 'engine':
+    engine_options(flags)             # reject unsupported reference options before any device work
     return run_engine(config, flags)
   return run_agent(config, flags)
 

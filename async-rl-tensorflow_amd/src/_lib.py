@@ -8,6 +8,7 @@ library or a gfx950 device is missing.
 """
 import ctypes
 import os
+import sys
 
 import torch
 
@@ -39,7 +40,8 @@ class EngineConfig(ctypes.Structure):
                 ('clip_norm', c_float), ('literal_adv', c_int), ('ep_start', c_float),
                 ('ep_end', c_float), ('ep_end_t', c_i64), ('learn_start', c_i64),
                 ('target_q_update_step', c_i64), ('discount', c_double), ('overlap', c_int),
-                ('external_env', c_int), ('frame84', c_int), ('split_exchange', c_int)]
+                ('external_env', c_int), ('frame84', c_int), ('split_exchange', c_int),
+                ('double_q', c_int)]
 
 
 class EngineBuffers(ctypes.Structure):
@@ -148,6 +150,10 @@ SIGNATURES = {
 
 # diagnostics an A/B build from an earlier commit may lack (every other symbol is required)
 MEASUREMENT_ONLY = ('a3c_engine_span_steps', 'a3c_engine_span_raw')
+# entry points an older build selected with A3C_LIB (A/B runs of earlier commits) may lack; any
+# other missing symbol is an error, and each one skipped is named on stderr
+OPTIONAL_IN_OLD_BUILDS = MEASUREMENT_ONLY + ('a3c_engine_exchange_split', 'a3c_engine_wait_grad_head',
+                                             'a3c_dev_alloc_kind', 'a3c_engine_time_kernel')
 
 KER_CONV12_FWD, KER_FC_FWD, KER_ENV_STEP, KER_CONV_BWD, KER_HEAD_SCREEN, KER_HEAD_SCREEN_CONV12, KER_FC_PART = 0, 1, 2, 3, 4, 5, 6
 
@@ -162,8 +168,13 @@ def lib():
             raise RuntimeError(f'{LIB_PATH} not built: run __graft_entry__.build() or make -C csrc')
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            if (name in MEASUREMENT_ONLY or os.environ.get('A3C_LIB')) and not hasattr(L, name):
-                continue          # (an older build selected by A3C_LIB for an A/B: no span dumps, ...)
+            if not hasattr(L, name):
+                if name in MEASUREMENT_ONLY:
+                    continue
+                if os.environ.get('A3C_LIB') and name in OPTIONAL_IN_OLD_BUILDS:
+                    print(f'[a3c] {LIB_PATH} lacks {name} (older build): skipped', file=sys.stderr)
+                    continue
+                raise RuntimeError(f'{LIB_PATH} does not export {name}: rebuild it (make -C csrc)')
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

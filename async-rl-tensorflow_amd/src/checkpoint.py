@@ -279,7 +279,7 @@ def restore_engine(saver, eng, names_shapes, rank=0, world=1):
         if path is not None:
             try:
                 w = int(load(path).get('world', -1))
-            except (OSError, ValueError):
+            except Exception:      # (a truncated zip raises BadZipFile, a short read EOFError, ...)
                 w = -2
             plan = (os.path.basename(path), 'exact' if w == world and not eng.external_env else 'params')
     plan = bcast(plan)
@@ -289,7 +289,7 @@ def restore_engine(saver, eng, names_shapes, rank=0, world=1):
     try:
         arrays = load(path)
         err = None
-    except (OSError, ValueError) as e:
+    except Exception as e:         # any failure goes through the agreed all_ok path below
         arrays, err = None, e
     if not all_ok(arrays is not None):
         raise RuntimeError('restore_engine: a rank cannot read %s (%s)' % (path, err or 'another rank'))
@@ -301,7 +301,7 @@ def restore_engine(saver, eng, names_shapes, rank=0, world=1):
                 eng.reset()
                 eng.load_state(state)
                 ok = True
-        except (OSError, ValueError, RuntimeError):
+        except Exception:
             ok = False
         if all_ok(ok):
             return int(arrays[STEP_KEY])

@@ -133,7 +133,7 @@ class PartitionedPS:
             t.copy_(self.gathered[:self.total])
 
     def apply(self, eng):
-        cut = getattr(eng, 'split_point', 0) if self.world > 1 else 0
+        cut = eng.split_point if self.world > 1 else 0
         if cut and self.split is None:
             cut = 0 if _host_staged(eng.grads, self.group) else cut
         if cut and self.split is not False:

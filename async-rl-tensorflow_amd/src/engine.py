@@ -186,6 +186,8 @@ class Engine:
     def split_point(self):
         """Split exchange (several GPUs): the float offset where the fc / head gradients start --
         clipped before the conv backward, so their exchange can run under it; 0: no split."""
+        if not hasattr(lib(), 'a3c_engine_exchange_split'):
+            return 0          # (an older build selected by A3C_LIB: the one-phase exchange, named on load)
         cut = _lib.c_i64()
         check(lib().a3c_engine_exchange_split(self._h, ctypes.byref(cut)), 'a3c_engine_exchange_split')
         return int(cut.value)
@@ -293,10 +295,17 @@ class Engine:
 
     def iterate_hogwild(self, ps):
         """Rollout + gradient, unlocked push of the (per-worker clipped) gradient into the
-        sharded Hogwild parameter server, pull of the shared parameters (src/hogwild.py)."""
-        if self.overlap:
-            raise ValueError('hogwild runs on a synchronous engine (overlap=False)')
+        sharded Hogwild parameter server, pull of the shared parameters (src/hogwild.py).
+
+        Overlap engine (the default of bench.py / main.py --update hogwild): rollout k runs on the
+        engine's rollout stream while the caller's stream back-propagates rollout k-1, pushes its
+        clipped gradient into every shard and pulls the shards into the parameter snapshot of
+        rollout k+1 -- the push and pull overlap the next rollout, at staleness 1 like the overlap
+        mode (the reference's workers keep acting while the PS applies, main.py:60-65).  Rollout
+        k+1 is enqueued behind that pull (the engine orders its rollout stream after the caller's)."""
         self.rollout_grad()
+        if not self.grad_ready:
+            return                      # overlap pipeline filling: no gradient yet
         if self.cfg.world_size == 1:
             # one worker: the engine fuses its clip into apply, which hogwild bypasses
             if not hasattr(self, '_clip_ws'):
@@ -307,10 +316,13 @@ class Engine:
                                        _lib.i64_array(self.sizes), float(self.cfg.clip_norm), None,
                                        _lib.ptr(self._clip_ws), _lib.stream_handle()), 'a3c_clip_grads')
         ps.push(self.grads, lr_dev=self.sched_ptr)
-        ps.pull(self.params)
-        # counters, and for q the target copy of the pulled (global) weights when the global step
-        # crossed a multiple of target_q_update_step (agent.py:166-167, 342-344)
-        self.apply_commit(None)
+        # counters, the overlap snapshot, and for q the target copy of the pulled (global) weights
+        # when the global step crossed a multiple of target_q_update_step (agent.py:166-167, 342-344)
+        if ps.world == 1:
+            self.apply_commit(ps.params_view())     # the one shard is the whole vector: pull = commit
+        else:
+            ps.pull(self.params)
+            self.apply_commit(None)
 
     # ---------------------------------------------------------------- host-stepped envs
     def ext_begin(self, rgb):

@@ -121,6 +121,11 @@ class HogwildPS:
             check(lib().a3c_copy_params(ctypes.c_void_p(pp + 4 * self.lo[q]), ctypes.c_void_p(self.base[q]),
                                         self.n[q], stream_handle()), 'a3c_copy_params')
 
+    def params_view(self):
+        """world 1: the single shard's parameters (the whole flat vector) as a device tensor."""
+        assert self.world == 1
+        return self.own[0, :self.total]
+
     def sync_slots(self, eng):
         """The shared RMSProp slots (every shard's ms / mom) into the engine's full ms / mom
         buffers, which Hogwild does not otherwise use: checkpoints then hold the true slots."""

@@ -72,6 +72,9 @@ def parse():
                     help='overlap: rollout k overlaps backward+apply of rollout k-1 (stale-1 async A3C); '
                          'sync: rollout -> backward -> all-reduce -> apply; hogwild: unlocked pushes into a '
                          'sharded IPC parameter server, no collective (BASELINE config 4)')
+    ap.add_argument('--hogwild-sync', action='store_true',
+                    help='--update hogwild on a synchronous engine (push + pull after each rollout, no overlap); '
+                         'default: the push of rollout k-1 and the pull overlap rollout k (staleness 1)')
     ap.add_argument('--hogwild-memory', default='fine', choices=['fine', 'coarse', 'uncached'],
                     help='--update hogwild: allocation kind of the IPC-shared shards (DESIGN §7 memory model)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
@@ -84,10 +87,11 @@ def parse():
                     help='N > 1 sync/overlap: sequential = partitioned PS (all-to-all, every worker\'s clipped '
                          'gradient its own RMSProp step in rank order, all-gather: the reference PS rule); '
                          'sum = one SUM all-reduce + one step (plain data parallel)')
-    ap.add_argument('--min-seconds', type=float, default=1.0,
-                    help='repeat the K-step timed window until about this much time is measured; value = '
-                         'median window rate, spread reported')
-    ap.add_argument('--max-windows', type=int, default=50)
+    ap.add_argument('--min-seconds', type=float, default=2.0,
+                    help='repeat the K-step timed window until at least this much time is measured (a short '
+                         'K leaves a few ms of GPU time per window); value = median window rate, spread reported')
+    ap.add_argument('--max-windows', type=int, default=100000,
+                    help='upper bound on the window count (the default never binds before --min-seconds)')
     return ap.parse_args()
 
 
@@ -173,7 +177,8 @@ def main():
         raise SystemExit('--frames84 is a device-env pool mode')
     eng = Engine(num_envs=E, n_step=n, action_size=A, algo=args.algo, start_lives=lives, num_frames=args.frames,
                  seed=123, env_id_base=rank * E, world_size=world, use_graph=args.graph and not args.no_graph,
-                 overlap=args.update == 'overlap', lstm=args.lstm, external_env=host, frame84=int(args.frames84))
+                 overlap=args.update == 'overlap' or (args.update == 'hogwild' and not args.hogwild_sync),
+                 lstm=args.lstm, external_env=host, frame84=int(args.frames84))
     hpool = None
     if host:
         from src.host_env import SyntheticHostEnvPool
@@ -226,16 +231,16 @@ def main():
         step()
     barrier()
     torch.cuda.synchronize()
-    live = not host and args.update != 'hogwild'
+    live = not host and (eng.overlap or args.update == 'sync')
     if live:                      # live launch spans of the dominant kernels, recorded in-graph
         eng.span_stats(0, reset=True)
         eng.span_stats(1, reset=True)
-    # a short K-step window is a few ms of GPU time: repeat it until ~min_seconds are measured
-    # (every rank derives the same count from the max-over-ranks first window) and report the
-    # median window with the spread
+    # a short K-step window is a few ms of GPU time: repeat it until min_seconds are measured and
+    # report the median window with the spread (every rank sees the same max-over-ranks window
+    # times, so every rank stops at the same count)
     windows = [timed_window()]
-    nwin = max(1, min(args.max_windows, int(np.ceil(args.min_seconds / max(windows[0], 1e-9)))))
-    windows += [timed_window() for _ in range(nwin - 1)]
+    while sum(windows) < args.min_seconds and len(windows) < args.max_windows:
+        windows.append(timed_window())
     el = float(np.median(windows))
     spans = {}
     if live:
@@ -251,7 +256,7 @@ def main():
     if rank == 0 and not args.no_kernel_timing and not host:
         # overlap mode fuses step t+1's conv1+conv2 into step t's head+screen kernel
         # (k_head_screen_conv12, engine.hip conv_fused): conv12 then runs once per rollout
-        fused = args.update == 'overlap' and os.environ.get('A3C_FUSE_CONV', '1') != '0'
+        fused = eng.overlap and os.environ.get('A3C_FUSE_CONV', '1') != '0'
         step_bytes = ENV_STEP_BYTES_84 if args.frames84 else ENV_STEP_BYTES
         ms = {
             'k_conv12_fwd': eng.time_kernel(_lib.KER_CONV12_FWD, 20),
@@ -361,7 +366,7 @@ def main():
                        'env_steps_per_step': world * E * n,
                        'parallelism': (f'dp{world} hogwild: unlocked RMSProp pushes into {world} IPC-mapped HBM '
                                        f'shards ({dict(fine="fine-grained", coarse="coarse-grained", uncached="uncached")[args.hogwild_memory]}) '
-                                       f'over xGMI, pull at rollout start, '
+                                       f'over xGMI, {"push + pull after each rollout" if args.hogwild_sync else "push of rollout k-1 + pull under rollout k (stale-1)"}, '
                                        f'no collective'
                                        if args.update == 'hogwild' else
                                        f'dp{world} partitioned PS: {coll} all-to-all of per-worker-clipped grads, '
@@ -369,12 +374,17 @@ def main():
                                        if args.exchange == 'sequential' else
                                        f'dp{world} all-reduce ({coll}) of per-worker-clipped grads, one summed step')
                        if world > 1 else 'dp1', 'hipgraph': args.graph and not args.no_graph,
+                       # every A3C_* switch set in the environment (a release library reads only the
+                       # documented ones, a3c_common.h A3C_KNOB; {} = the defaults)
+                       'env_knobs': {k: v for k, v in sorted(os.environ.items()) if k.startswith('A3C_')},
                        'update': {'overlap': 'overlap: rollout k uses params after update k-2 (stale-1 async), '
                                              'backward+apply of k-1 concurrent with rollout k',
                                   'sync': 'synchronous: rollout -> backward -> apply',
-                                  'hogwild': 'hogwild: sharded lock-free parameter server (reference PS semantics)'
+                                  'hogwild': 'hogwild: sharded lock-free parameter server (reference PS semantics)' +
+                                             ('' if args.hogwild_sync else ', overlapped with the next rollout (stale-1)')
                                   }[args.update]},
             'timing': {'windows': len(windows), 'steps_per_window': args.steps,
+                       'timed_seconds': round(sum(windows), 3),
                        'window_ms': [round(w * 1e3, 3) for w in windows],
                        'value_spread': [round(steps_total / max(windows), 1), round(steps_total / min(windows), 1)],
                        'value_mean_over_windows': round(steps_total * len(windows) / sum(windows), 1)},

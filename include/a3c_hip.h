@@ -300,6 +300,10 @@ typedef struct a3c_engine_config {
                         stream under the conv backward (a3c_engine_wait_grad_head); only the
                         conv tensors' exchange waits for the whole backward.  Gradients are
                         bit-identical either way.  Default 1.                                 */
+  int double_q;       /* q only: double Q-learning (agent.py:176-184) -- the TD target of transition
+                        t takes the target net's q of s_{t+1} at the online net's argmax action
+                        (the rollout's own q rows, plus one online forward of the bootstrap state
+                        s_n) instead of the target net's max.  Default 0.                     */
 } a3c_engine_config;
 
 void a3c_engine_config_default(a3c_engine_config* cfg);

@@ -24,7 +24,7 @@ class EngineRef:
                  gamma=0.99, beta=0.01, learning_rate=0.0007, max_step=80_000_000, decay=0.99,
                  momentum=0.0, epsilon=0.1, clip_norm=40.0, literal_adv=False, ep_start=1.0,
                  ep_end_t=4_000_000, learn_start=32, target_q_update_step=40_000, discount=0.99,
-                 dtype=np.float64, lstm=False, frame84=False):
+                 dtype=np.float64, lstm=False, frame84=False, double_q=False):
         self.algo, self.A, self.E, self.n = algo, int(action_size), int(num_envs), int(n_step)
         self.seed = int(seed)
         self.k0, self.k1 = px.seed_key(seed)
@@ -47,6 +47,9 @@ class EngineRef:
                       ep_start=ep_start, ep_end_t=ep_end_t, learn_start=learn_start,
                       target_q_update_step=target_q_update_step, discount=discount)
         self.dtype = dtype
+        self.double_q = bool(double_q)     # agent.py:176-184 (q only)
+        if self.double_q and algo != 'q':
+            raise ValueError('double_q is a Q-learning option')
         # C5 LSTM head (ref_cpu.lstm_*): recurrent state carried across iterations, zeroed after a
         # terminal transition
         self.lstm = bool(lstm)
@@ -169,8 +172,14 @@ class EngineRef:
         else:
             nxt = np.concatenate([self.states(self.tau + t + 1) for t in range(n)])
             qn = R.forward(self.tparams, nxt, 'q', dtype=self.dtype, keep=False)['z']
-            target = R.td_target(rewards.reshape(-1), terms.reshape(-1), qn.astype(np.float32),
-                                 h['discount']).astype(np.float32)
+            if self.double_q:      # the online net's argmax on s_{t+1}, the target net's value there
+                qo = R.forward(self.params, nxt, 'q', dtype=self.dtype, keep=False)['z']
+                target = R.td_target_double(rewards.reshape(-1), terms.reshape(-1), qn.astype(np.float32),
+                                            qo[:, :A].astype(np.float32), h['discount']).astype(np.float32)
+                out['q_next_online'] = qo
+            else:
+                target = R.td_target(rewards.reshape(-1), terms.reshape(-1), qn.astype(np.float32),
+                                     h['discount']).astype(np.float32)
         out['target'] = target.reshape(n, E)
         if not grads:
             return out

@@ -295,6 +295,16 @@ def td_target(reward, terminal, q_next, discount=0.99):
         np.asarray(reward, np.float64)
 
 
+def td_target_double(reward, terminal, q_next_target, q_next_online, discount=0.99):
+    """agent.py:176-184 (double Q-learning) in float64: pred_action = argmax_a Q(s') of the online
+    net (q_action = tf.argmax: the first maximum), then (1 - term) * discount * Q'(s', pred_action)
+    + reward with the target net's Q'."""
+    pred = np.argmax(np.asarray(q_next_online), axis=1)
+    qt = np.asarray(q_next_target, np.float64)[np.arange(len(pred)), pred]
+    terminal = np.asarray(terminal) + 0.
+    return (1. - terminal) * discount * qt + np.asarray(reward, np.float64)
+
+
 def a3c_loss_and_dz(z, actions, R, beta=0.01, literal_advantage_grad=False):
     """network.py:81-94 with the two bugs fixed: V squeezed to [N]
     and log pi(a) = log_softmax gathered at a.  Per-sample

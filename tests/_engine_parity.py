@@ -25,7 +25,7 @@ def rel_l2(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
 
 
-REF_KEYS = ('target_q_update_step', 'learning_rate', 'frame84')
+REF_KEYS = ('target_q_update_step', 'learning_rate', 'frame84', 'double_q')
 
 
 def build(algo, A, E, n, lives, seed, frames=48, use_graph=False, scale=4.0, **kw):
@@ -167,18 +167,28 @@ def check_sync_vs_oracle(algo, A, E, n, lives, iters=3, seed=None, frames=48, sc
     return eng, ref
 
 
-def check_overlap_vs_oracle(A, E, n, lives, rollouts=5, seed=77, frames=48, scale=4.0, algo='a3c', **kw):
+def check_overlap_vs_oracle(A, E, n, lives, rollouts=5, seed=77, frames=48, scale=4.0, algo='a3c', hogwild=False,
+                            **kw):
     """Overlap (stale-1) pipeline: rollout k uses the parameters after update k-2.  The oracle is
     replayed in that order with the engine's own actions and activations.  algo='q': the TD targets
     of rollout k-1 are formed by its backward, after rollout k, with the target network as it
     stands then (synced by apply k-2 at the latest), so the replay recomputes them from the
-    rollout's next-state planes with the oracle's target parameters at that point."""
+    rollout's next-state planes with the oracle's target parameters at that point.
+    hogwild=True: the engine runs Engine.iterate_hogwild on a one-shard HogwildPS (the clipped
+    gradient of rollout k-1 pushed and the shard pulled under rollout k): the same stale-1 replay."""
     if algo == 'q':
         kw.setdefault('target_q_update_step', 40)
     eng, ref, ns = build(algo, A, E, n, lives, seed=seed, frames=frames, scale=scale, overlap=True, **kw)
+    ps = None
+    if hogwild:
+        from src.hogwild import HogwildPS
+        ps = HogwildPS(eng.params)
     hist = []                  # per rollout: (oracle params used, planes, oracle out)
     for k in range(rollouts):
-        eng.iterate()
+        if ps is not None:
+            eng.iterate_hogwild(ps)
+        else:
+            eng.iterate()
         torch.cuda.synchronize()
         sl = eng.slot(k & 1)
         Pk = {kk: v.copy() for kk, v in ref.params.items()}
@@ -205,23 +215,36 @@ def check_overlap_vs_oracle(A, E, n, lives, rollouts=5, seed=77, frames=48, scal
         want = out_p['target']
         if algo == 'q':
             qn = Rc.forward(ref.tparams, out_p['next_states'], 'q', keep=False)['z']
-            want = Rc.td_target(out_p['rewards'].reshape(-1), out_p['terminals'].reshape(-1),
-                                qn.astype(np.float32), ref.h['discount']).astype(np.float32).reshape(n, E)
+            if kw.get('double_q'):     # the argmax of the online net the rollout ran (its q rows)
+                qo = Rc.forward(Pp, out_p['next_states'], 'q', keep=False)['z']
+                want = Rc.td_target_double(out_p['rewards'].reshape(-1), out_p['terminals'].reshape(-1),
+                                           qn.astype(np.float32), qo[:, :A].astype(np.float32),
+                                           ref.h['discount']).astype(np.float32).reshape(n, E)
+            else:
+                want = Rc.td_target(out_p['rewards'].reshape(-1), out_p['terminals'].reshape(-1),
+                                    qn.astype(np.float32), ref.h['discount']).astype(np.float32).reshape(n, E)
         np.testing.assert_allclose(tgt, want, rtol=1e-5, atol=1e-5)
         losses, g_same = same_act_grads(slp, planes_p, Pp, algo, A, n, E, tgt)
         assert_losses(eng.loss.cpu().numpy(), losses, algo, k)
         G = unflat(eng, ns, eng.grads)
+        if ps is not None:     # (hogwild clips the buffer in place before its push)
+            g_same_c = {kk: Rc.clip_by_norm(v, 40.0) for kk, v in g_same.items()}
         for name, _ in ns:
-            assert rel_l2(G[name], g_same[name]) < 1e-4, (k, name, rel_l2(G[name], g_same[name]))
-            if algo == 'a3c':    # (q: the rollout-time oracle targets are not the late ones)
+            want_g = g_same_c[name] if ps is not None else g_same[name]
+            assert rel_l2(G[name], want_g) < 1e-4, (k, name, rel_l2(G[name], want_g))
+            if algo == 'a3c' and ps is None:    # (q: the rollout-time oracle targets are not the late ones)
                 assert rel_l2(G[name], out_p['grads'][name]) < 2e-2, (k, name)
         ref.apply({kk: Rc.clip_by_norm(v, 40.0) for kk, v in g_same.items()}, advance_tau=False, tau=out_p['tau'])
         assert_params(eng, ns, ref, k)
+        if ps is not None:
+            assert torch.equal(ps.gather(), eng.params)
         assert int(eng.counters[1].item()) == ref.global_step
         if algo == 'q':
             T = unflat(eng, ns, eng.target_params)
             for name, _ in ns:
                 np.testing.assert_allclose(T[name], ref.tparams[name], rtol=1e-5, atol=1e-6)
+    if ps is not None:
+        ps.close()
     return eng, ref
 
 

@@ -159,6 +159,19 @@ def test_q_overlap_stale_semantics_match_oracle(E, tq):
                             target_q_update_step=tq)
 
 
+@pytest.mark.parametrize('overlap', [False, True], ids=['sync', 'overlap'])
+def test_double_q_matches_oracle(overlap):
+    """--double_q (agent.py:176-184): the TD target takes the target net's q of s_{t+1} at the
+    online net's argmax -- the engine's own q rows of the rollout plus one online forward of the
+    bootstrap state s_n -- checked against the oracle's double-Q targets, then losses, gradients
+    and parameters as for the vanilla target (overlap: the online net is the one the rollout ran)."""
+    if overlap:
+        check_overlap_vs_oracle(6, 8, 5, 3, rollouts=6, seed=57, learning_rate=3e-3, algo='q',
+                                target_q_update_step=100, double_q=1)
+    else:
+        check_sync_vs_oracle('q', 6, 4, 8, 3, iters=4, learning_rate=3e-3, double_q=1)
+
+
 def test_stream_ordering_modes_are_bit_identical(monkeypatch):
     """Overlap pipeline: ordering the rollout and backward streams by stream wait-value operations
     on device counters (default) or by HIP events gives the same training, bit for bit."""

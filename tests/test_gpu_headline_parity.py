@@ -62,15 +62,18 @@ def test_c3_breakout_shard_matches_oracle(overlap):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize('mode', ['overlap', 'sync', 'hogwild'])
+@pytest.mark.parametrize('mode', ['overlap', 'sync', 'hogwild', 'hogwild-sync'])
 def test_c4_512_env_shard_matches_oracle(mode):
-    """C4 per GPU: Pong, 512 envs, in the three update modes (Hogwild at world 1: one worker's
-    clip + unlocked push + pull equals the oracle's clip + RMSProp)."""
+    """C4 per GPU: Pong, 512 envs, in the update modes (Hogwild at world 1: one worker's clip +
+    unlocked push + pull equals the oracle's clip + RMSProp -- overlapped with the next rollout at
+    staleness 1, bench.py's default, or after each rollout)."""
     kw = dict(seed=44, frames=1024, scale=4.0, learning_rate=2e-3)
     if mode == 'overlap':
         check_overlap_vs_oracle(6, 512, 5, 0, rollouts=3, **kw)
     elif mode == 'sync':
         check_sync_vs_oracle('a3c', 6, 512, 5, 0, iters=2, **kw)
+    elif mode == 'hogwild':
+        check_overlap_vs_oracle(6, 512, 5, 0, rollouts=3, hogwild=True, **kw)
     else:
         check_hogwild1_vs_oracle(6, 512, 5, 0, iters=2, **kw)
 

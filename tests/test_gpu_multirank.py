@@ -38,7 +38,7 @@ TQ = 2000       # q target period: with 64 envs x 5 steps x 4 ranks (1,280 per u
 
 
 def _cfg(cfg):
-    c = dict(A=A, lives=0, lstm=False, algo='a3c', E=E, n=N, tq=TQ, split=1)
+    c = dict(A=A, lives=0, lstm=False, algo='a3c', E=E, n=N, tq=TQ, split=1, ov=False)
     c.update(cfg or {})
     return c
 
@@ -338,25 +338,45 @@ def test_partitioned_ps_ranks(world, overlap, cfg, oracle):
         assert any(a['target'] != b['target'] for a, b in zip(recs[0], recs[0][1:]))
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('overlap', [False, True], ids=['sync', 'overlap'])
+def test_split_exchange_equals_one_phase(overlap):
+    """The two-phase exchange (fc / head range under the conv backward, then the conv prefix) and
+    the one-phase exchange after the whole backward, from one seed at world 2: the backward of
+    either sums every gradient in the same order (the split backward takes the fc weight GEMM form
+    of the one-phase backward of the same configuration, net_bwd.hip), so the parameters, counters
+    and per-iteration records are bit-identical."""
+    two = _run_ranks(_pps_worker, 2, (overlap, dict(split=1)))
+    one = _run_ranks(_pps_worker, 2, (overlap, dict(split=0)))
+    for r in range(2):
+        np.testing.assert_array_equal(two[r]['params'], one[r]['params'])
+        assert two[r]['step'] == one[r]['step']
+        assert two[r]['recs'] == one[r]['recs'], r
+
+
 # ------------------------------------------------------------------ Hogwild (SURVEY §8(e) async)
 def _hog_worker(rank, world, port, out, lockstep, cfg):
     _worker_env(rank, world, port)
     import torch.distributed as dist
     from src.hogwild import HogwildPS
     dist.init_process_group('gloo')
-    eng = _make(rank, world, False, cfg)
+    ov = _cfg(cfg)['ov']
+    eng = _make(rank, world, ov, cfg)
     ps = HogwildPS(eng.params)
     for it in range(ITERS):
         if lockstep:                      # deterministic order for the check: rank 0, then rank 1, ...
+            # (overlap: rollout k and the backward of k-1; the push / pull of k-1's gradient land in
+            # the snapshot of rollout k+1, as iterate_hogwild does)
             for turn in range(world):
                 dist.barrier()
                 if turn == rank:
                     eng.rollout_grad()
-                    ps.push(eng.grads, lr_dev=eng.sched_ptr)
+                    if eng.grad_ready:
+                        ps.push(eng.grads, lr_dev=eng.sched_ptr)
                     torch.cuda.synchronize()
             dist.barrier()
             ps.pull(eng.params)
-            eng.apply_commit(None)        # target copy (q) of the pulled params, counters
+            eng.apply_commit(None)        # target copy (q) of the pulled params, snapshot, counters
             torch.cuda.synchronize()
         else:
             eng.iterate_hogwild(ps)
@@ -371,9 +391,12 @@ def _hog_worker(rank, world, port, out, lockstep, cfg):
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize('world,lockstep,cfg', [(2, True, {}), (2, False, {}), (4, True, {}), (4, False, {}),
-                                                (2, True, dict(algo='q', tq=300)), (4, True, dict(algo='q', A=4, lives=5, tq=300))],
+                                                (2, True, dict(algo='q', tq=300)), (4, True, dict(algo='q', A=4, lives=5, tq=300)),
+                                                (2, True, dict(ov=True)), (4, False, dict(ov=True)),
+                                                (2, True, dict(algo='q', tq=300, ov=True))],
                          ids=['w2-lockstep', 'w2-free', 'w4-lockstep', 'w4-free', 'w2-q-lockstep',
-                              'w4-q-breakout-lockstep'])
+                              'w4-q-breakout-lockstep', 'w2-overlap-lockstep', 'w4-overlap-free',
+                              'w2-q-overlap-lockstep'])
 def test_hogwild_sharded_ps(world, lockstep, cfg):
     """`world` ranks on one GPU push into each other's IPC-mapped shards.  Lock-step order must
     equal a single process applying every rank's clipped gradient in rank order each iteration
@@ -390,10 +413,21 @@ def test_hogwild_sharded_ps(world, lockstep, cfg):
     # replay: the engines, one shared RMSProp state applied in the same order
     import ctypes
     from src._lib import lib, ptr, stream_handle
-    engs = [_make(r, world, False, cfg) for r in range(world)]
+    engs = [_make(r, world, c['ov'], cfg) for r in range(world)]
     w = engs[0].params.clone()
     ms, mom = torch.ones_like(w), torch.zeros_like(w)
-    for it in range(ITERS):
+    for it in range(ITERS if c['ov'] else 0):     # overlap: rollout k, push / pull of rollout k-1
+        for e in engs:
+            e.rollout_grad()
+        if not engs[0].grad_ready:
+            continue
+        for e in engs:
+            lib().a3c_rmsprop_range(ptr(w), ptr(ms), ptr(mom), ptr(e.grads), w.numel(), ctypes.c_void_p(e.sched_ptr),
+                                    0.0, 0.99, 0.0, 0.1, stream_handle())
+        for e in engs:
+            e.params.copy_(w)
+            e.apply_commit(None)
+    for it in range(0 if c['ov'] else ITERS):
         for e in engs:          # every engine of an iteration uses the start-of-iteration params
             e.params.copy_(w)
         for e in engs:
@@ -408,6 +442,6 @@ def test_hogwild_sharded_ps(world, lockstep, cfg):
     for r in range(world):
         np.testing.assert_array_equal(engs[r].params.cpu().numpy(), res[r]['params'])
         np.testing.assert_array_equal(engs[r].target_params.cpu().numpy(), res[r]['target'])
-        assert res[r]['step'] == ITERS * c['n'] * c['E'] * world
+        assert res[r]['step'] == (ITERS - (1 if c['ov'] else 0)) * c['n'] * c['E'] * world
     if c['algo'] == 'q':    # the target copy fired (tq 300: at updates 1 and 3 at world 2, every update at 4)
         assert not np.array_equal(res[0]['target'], _make(0, world, False, cfg).target_params.cpu().numpy())

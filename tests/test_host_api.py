@@ -86,3 +86,45 @@ def test_network_value_errors_before_device():
         Network(None, 'NCWH', 4, 84, 84, 6, DQN_type='nips')
     with pytest.raises(ValueError, match='Wrong DQN type'):
         Network(None, 'NHWC', 4, 84, 84, 6, DQN_type='')
+
+
+@pytest.mark.parametrize('argv,want', [
+    ([], dict(lstm=False)),
+    (['--lstm', 'true'], dict(lstm=True)),
+    (['--algo', 'q', '--double_q', 'true'], dict(lstm=False, double_q=True)),
+    (['--algo', 'q'], dict(lstm=False)),
+])
+def test_engine_mode_honours_reference_options(argv, want):
+    """main.py --mode engine passes every reference option it supports into the Engine config:
+    --lstm (config 5), --double_q (agent.py:176-184, implemented in the engine's TD target)."""
+    import main
+    assert main.engine_options(main.parse_flags(['--mode', 'engine'] + argv)) == want
+
+
+@pytest.mark.parametrize('argv,match', [
+    (['--dueling', 'true'], 'dueling'),
+    (['--algo', 'q', '--dueling', 'true'], 'dueling'),
+    (['--dqn_type', 'nature'], 'nature'),
+    (['--double_q', 'true'], 'Q-learning option'),
+    (['--algo', 'q', '--lstm', 'true'], 'A3C policy head'),
+])
+def test_engine_mode_rejects_unsupported_options(argv, match):
+    """... and rejects the ones the fused engine does not implement, before any device work, so a
+    user asking for them never silently gets the vanilla network (agent.py:234-249 dueling,
+    network.py:30-42 nature trunk)."""
+    import main
+    with pytest.raises(ValueError, match=match):
+        main.main(['--mode', 'engine'] + argv)
+
+
+def test_double_q_target_oracle():
+    """oracle td_target_double (agent.py:176-184): the target net's value at the ONLINE net's
+    argmax (first maximum on ties), which differs from max_a Q' when the nets disagree."""
+    from oracle import ref_cpu as R
+    qt = np.array([[1.0, 5.0, 2.0], [3.0, 3.0, 0.0], [0.0, 1.0, 9.0]], np.float32)
+    qo = np.array([[9.0, 0.0, 0.0], [2.0, 2.0, 1.0], [0.0, 0.0, 7.0]], np.float32)
+    r = np.array([1.0, 0.0, -1.0], np.float32)
+    term = np.array([0, 0, 1], np.uint8)
+    got = R.td_target_double(r, term, qt, qo, 0.5)
+    np.testing.assert_array_equal(got, [1.0 + 0.5 * 1.0, 0.5 * 3.0, -1.0])
+    assert not np.array_equal(got, R.td_target(r, term, qt, 0.5))
