@@ -494,7 +494,8 @@ static bool spans_on() {
 // conv fusion (k_head_screen_conv12) runs with the device envs and the fused screen
 static bool conv_fused(const a3c_engine* e) { return e->fuse_conv && !e->ext && e->fused_screen; }
 // the fused rollout's fc as K-slice partials folded by the head (feed-forward head only)
-static bool fc_split(const a3c_engine* e) { return conv_fused(e) && e->fc_split && !e->L.lstm; }
+// (the LSTM head: the cell kernel folds them, k_lstm_fwd)
+static bool fc_split(const a3c_engine* e) { return conv_fused(e) && e->fc_split; }
 
 __global__ void k_advance_tau(int64_t* counters, int n) { counters[0] += n; }
 

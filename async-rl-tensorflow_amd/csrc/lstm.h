@@ -12,6 +12,12 @@ struct LstmStep {
   const float* c_src;
   const uint8_t* prev_terms;
   float *hp, *cp, *gates, *h, *c;
+  // the cell's input as the fc layer's FC_NS K-slice partials (a3c_fc_part_launch), folded by the
+  // cell kernel in slice order + fc bias + ReLU (as the feed-forward head folds them); the folded
+  // rows go to l3_out (the backward's act_l3).  nullptr: x is the finished fc output
+  const float* fc_part = nullptr;
+  const float* fc_bias = nullptr;
+  float* l3_out = nullptr;
 };
 
 int a3c_lstm_fwd_launch(const float* bias, const float* x, const LstmStep& st, int64_t B, hipStream_t s);

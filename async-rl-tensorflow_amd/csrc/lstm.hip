@@ -47,28 +47,79 @@ __device__ inline f32x4 mfma_k16(const f32x4 a, const f32x4 b, f32x4 c) {
 
 // cell step: workgroup = 16 envs x 16 units x 4 gates, 8 waves = (gate g, K half kh): kh 0 runs
 // x @ W[0:256], kh 1 runs h_prev @ W[256:512] (rows of terminal-masked envs zeroed afterwards:
-// (keep h) W = keep (h W)).  All 16 k-blocks of both operands are loaded up front.
+// (keep h) W = keep (h W)).  The tile's 16 rows of [x, h_prev] (32 KB) are staged in LDS once and
+// shared by the 4 gate waves of each half (each wave loaded them itself before round 5: 4x the
+// operand traffic); with st.fc_part the x rows are folded there from the fc's K-slice partials
+// (slice order + bias + ReLU, the feed-forward head's fold) and written to st.l3_out by the
+// workgroups of unit tile 0, so the fc needs no separate finishing pass.  The W rows of the
+// wave's 16 units (16 KB) go straight to registers, issued first.
+#define LSTM_LD (FC + 4)            // LDS row of the [x, h] tile: 260 floats (row r starts 4 r banks on)
 __global__ void __launch_bounds__(512) k_lstm_fwd(const float* __restrict__ X, const float* __restrict__ bias,
                                                   LstmStep st, int64_t B) {
+  __shared__ __attribute__((aligned(16))) float As[2][LT][LSTM_LD];
   __shared__ float Gs[2][4][LT][LT + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = w & 3, kh = w >> 2, i16 = lane & 15, j4 = lane >> 4;
   const int64_t e0 = (int64_t)blockIdx.x * LT;
   const int u0 = blockIdx.y * LT;
-  const int64_t er = min(e0 + i16, B - 1);
-  const float* pa = (kh ? st.h_src : X) + er * FC + 4 * j4;
   const float* pw = st.wt + (int64_t)(g * LSTM_U + u0 + i16) * LSTM_K + kh * FC + 4 * j4;
-  f32x4 a[FC / 16], b[FC / 16];
+  f32x4 b[FC / 16];
 #pragma unroll
-  for (int it = 0; it < FC / 16; ++it) {
-    a[it] = *(const f32x4*)(pa + 16 * it);
-    b[it] = *(const f32x4*)(pw + 16 * it);
+  for (int it = 0; it < FC / 16; ++it) b[it] = *(const f32x4*)(pw + 16 * it);
+  // stage [x, h_prev] of the tile's 16 envs: 2 x 16 x 64 chunks of 4 floats, 4 per thread
+  // (chunks 0..1023 the x half: thread tid's q = 0, 1; 1024..2047 the h half: q = 2, 3)
+  constexpr int NCH = 2 * LT * (FC / 4);
+  static_assert(NCH == 4 * 512 && LSTM_U == FC, "tile staging");
+  f32x4 xin[2], hin[2];
+  if (st.fc_part) {
+    f32x4 p[2][FC_NS];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = tid + 512 * q, row = c >> 6, c4 = c & 63;
+      const int64_t e = min(e0 + row, B - 1);
+#pragma unroll
+      for (int x = 0; x < FC_NS; ++x) p[q][x] = *(const f32x4*)(st.fc_part + ((int64_t)x * B + e) * FC + 4 * c4);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = tid + 512 * q, row = c >> 6, c4 = c & 63;
+      const int64_t e = min(e0 + row, B - 1);
+      hin[q] = *(const f32x4*)(st.h_src + e * FC + 4 * c4);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = tid + 512 * q, row = c >> 6, c4 = c & 63;
+      const f32x4 fb = *(const f32x4*)(st.fc_bias + 4 * c4);
+      f32x4 v = p[q][0];
+#pragma unroll
+      for (int x = 1; x < FC_NS; ++x) v += p[q][x];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + fb[r], 0.f);
+      xin[q] = v;
+      if (blockIdx.y == 0 && e0 + row < B) *(f32x4*)(st.l3_out + (e0 + row) * FC + 4 * c4) = v;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = tid + 512 * q, row = c >> 6, c4 = c & 63;
+      const int64_t e = min(e0 + row, B - 1);
+      xin[q] = *(const f32x4*)(X + e * FC + 4 * c4);
+      hin[q] = *(const f32x4*)(st.h_src + e * FC + 4 * c4);
+    }
   }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int c = tid + 512 * q, row = c >> 6, c4 = c & 63;
+    *(f32x4*)&As[0][row][4 * c4] = xin[q];
+    *(f32x4*)&As[1][row][4 * c4] = hin[q];
+  }
+  __syncthreads();
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const float* ar = &As[kh][i16][4 * j4];
 #pragma unroll
   for (int it = 0; it < FC / 16; it += 2) {
-    acc0 = mfma_k16(a[it], b[it], acc0);
-    acc1 = mfma_k16(a[it + 1], b[it + 1], acc1);
+    acc0 = mfma_k16(*(const f32x4*)(ar + 16 * it), b[it], acc0);
+    acc1 = mfma_k16(*(const f32x4*)(ar + 16 * it + 16), b[it + 1], acc1);
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -113,8 +164,9 @@ __global__ void __launch_bounds__(512) k_lstm_fwd(const float* __restrict__ X, c
 
 int a3c_lstm_fwd_launch(const float* bias, const float* x, const LstmStep& st, int64_t B, hipStream_t s) {
   if (B <= 0) return 0;
-  if (!st.wt || !bias || !x || !st.h_src || !st.c_src || !st.h || !st.c ||
-      (((uintptr_t)x | (uintptr_t)st.h_src | (uintptr_t)st.wt) & 15))
+  if (!st.wt || !bias || !st.h_src || !st.c_src || !st.h || !st.c || (!x && !st.fc_part) ||
+      (st.fc_part && (!st.fc_bias || !st.l3_out)) ||
+      (((uintptr_t)x | (uintptr_t)st.h_src | (uintptr_t)st.wt | (uintptr_t)st.fc_part) & 15))
     return a3c_set_error(A3C_ERR_INVALID, "a3c_lstm_step", "bad argument");
   hipLaunchKernelGGL(k_lstm_fwd, dim3((unsigned)((B + LT - 1) / LT), LSTM_U / LT), dim3(512), 0, s, x, bias, st, B);
   A3C_CHECK(hipGetLastError());

@@ -941,14 +941,22 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
   }
   // fused overlap rollout: the fc as K-slice partials, folded by the head of k_head_screen_conv12
   // (and the bootstrap state's, folded by k_head_fwd)
-  const bool part = fc_part && !ls && (next ? sel.mode >= 0 && sel.env_on && sel.ring : sel.mode < 0);
+  // C5: the LSTM cell folds the partials itself (k_lstm_fwd), on every step of a fused rollout
+  const bool part_lstm = fc_part && ls != nullptr;
+  const bool part = fc_part && (part_lstm || (next ? sel.mode >= 0 && sel.env_on && sel.ring : sel.mode < 0));
   int rc = part ? a3c_fc_part_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), fc_part, B, s)
                 : a3c_fc_fwd_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), P + L.off[T_FCB], act_l3, B, s,
                                     P + L.off[T_FCW]);
   if (rc) return rc;
   const float* head_in = act_l3;
   if (ls) {   // C5: LSTM cell on the fc output, heads on its h
-    rc = a3c_lstm_fwd_launch(P + L.off[T_LB], act_l3, *ls, B, s);
+    LstmStep st = *ls;
+    if (part_lstm) {
+      st.fc_part = fc_part;
+      st.fc_bias = P + L.off[T_FCB];
+      st.l3_out = act_l3;
+    }
+    rc = a3c_lstm_fwd_launch(P + L.off[T_LB], act_l3, st, B, s);
     if (rc) return rc;
     head_in = ls->h;
   }
@@ -956,7 +964,7 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
   const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
   if (sel.mode >= 0 && sel.env_on && sel.ring && next) {
     HeadSelect hs = sel;
-    if (part) {
+    if (part && !part_lstm) {
       hs.fc_part = fc_part;
       hs.fc_bias = P + L.off[T_FCB];
       hs.l3_out = act_l3;
@@ -968,7 +976,7 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
     return a3c_head_screen_launch(L, P, head_in, B, z, sel, s);
   else {
     HeadSelect hs = sel;
-    if (part) {
+    if (part && !part_lstm) {
       hs.fc_part = fc_part;
       hs.fc_bias = P + L.off[T_FCB];
       hs.l3_out = act_l3;

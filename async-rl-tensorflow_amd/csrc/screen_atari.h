@@ -187,15 +187,6 @@ __device__ inline void hpass_seg(const uint8_t* __restrict__ grow, uint8_t* __re
   }
 }
 
-// Whole-frame Environment.screen by one workgroup of NT threads (gray 210x160, the
-// horizontal-pass 210x84 and the vertical taps in LDS, SCREEN_FRAME_SMEM bytes); the RGB frame
-// streams from HBM straight into registers (all of a thread's loads issued before any use).
-// Both resampling passes give every wave the same amount of work with wave-uniform code:
-// horizontal = 16 tasks (column segment, block of 64 rows), lane = row; vertical = 28 tasks
-// of 3 output rows x 21 column quads, lane = (row, quad), taps read from the LDS table.
-#define SCREEN_KV_BYTES (84 * 8 * 4)
-#define SCREEN_FRAME_SMEM_NOKV (210 * 160 + 210 * 84 + 96)   // the tap table elsewhere (kvs_at)
-#define SCREEN_FRAME_SMEM (SCREEN_FRAME_SMEM_NOKV + SCREEN_KV_BYTES)
 // 4 u8 pixels (one dword, little-endian) -> 4 bf16 (exact: integers 0..255 are the upper half of
 // their f32)
 __device__ inline uint2 u8x4_to_bf16x4(uint32_t d) {
@@ -204,6 +195,139 @@ __device__ inline uint2 u8x4_to_bf16x4(uint32_t d) {
   return make_uint2(__builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u),
                     __builtin_amdgcn_perm(__float_as_uint(f3), __float_as_uint(f2), 0x07060302u));
 }
+
+// ---------------------------------------------------------------------------------------
+// Both resampling passes on the int8 matrix cores (v_mfma_i32_16x16x64_i8), bit-exact.
+// Pillow's pass is out = (2^21 + sum_t k_t v_t) >> 22 over 8-bit v and 22-bit taps k (every
+// output's taps sum to 2^22 - delta, delta in {0, 1}; taps_shift_only: no clip).  As an integer
+// GEMM on signed bytes:
+//   v = x' + 128 with x' = v ^ 0x80 (a signed byte),  k = 65536 d2 + 256 d1 + d0 in balanced
+//   base-256 digits d in [-128, 127] (k < 2^22: d2 <= 33),
+//   acc = ((((2^21 >> 16) + S2) << 8) + S1) << 8) - 128 delta + S0,   S_j = sum_t d_j x'_t
+// (three MFMAs chained by Horner shift-adds: the constants ride in the C input and the adds,
+// every partial an exact i32) = 2^21 + sum k x' - 128 delta, and since sum k v = sum k x' +
+// 128 (2^22 - delta):  2^21 + sum k v = acc + 2^29, so
+//   out = 128 + (acc >> 22)   (arithmetic shift),  and the output byte is (acc >> 22) ^ 0x80.
+// Horizontal: C[y][X] = sum_k gray[y][hbase + k] H[k][X] over 14 x 6 tiles of 16 rows x 16 outputs,
+// the K = 64 window of each output tile starting at a 16-aligned source column; the result is
+// written transposed, tmpT[X][y] (4 consecutive y per lane: one dword).  Vertical: C[x][yy] =
+// sum_k tmpT[x][vbase + k] V[k][yy] over 6 x 6 tiles, 4 consecutive x per lane: one dword of the
+// output row.  The B fragments (the tap digits) are compile-time tables in constant memory.
+// Lane layout of 16x16x64 i8 (tools/probes/mfma_i8_layout.hip): lane l holds A[l&15][16(l>>4)+j],
+// B[16(l>>4)+j][l&15], j = 0..15, and C[4(l>>4)+i][l&15], i = 0..3.
+// ---------------------------------------------------------------------------------------
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+constexpr int MT_N = 6;                 // 16-wide tiles over the 84 outputs of a pass (+12 pad)
+constexpr int TMPT_LD = 224;            // tmpT row: 210 source rows padded to a multiple of 16
+constexpr int H_MT = 14;                // 16-row tiles over the 210 source rows
+
+struct MfmaTab {
+  int8_t hb[MT_N][3][64][16];           // horizontal B fragments [n-tile][digit 2, 1, 0][lane][j]
+  int8_t vb[MT_N][3][64][16];           // vertical
+  int hbase[MT_N], vbase[MT_N];         // 16-aligned K-window starts (source column / row)
+  int hc0[MT_N * 16], vc0[MT_N * 16];   // -128 delta per output (0 in the pad)
+  bool ok;                              // every window covers its taps, digits in range
+  template <int IN, int OUT>
+  constexpr void fill(const Coef<IN, OUT>& c, int8_t (&b)[MT_N][3][64][16], int (&base)[MT_N], int (&c0)[MT_N * 16]) {
+    constexpr int K = Coef<IN, OUT>::K;
+    for (int nt = 0; nt < MT_N; ++nt) {
+      base[nt] = c.xmin[16 * nt] / 16 * 16;
+      for (int n = 0; n < 16; ++n) {
+        const int o = 16 * nt + n;
+        long sum = 0;
+        if (o < OUT) {
+          for (int t = 0; t < K; ++t) sum += c.k[o][t];
+          if (c.xmin[o] + K - 1 - base[nt] >= 64 && c.k[o][K - 1] != 0) ok = false;
+          for (int t = 0; t < K; ++t)
+            if (c.k[o][t] != 0 && c.xmin[o] + t - base[nt] >= 64) ok = false;
+        }
+        c0[o] = o < OUT ? -128 * (int)((1L << A3C_PRECISION_BITS) - sum) : 0;
+        for (int k = 0; k < 64; ++k) {
+          const int t = base[nt] + k - (o < OUT ? c.xmin[o] : 0);
+          const int w = (o < OUT && t >= 0 && t < K) ? c.k[o][t] : 0;
+          const int d0 = ((w + 128) & 255) - 128, w1 = (w - d0) / 256;
+          const int d1 = ((w1 + 128) & 255) - 128, d2 = (w1 - d1) / 256;
+          if (d2 < -128 || d2 > 127) ok = false;
+          const int lane = n + 16 * (k >> 4), j = k & 15;
+          b[nt][0][lane][j] = (int8_t)d2;
+          b[nt][1][lane][j] = (int8_t)d1;
+          b[nt][2][lane][j] = (int8_t)d0;
+        }
+      }
+    }
+  }
+  constexpr MfmaTab() : hb(), vb(), hbase(), vbase(), hc0(), vc0(), ok(true) {
+    fill(kH, hb, hbase, hc0);
+    fill(kV, vb, vbase, vc0);
+  }
+};
+constexpr MfmaTab kTab{};
+static_assert(kTab.ok, "resampling tap windows / digits");
+__constant__ MfmaTab cTab = kTab;
+
+// one 16x16 output tile of a pass: A = 16 bytes of the lane's source row at `a_src` (LDS),
+// B = the tile's digit fragments, c0 = the lane's output correction; returns the 4 output bytes
+__device__ inline uint32_t resample_tile(const uint8_t* a_src, const int8_t (&b)[3][64][16], int lane, int c0) {
+  i32x4 a = *(const i32x4*)a_src;
+  a ^= (i32x4){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+  const i32x4 b2 = *(const i32x4*)b[0][lane], b1 = *(const i32x4*)b[1][lane], b0 = *(const i32x4*)b[2][lane];
+  i32x4 acc = {32, 32, 32, 32};                                     // 2^21 >> 16
+  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b2, acc, 0, 0, 0);
+  acc = acc << 8;
+  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1, acc, 0, 0, 0);
+  acc = (acc << 8) + c0;
+  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b0, acc, 0, 0, 0);
+  uint32_t packed = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) packed |= (((uint32_t)acc[i] >> 22) & 255u) << (8 * i);
+  return packed ^ 0x80808080u;
+}
+
+// horizontal pass: gray [210][160] -> tmpT [84][TMPT_LD] (transposed), 84 tiles over the waves
+template <int NT>
+__device__ inline void hpass_mfma(const uint8_t* __restrict__ gray, uint8_t* __restrict__ tmpT) {
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n = lane & 15, h = lane >> 4;
+  for (int q = wid; q < H_MT * MT_N; q += NT / 64) {
+    const int nt = q % MT_N, mt = q / MT_N;
+    const int y = min(16 * mt + n, IH - 1);
+    const uint32_t v = resample_tile(gray + y * IW + cTab.hbase[nt] + 16 * h, cTab.hb[nt], lane, cTab.hc0[16 * nt + n]);
+    const int X = 16 * nt + n;
+    if (X < OW) *(uint32_t*)(tmpT + X * TMPT_LD + 16 * mt + 4 * h) = v;
+  }
+}
+
+// vertical pass: tmpT -> the 84x84 screen (out, HBM ring slot) and, for the fused conv, the
+// same plane as bf16 in LDS
+template <int NT>
+__device__ inline void vpass_mfma(const uint8_t* __restrict__ tmpT, uint8_t* __restrict__ out, uint16_t* lds_bf16) {
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n = lane & 15, h = lane >> 4;
+  for (int q = wid; q < MT_N * MT_N; q += NT / 64) {
+    const int nt = q % MT_N, mt = q / MT_N;                 // nt: output rows yy, mt: columns x
+    const int x = min(16 * mt + n, OW - 1);
+    const uint32_t v = resample_tile(tmpT + x * TMPT_LD + cTab.vbase[nt], cTab.vb[nt], lane, cTab.vc0[16 * nt + n]);
+    const int yy = 16 * nt + n, x0 = 16 * mt + 4 * h;
+    if (yy < OH && x0 < OW) {
+      st_act((uint32_t*)(out + yy * OW + x0), v);
+      if (lds_bf16) *(uint2*)(lds_bf16 + yy * OW + x0) = u8x4_to_bf16x4(v);   // (fused conv12)
+    }
+  }
+}
+
+// Whole-frame Environment.screen by one workgroup of NT threads (gray 210x160 and the
+// transposed horizontal-pass image tmpT in LDS, SCREEN_FRAME_SMEM bytes); the RGB frame streams
+// from HBM straight into registers (all of a thread's loads issued before any use), the
+// luminance runs on the vector ALUs, both resampling passes on the int8 matrix cores (above).
+// -DSCREEN_VALU: the vector-ALU resampling passes of rounds 1-4 (A/B builds).
+#define SCREEN_KV_BYTES (84 * 8 * 4)
+#ifdef SCREEN_VALU
+#define SCREEN_FRAME_SMEM_NOKV (210 * 160 + 210 * 84 + 96)   // the tap table elsewhere (kvs_at)
+#define SCREEN_FRAME_SMEM (SCREEN_FRAME_SMEM_NOKV + SCREEN_KV_BYTES)
+#else
+#define SCREEN_FRAME_SMEM_NOKV (210 * 160 + 84 * 224)        // gray | tmpT
+#define SCREEN_FRAME_SMEM SCREEN_FRAME_SMEM_NOKV
+#endif
 
 struct NoScreenMid {
   __device__ void operator()() const {}
@@ -217,13 +341,14 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
                                     int* kvs_at = nullptr) {
   uint8_t* gray = smem;
   uint8_t* tmp = smem + IH * IW;
-  // [yy][8]: 7 taps, xmin -- after the scratch, or at kvs_at (written after mid())
-  int* kvs = kvs_at ? kvs_at : (int*)(tmp + IH * OW + 96);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr int NWV = NT / 64;
   constexpr int NUNIT = IH * IW / 4;                   // 8400 units of 4 pixels (12 bytes)
   constexpr int PER = (NUNIT + NT - 1) / NT;
+#ifdef SCREEN_VALU
+  // [yy][8]: 7 taps, xmin -- after the scratch, or at kvs_at (written after mid())
+  int* kvs = kvs_at ? kvs_at : (int*)(tmp + IH * OW + 96);
   // the vertical-tap table's loads are issued first and written after mid(): loads retire in
   // order (vmcnt), so waiting for one issued behind the frame would wait for the whole frame
   constexpr int NKV = OH * 8, PKV = (NKV + NT - 1) / NT;
@@ -233,6 +358,9 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
     const int i = min(tid + NT * j, NKV - 1);
     kv[j] = (i & 7) < KV ? cV.k[i >> 3][i & 7] : cV.xmin[i >> 3];
   }
+#else
+  (void)kvs_at;
+#endif
   uint3 r[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -242,9 +370,11 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
   if (dbg && tid == 0) dbg[14] = __builtin_readcyclecounter();
   mid();
   if (dbg && tid == 0) dbg[15] = __builtin_readcyclecounter();
+#ifdef SCREEN_VALU
 #pragma unroll
   for (int j = 0; j < PKV; ++j)
     if (tid + NT * j < NKV) kvs[tid + NT * j] = kv[j];
+#endif
   if (dbg && tid == 0) dbg[4] = __builtin_readcyclecounter() + (r[0].x & 0);   // first unit landed
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -254,6 +384,12 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
   if (dbg && tid == 0) dbg[5] = __builtin_readcyclecounter();
   __syncthreads();
   if (dbg && tid == 0) dbg[6] = __builtin_readcyclecounter();
+#ifndef SCREEN_VALU
+  hpass_mfma<NT>(gray, tmp);                           // tmp = tmpT [84][224]
+  __syncthreads();
+  if (dbg && tid == 0) dbg[7] = __builtin_readcyclecounter();
+  vpass_mfma<NT>(tmp, out, lds_bf16);
+#else
   for (int task = wid; task < 16; task += NWV) {
     const int seg = task & 3, rr = (task >> 2) * 64 + lane;
     if (rr < IH) {
@@ -291,6 +427,7 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
       if (lds_bf16) *(uint2*)(lds_bf16 + yy * OW + 4 * cq) = u8x4_to_bf16x4(packed);   // (fused conv12)
     }
   }
+#endif
   if (dbg) {
     __syncthreads();
     if (tid == 0) dbg[8] = __builtin_readcyclecounter();

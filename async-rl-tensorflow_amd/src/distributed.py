@@ -214,6 +214,76 @@ class PartitionedPS:
         eng.apply_commit(self.gathered)
 
 
+class LoopbackPS(PartitionedPS):
+    """The partitioned PS of ``world`` virtual ranks inside ONE process on one GPU: every virtual
+    rank holds this engine's (per-worker clipped) gradient, so the all-to-all and all-gather become
+    device-to-device copies on the exchange's own streams, with no host staging and no process
+    group.  It drives the exchange code path of a real multi-GPU run -- the two-phase form with
+    phase A on the comm stream behind ``wait_grad_head`` (under the conv backward), phase B on the
+    caller's stream, the join and the commit; the one-phase form after the whole backward -- on a
+    one-GPU box, where RCCL refuses two ranks.  The update it applies is the reference PS rule for
+    W workers that pushed the same gradient: W rank-ordered RMSProp steps of every range
+    (main.py:63-65).  Test and rehearsal infrastructure: the engine must be created with
+    ``world_size=world`` (per-worker clip, split backward, global-step accounting)."""
+
+    def __init__(self, total, world, device='cuda', split=True):
+        self.group = None
+        self.split = split
+        self.world, self.rank = int(world), 0
+        self.total = int(total)
+        self.shard, self.lo, self.n = shard_ranges(self.total, self.world)
+        self.recv = torch.zeros(max(1, self.world * max(self.n)), dtype=torch.float32, device=device)
+        self.recv_a = torch.zeros_like(self.recv)      # phase A's staging (the comm stream's own)
+        self.w_out = torch.zeros(self.shard, dtype=torch.float32, device=device)
+        self.gathered = torch.zeros(self.world * self.shard, dtype=torch.float32, device=device)
+
+    def _steps(self, eng, g, a, b, recv, out):
+        """the W rank-ordered steps of [a, b): every virtual rank's gradient is g[a:b]"""
+        n = b - a
+        if n <= 0:
+            return
+        for q in range(self.world):
+            recv[q * n:(q + 1) * n].copy_(g[a:b])
+        eng.apply_shard(recv, self.world, a, n, out)
+
+    def apply(self, eng):
+        cut = eng.split_point
+        g = eng.grads
+        if cut and self.split:
+            return self._apply_split_loopback(eng, cut)
+        for q in range(self.world):               # one phase: every range after the whole backward
+            a = self.lo[q]
+            self._steps(eng, g, a, a + self.n[q], self.recv, self.w_out)
+            self.gathered[q * self.shard:q * self.shard + self.n[q]].copy_(self.w_out[:self.n[q]])
+        eng.apply_commit(self.gathered)
+
+    def _apply_split_loopback(self, eng, cut):
+        """PartitionedPS._apply_split with the collectives as copies: phase A (the fc / head part
+        of every range) on the comm stream after ``wait_grad_head``, phase B (the conv prefix) on
+        the caller's stream after the whole backward, then the join and the commit."""
+        self._split_plan(cut)
+        g = eng.grads
+        # (the event it waits for is recorded on the caller's stream behind the previous commit,
+        # so the comm stream's buffers are free again when it fires)
+        with torch.cuda.stream(self.comm):
+            eng.wait_grad_head()
+            for q in range(self.world):
+                a = self.lo[q] + self.conv_n[q]
+                self._steps(eng, g, a, self.lo[q] + self.n[q], self.recv_a, self.w_out[self.conv_n[q]:])
+                self.gathered[q * self.shard + self.conv_n[q]:q * self.shard + self.n[q]].copy_(
+                    self.w_out[self.conv_n[q]:self.n[q]])
+        for q in range(self.world):
+            if self.conv_n[q]:
+                self._steps(eng, g, self.lo[q], self.lo[q] + self.conv_n[q], self.recv, self.w_conv)
+                self.g_conv[q * self.cmax:q * self.cmax + self.conv_n[q]].copy_(self.w_conv[:self.conv_n[q]])
+        torch.cuda.current_stream().wait_stream(self.comm)
+        for q in range(self.world):
+            if self.conv_n[q]:
+                self.gathered[q * self.shard:q * self.shard + self.conv_n[q]].copy_(
+                    self.g_conv[q * self.cmax:q * self.cmax + self.conv_n[q]])
+        eng.apply_commit(self.gathered)
+
+
 class GradExchange:
     """Callable handed to ``Engine.iterate(exchange=...)``: SUM all-reduce of the clipped grads
     (the plain data-parallel rule, NOT the reference PS's: module docstring)."""

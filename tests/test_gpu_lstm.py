@@ -199,3 +199,48 @@ def test_lstm_rejected_where_unsupported():
     desc = _lib.net_desc(6, 'q', lstm=True)
     with pytest.raises(RuntimeError):
         _lib.param_layout(desc)
+
+
+@pytest.mark.parametrize('E,frames', [(16, 48), (256, 512)])
+def test_engine_lstm_overlap_matches_oracle(E, frames):
+    """The pipelined C5 engine (bench.py --lstm: rollout k on the parameters after update k-2) against
+    the oracle replayed in that order with the engine's own actions: per-step outputs, returns,
+    losses, gradients on the engine's own saved activations and LSTM sequence, and parameters.  The
+    fc arrives at the cell as K-slice partials folded by k_lstm_fwd (act_l3 written there)."""
+    from _engine_parity import rollout_planes
+    A, n = 6, 5
+    eng, ref, ns = build(A, E, n, 3, seed=60 + E, frames=frames, scale=2.0, learning_rate=2e-3, overlap=True)
+    hist = []
+    for k in range(4):
+        eng.iterate()
+        torch.cuda.synchronize()
+        sl = eng.slot(k & 1)
+        Pk = {kk: v.copy() for kk, v in ref.params.items()}
+        out = ref.iterate(forced_actions=sl['actions'].cpu().numpy(), grads=False)
+        planes = rollout_planes(ref, n)
+        ref.tau += n
+        assert np.array_equal(sl['rewards'].cpu().numpy(), out['rewards']), k
+        assert np.array_equal(sl['terminals'].cpu().numpy(), out['terminals']), k
+        assert (sl['actions'].cpu().numpy() == out['sampled']).mean() >= 0.98, k
+        z = sl['z'].cpu().numpy()[:n].reshape(n, E, -1)[:, :, :A + 1]
+        np.testing.assert_allclose(z, out['z'][:, :, :A + 1], rtol=1e-4, atol=2e-5)
+        hist.append((Pk, planes, out))
+        if k == 0:
+            continue
+        Pp, planes_p, out_p = hist[k - 1]
+        slp = eng.slot((k - 1) & 1)
+        tgt = slp['returns'].cpu().numpy()
+        np.testing.assert_allclose(tgt, out_p['target'], rtol=1e-4, atol=2e-5)
+        terms = slp['terminals'].cpu().numpy()
+        losses, g_same = same_act_grads(slp, planes_p, Pp, A, n, E, tgt, terms)
+        loss = eng.loss.cpu().numpy()
+        for i, key in enumerate(('policy', 'value', 'entropy', 'total')):
+            assert abs(loss[i] - losses[key]) <= 1e-4 * max(1.0, abs(losses[key])), (k, key, loss[i], losses[key])
+        G = unflat(eng, ns, eng.grads)
+        for name, _ in ns:
+            assert rel_l2(G[name], g_same[name]) < 1e-4, (k, name, rel_l2(G[name], g_same[name]))
+        ref.apply({kk: Rc.clip_by_norm(v, 40.0) for kk, v in g_same.items()}, advance_tau=False, tau=out_p['tau'])
+        P = unflat(eng, ns, eng.params)
+        for name, _ in ns:
+            d = np.abs(P[name] - ref.params[name]).max()
+            assert d <= 1e-5 * max(1.0, np.abs(ref.params[name]).max()), (k, name, d)
