@@ -306,7 +306,7 @@ __device__ inline void vpass_mfma(const uint8_t* __restrict__ tmpT, uint8_t* __r
   for (int q = wid; q < MT_N * MT_N; q += NT / 64) {
     const int nt = q % MT_N, mt = q / MT_N;                 // nt: output rows yy, mt: columns x
     const int x = min(16 * mt + n, OW - 1);
-    const uint32_t v = resample_tile(tmpT + x * TMPT_LD + cTab.vbase[nt], cTab.vb[nt], lane, cTab.vc0[16 * nt + n]);
+    const uint32_t v = resample_tile(tmpT + x * TMPT_LD + cTab.vbase[nt] + 16 * h, cTab.vb[nt], lane, cTab.vc0[16 * nt + n]);
     const int yy = 16 * nt + n, x0 = 16 * mt + 4 * h;
     if (yy < OH && x0 < OW) {
       st_act((uint32_t*)(out + yy * OW + x0), v);

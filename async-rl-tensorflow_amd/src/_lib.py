@@ -153,7 +153,10 @@ MEASUREMENT_ONLY = ('a3c_engine_span_steps', 'a3c_engine_span_raw')
 # entry points an older build selected with A3C_LIB (A/B runs of earlier commits) may lack; any
 # other missing symbol is an error, and each one skipped is named on stderr
 OPTIONAL_IN_OLD_BUILDS = MEASUREMENT_ONLY + ('a3c_engine_exchange_split', 'a3c_engine_wait_grad_head',
-                                             'a3c_dev_alloc_kind', 'a3c_engine_time_kernel')
+                                             'a3c_dev_alloc_kind', 'a3c_engine_time_kernel', 'a3c_engine_set_step',
+                                             'a3c_engine_stats_accumulate', 'a3c_engine_stats_read',
+                                             'a3c_engine_state_bytes', 'a3c_engine_state_save',
+                                             'a3c_engine_state_load')
 
 KER_CONV12_FWD, KER_FC_FWD, KER_ENV_STEP, KER_CONV_BWD, KER_HEAD_SCREEN, KER_HEAD_SCREEN_CONV12, KER_FC_PART = 0, 1, 2, 3, 4, 5, 6
 
