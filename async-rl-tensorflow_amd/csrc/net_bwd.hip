@@ -1257,7 +1257,7 @@ void a3c_set_shared_gpu(bool v) { t_shared_gpu = v; }
 // behind the conv backward (as in sync mode); A3C_CB_LEAN, A3C_GEMM_MULTI, A3C_GEMM_XCD and
 // A3C_DWFC_LATE (0/1) override the choices
 static thread_local bool t_bwd_bound = false;
-static int env_knob(const char* name) { return getenv(name) ? atoi(getenv(name)) : -1; }
+static int env_knob(const char* name) { return (int)A3C_AB_KNOB(name, -1); }   // (A/B builds only)
 bool a3c_lean_cbwd() {   // (every overlap mode since the 256-workgroup plan: M1 4.63M -> 4.66M)
   static const int env = env_knob("A3C_CB_LEAN");
   return env >= 0 ? env != 0 : true;

@@ -265,49 +265,76 @@ constexpr MfmaTab kTab{};
 static_assert(kTab.ok, "resampling tap windows / digits");
 __constant__ MfmaTab cTab = kTab;
 
-// one 16x16 output tile of a pass: A = 16 bytes of the lane's source row at `a_src` (LDS),
-// B = the tile's digit fragments, c0 = the lane's output correction; returns the 4 output bytes
-__device__ inline uint32_t resample_tile(const uint8_t* a_src, const int8_t (&b)[3][64][16], int lane, int c0) {
+// A wave's B fragments of one pass (its n-tile's three digit planes) and the lane's output
+// correction: loaded once per pass, issued right behind the frame loads (so the luminance pass's
+// waits for the frame cover them too) -- per-tile loads of the constant tables each exposed an L2
+// round trip (a first build: the fused kernel 25.9 vs 24.9 us alone).
+struct TapFrag {
+  i32x4 b2, b1, b0;
+  int base, c0;
+};
+__device__ inline TapFrag load_frag(const int8_t (&b)[MT_N][3][64][16], const int (&base)[MT_N], const int (&c0)[MT_N * 16],
+                                    int nt, int lane) {
+  TapFrag f;
+  f.b2 = *(const i32x4*)b[nt][0][lane];
+  f.b1 = *(const i32x4*)b[nt][1][lane];
+  f.b0 = *(const i32x4*)b[nt][2][lane];
+  f.base = base[nt];
+  f.c0 = c0[16 * nt + (lane & 15)];
+  return f;
+}
+// wave -> (n-tile, m-tiles [m0, m1)) of a pass with `mt` m-tiles: waves 0-3 own n-tiles 0-3 whole,
+// n-tiles 4 and 5 are split between waves 4/6 and 5/7 -- each SIMD (waves s, s + 4) gets 1.5
+// n-tiles' work; waves 8+ (1024-thread kernels) take none
+struct PassPlan {
+  int nt, m0, m1;
+};
+__device__ inline PassPlan pass_plan(int wid, int mt) {
+  if (wid < 4) return {wid, 0, mt};
+  if (wid >= 8) return {0, 0, 0};
+  const int half = (mt + 1) / 2;
+  return {4 + (wid & 1), wid < 6 ? 0 : half, wid < 6 ? half : mt};
+}
+
+// one 16x16 output tile of a pass: A = 16 bytes of the lane's source row at `a_src` (LDS);
+// returns the lane's 4 output bytes
+__device__ inline uint32_t resample_tile(const uint8_t* a_src, const TapFrag& f) {
   i32x4 a = *(const i32x4*)a_src;
   a ^= (i32x4){(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
-  const i32x4 b2 = *(const i32x4*)b[0][lane], b1 = *(const i32x4*)b[1][lane], b0 = *(const i32x4*)b[2][lane];
   i32x4 acc = {32, 32, 32, 32};                                     // 2^21 >> 16
-  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b2, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, f.b2, acc, 0, 0, 0);
   acc = acc << 8;
-  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1, acc, 0, 0, 0);
-  acc = (acc << 8) + c0;
-  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, f.b1, acc, 0, 0, 0);
+  acc = (acc << 8) + f.c0;
+  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, f.b0, acc, 0, 0, 0);
   uint32_t packed = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) packed |= (((uint32_t)acc[i] >> 22) & 255u) << (8 * i);
   return packed ^ 0x80808080u;
 }
 
-// horizontal pass: gray [210][160] -> tmpT [84][TMPT_LD] (transposed), 84 tiles over the waves
-template <int NT>
-__device__ inline void hpass_mfma(const uint8_t* __restrict__ gray, uint8_t* __restrict__ tmpT) {
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int n = lane & 15, h = lane >> 4;
-  for (int q = wid; q < H_MT * MT_N; q += NT / 64) {
-    const int nt = q % MT_N, mt = q / MT_N;
+// horizontal pass: gray [210][160] -> tmpT [84][TMPT_LD] (transposed)
+__device__ inline void hpass_mfma(const uint8_t* __restrict__ gray, uint8_t* __restrict__ tmpT, const TapFrag& f,
+                                  const PassPlan& p) {
+  const int lane = threadIdx.x & 63, n = lane & 15, h = lane >> 4;
+  const int X = 16 * p.nt + n;
+  for (int mt = p.m0; mt < p.m1; ++mt) {
     const int y = min(16 * mt + n, IH - 1);
-    const uint32_t v = resample_tile(gray + y * IW + cTab.hbase[nt] + 16 * h, cTab.hb[nt], lane, cTab.hc0[16 * nt + n]);
-    const int X = 16 * nt + n;
+    const uint32_t v = resample_tile(gray + y * IW + f.base + 16 * h, f);
     if (X < OW) *(uint32_t*)(tmpT + X * TMPT_LD + 16 * mt + 4 * h) = v;
   }
 }
 
 // vertical pass: tmpT -> the 84x84 screen (out, HBM ring slot) and, for the fused conv, the
 // same plane as bf16 in LDS
-template <int NT>
-__device__ inline void vpass_mfma(const uint8_t* __restrict__ tmpT, uint8_t* __restrict__ out, uint16_t* lds_bf16) {
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int n = lane & 15, h = lane >> 4;
-  for (int q = wid; q < MT_N * MT_N; q += NT / 64) {
-    const int nt = q % MT_N, mt = q / MT_N;                 // nt: output rows yy, mt: columns x
+__device__ inline void vpass_mfma(const uint8_t* __restrict__ tmpT, uint8_t* __restrict__ out, uint16_t* lds_bf16,
+                                  const TapFrag& f, const PassPlan& p) {
+  const int lane = threadIdx.x & 63, n = lane & 15, h = lane >> 4;
+  const int yy = 16 * p.nt + n;                            // n-tile: output rows, m-tile: columns
+  for (int mt = p.m0; mt < p.m1; ++mt) {
     const int x = min(16 * mt + n, OW - 1);
-    const uint32_t v = resample_tile(tmpT + x * TMPT_LD + cTab.vbase[nt] + 16 * h, cTab.vb[nt], lane, cTab.vc0[16 * nt + n]);
-    const int yy = 16 * nt + n, x0 = 16 * mt + 4 * h;
+    const uint32_t v = resample_tile(tmpT + x * TMPT_LD + f.base + 16 * h, f);
+    const int x0 = 16 * mt + 4 * h;
     if (yy < OH && x0 < OW) {
       st_act((uint32_t*)(out + yy * OW + x0), v);
       if (lds_bf16) *(uint2*)(lds_bf16 + yy * OW + x0) = u8x4_to_bf16x4(v);   // (fused conv12)
@@ -374,6 +401,11 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
 #pragma unroll
   for (int j = 0; j < PKV; ++j)
     if (tid + NT * j < NKV) kvs[tid + NT * j] = kv[j];
+#else
+  // the wave's tap fragments of both passes, behind the frame loads (retire with them)
+  const PassPlan hp = pass_plan(wid, H_MT), vp = pass_plan(wid, MT_N);
+  const TapFrag hf = load_frag(cTab.hb, cTab.hbase, cTab.hc0, hp.nt, lane);
+  const TapFrag vf = load_frag(cTab.vb, cTab.vbase, cTab.vc0, vp.nt, lane);
 #endif
   if (dbg && tid == 0) dbg[4] = __builtin_readcyclecounter() + (r[0].x & 0);   // first unit landed
 #pragma unroll
@@ -385,10 +417,10 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
   __syncthreads();
   if (dbg && tid == 0) dbg[6] = __builtin_readcyclecounter();
 #ifndef SCREEN_VALU
-  hpass_mfma<NT>(gray, tmp);                           // tmp = tmpT [84][224]
+  hpass_mfma(gray, tmp, hf, hp);                       // tmp = tmpT [84][224]
   __syncthreads();
   if (dbg && tid == 0) dbg[7] = __builtin_readcyclecounter();
-  vpass_mfma<NT>(tmp, out, lds_bf16);
+  vpass_mfma(tmp, out, lds_bf16, vf, vp);
 #else
   for (int task = wid; task < 16; task += NWV) {
     const int seg = task & 3, rr = (task >> 2) * 64 + lane;
