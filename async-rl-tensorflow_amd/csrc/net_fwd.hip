@@ -754,17 +754,20 @@ __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restr
 // (as k_head_screen), then conv1 + conv2 of env b's next state s_{t+1} in the same workgroup --
 // the next state is the 3 newest ring planes (prefetched into registers at kernel start, they
 // are final) plus the screen just computed (kept in LDS).  One kernel boundary and the conv
-// staging latency fewer per rollout step.  LDS: screen scratch (54 KB, later overlaid by l1) |
-// x8 (28 KB).
-// The screen's vertical-tap table goes to the x8 region behind the new plane's bf16 copy (free
-// during the screen), which keeps the kernel under 80 KB: a CU holds one of it beside one
-// compact conv backward workgroup (CB_SMEM_SOLO).
+// staging latency fewer per rollout step.  LDS: screen scratch (gray | tmpT, 51 KB, later
+// overlaid by l1) | x8 (18 KB: the older planes' conv1 weight fragments, then the new plane as
+// bf16 (14 KB) -- and in -DSCREEN_VALU builds the vertical-tap table behind it).
+// A CU must hold one of it beside one compact conv backward workgroup (CB_SMEM_SOLO, 81 KB): the
+// round-5 MFMA screen's first layout (78.8 KB, a 28 KB x8 region sized for u8 planes it no longer
+// holds) left them no co-residency -- the conv backward then ran alone (90 us live) after the
+// rollout, 4.10M vs 4.87M env-steps/s.  Hence the margin in the assert below.
 #define HSC_X8_OFF (((SCREEN_FRAME_SMEM_NOKV) + 15) / 16 * 16)
-#define HSC_SMEM (HSC_X8_OFF + HIST * PLANE)
+#define HSC_X8_BYTES ((HIST - 1) * 2 * 3 * 64 * 16)              // 18432: the weight fragments
+#define HSC_SMEM (HSC_X8_OFF + HSC_X8_BYTES)
 #define HSC_KV_OFF (PLANE * 2)
 static_assert(L1S_BYTES <= SCREEN_FRAME_SMEM_NOKV, "l1 overlays the screen scratch");
-static_assert(HSC_KV_OFF % 16 == 0 && HSC_KV_OFF + SCREEN_KV_BYTES <= HIST * PLANE, "tap table in the x8 region");
-static_assert(HSC_SMEM + 16 <= 160 * 1024 - 82944, "rollout workgroup beside a compact conv backward one");
+static_assert(HSC_KV_OFF % 16 == 0 && HSC_KV_OFF + SCREEN_KV_BYTES <= HSC_X8_BYTES, "tap table in the x8 region");
+static_assert(HSC_SMEM + 16 + 4096 <= 160 * 1024 - 82944, "rollout workgroup beside a compact conv backward one");
 // waves_per_eu(4) caps it at 128 VGPRs: with the concurrent k_conv_bwd<false,4> (254 VGPRs,
 // one wave per SIMD) two of its waves per SIMD must fit in the remaining 258
 template <bool SAVE_L1, bool L2M>
@@ -801,9 +804,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   constexpr int PER3 = (NCH3 + PT - 1) / PT;             // 4
   constexpr int NWF = (HIST - 1) * 2 * 3 * 64;           // 1152 16-byte fragment rows
   constexpr int PERW = NWF / PT;                         // 3
-  static_assert(NWF % PT == 0 && NWF * 16 <= HIST * PLANE, "old-plane conv1 weights in the x8 region");
+  static_assert(NWF % PT == 0 && NWF * 16 <= HSC_X8_BYTES, "old-plane conv1 weights in the x8 region");
   static_assert((HIST - 1) * PLANE * 2 <= 51 * 1024, "old planes as bf16 in the screen scratch");
-  static_assert(PLANE * 2 <= HIST * PLANE, "new plane as bf16 in the x8 region");
+  static_assert(PLANE * 2 <= HSC_X8_BYTES, "new plane as bf16 in the x8 region");
   // fc as K-slice partials (sel.fc_part), folded by wave 0 ahead of the head
   const int fwid = threadIdx.x >> 6, flane = threadIdx.x & 63;
   const bool fold = sel.fc_part != nullptr;

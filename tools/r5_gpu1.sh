@@ -10,7 +10,7 @@ timeout -k 10 900 python3 -u -m pytest tests/test_gpu_engine.py tests/test_gpu_k
   -k "matches_oracle or double_q or screen or preprocess or bench_shape" > $O/pytest1.log 2>&1
 rc=$?; tail -3 $O/pytest1.log; [ $rc -ne 0 ] && { grep -E "Error|assert|FAILED" $O/pytest1.log | head -30; exit $rc; }
 for rep in 1 2 3; do
-  for L in "" "async-rl-tensorflow_amd/lib/var/svalu/liba3c_hip.so"; do
+  for L in "" "async-rl-tensorflow_amd/lib/var/svalu/liba3c_hip.so" "async-rl-tensorflow_amd/lib/var/r5a/liba3c_hip.so"; do
     A3C_LIB=$L timeout -k 10 200 python3 bench.py --no-cpu-baseline --steps 200 > $O/ab.json 2>$O/ab.err || exit 1
     python3 -c "
 import json;d=json.load(open('$O/ab.json'));r=d['roofline']
