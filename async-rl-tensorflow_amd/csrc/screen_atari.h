@@ -313,15 +313,51 @@ __device__ inline uint32_t resample_tile(const uint8_t* a_src, const TapFrag& f)
   return packed ^ 0x80808080u;
 }
 
-// horizontal pass: gray [210][160] -> tmpT [84][TMPT_LD] (transposed)
+// two independent tiles interleaved: each tile's three MFMAs form a dependent chain (Horner), so
+// one chain alone waits out every MFMA's latency; two chains fill each other's gaps
+__device__ inline void resample_tile2(const uint8_t* s0, const uint8_t* s1, const TapFrag& f, uint32_t& v0, uint32_t& v1) {
+  const i32x4 flip = {(int)0x80808080, (int)0x80808080, (int)0x80808080, (int)0x80808080};
+  const i32x4 a0 = *(const i32x4*)s0 ^ flip, a1 = *(const i32x4*)s1 ^ flip;
+  i32x4 c0 = {32, 32, 32, 32}, c1 = {32, 32, 32, 32};
+  c0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, f.b2, c0, 0, 0, 0);
+  c1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, f.b2, c1, 0, 0, 0);
+  c0 = c0 << 8;
+  c1 = c1 << 8;
+  c0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, f.b1, c0, 0, 0, 0);
+  c1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, f.b1, c1, 0, 0, 0);
+  c0 = (c0 << 8) + f.c0;
+  c1 = (c1 << 8) + f.c0;
+  c0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, f.b0, c0, 0, 0, 0);
+  c1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, f.b0, c1, 0, 0, 0);
+  uint32_t p0 = 0, p1 = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    p0 |= (((uint32_t)c0[i] >> 22) & 255u) << (8 * i);
+    p1 |= (((uint32_t)c1[i] >> 22) & 255u) << (8 * i);
+  }
+  v0 = p0 ^ 0x80808080u;
+  v1 = p1 ^ 0x80808080u;
+}
+
+// horizontal pass: gray [210][160] -> tmpT [84][TMPT_LD] (transposed), tiles in pairs
 __device__ inline void hpass_mfma(const uint8_t* __restrict__ gray, uint8_t* __restrict__ tmpT, const TapFrag& f,
                                   const PassPlan& p) {
   const int lane = threadIdx.x & 63, n = lane & 15, h = lane >> 4;
   const int X = 16 * p.nt + n;
-  for (int mt = p.m0; mt < p.m1; ++mt) {
-    const int y = min(16 * mt + n, IH - 1);
-    const uint32_t v = resample_tile(gray + y * IW + f.base + 16 * h, f);
-    if (X < OW) *(uint32_t*)(tmpT + X * TMPT_LD + 16 * mt + 4 * h) = v;
+  uint8_t* t = tmpT + X * TMPT_LD + 4 * h;
+  const uint8_t* g = gray + f.base + 16 * h;
+  int mt = p.m0;
+  for (; mt + 1 < p.m1; mt += 2) {
+    uint32_t v0, v1;
+    resample_tile2(g + min(16 * mt + n, IH - 1) * IW, g + min(16 * mt + 16 + n, IH - 1) * IW, f, v0, v1);
+    if (X < OW) {
+      *(uint32_t*)(t + 16 * mt) = v0;
+      *(uint32_t*)(t + 16 * mt + 16) = v1;
+    }
+  }
+  if (mt < p.m1) {
+    const uint32_t v = resample_tile(g + min(16 * mt + n, IH - 1) * IW, f);
+    if (X < OW) *(uint32_t*)(t + 16 * mt) = v;
   }
 }
 
@@ -331,15 +367,22 @@ __device__ inline void vpass_mfma(const uint8_t* __restrict__ tmpT, uint8_t* __r
                                   const TapFrag& f, const PassPlan& p) {
   const int lane = threadIdx.x & 63, n = lane & 15, h = lane >> 4;
   const int yy = 16 * p.nt + n;                            // n-tile: output rows, m-tile: columns
-  for (int mt = p.m0; mt < p.m1; ++mt) {
-    const int x = min(16 * mt + n, OW - 1);
-    const uint32_t v = resample_tile(tmpT + x * TMPT_LD + f.base + 16 * h, f);
+  const uint8_t* t = tmpT + f.base + 16 * h;
+  auto put = [&](int mt, uint32_t v) {
     const int x0 = 16 * mt + 4 * h;
     if (yy < OH && x0 < OW) {
       st_act((uint32_t*)(out + yy * OW + x0), v);
       if (lds_bf16) *(uint2*)(lds_bf16 + yy * OW + x0) = u8x4_to_bf16x4(v);   // (fused conv12)
     }
+  };
+  int mt = p.m0;
+  for (; mt + 1 < p.m1; mt += 2) {
+    uint32_t v0, v1;
+    resample_tile2(t + min(16 * mt + n, OW - 1) * TMPT_LD, t + min(16 * mt + 16 + n, OW - 1) * TMPT_LD, f, v0, v1);
+    put(mt, v0);
+    put(mt + 1, v1);
   }
+  if (mt < p.m1) put(mt, resample_tile(t + min(16 * mt + n, OW - 1) * TMPT_LD, f));
 }
 
 // Whole-frame Environment.screen by one workgroup of NT threads (gray 210x160 and the
