@@ -3,6 +3,7 @@
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$ROOT"
 O=gpurun_out/r5g3; mkdir -p $O
+A3C_LIB=async-rl-tensorflow_amd/lib/var/cbp/liba3c_hip.so timeout -k 10 200 python3 tools/cb_phases.py 2>&1 | grep -v amdgpu.ids || exit 1
 K=async-rl-tensorflow_amd/lib/var/knobs/liba3c_hip.so
 for rep in 1 2 3; do
   for cfg in "X=0" "A3C_WKS_XCD=1" "A3C_GEMM_XCD=1" "A3C_L2BITS=1" "A3C_WKS_XCD=1 A3C_GEMM_XCD=1 A3C_L2BITS=1"; do
