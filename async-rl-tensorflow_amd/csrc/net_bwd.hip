@@ -1098,10 +1098,12 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
   gf.epi = EPI_STORE; gf.slab = ws + p.fcslab; gf.nsplit = p.fc_split; gf.colsum = ws + p.fccol;
   gf.wg_split = wks ? 4 : 0;
   gf.xcd = xcd_gemm() ? 1 : 0;          // the 4 column tiles of an l2 strip on one XCD
-  // A3C_WKS_XCD=1: the in-workgroup split-K form in XCD-grouped order (its 4 N tiles share the
-  // 64-row strip of l2): M1 4.84M vs 4.85M with the plain grid (3 interleaved reps), so off
+  // The in-workgroup split-K form in XCD-grouped order (its 4 N tiles share the 64-row strip of l2,
+  // fetched once per XCD instead of once per N tile): HBM bytes per launch 58.5 -> 26.6 MB (PMC,
+  // profiles/round5_ab/gemm_knobs.txt; the 8-XCD floor is 26.5: l2 13.3 + dl3 1.3 per XCD + dW
+  // 2.65), M1 unchanged (4.884M vs 4.886M, 3 interleaved reps).  A3C_WKS_XCD=0 (A/B builds): plain grid
   if (wks) {
-    static const int env_wx = (int)A3C_AB_KNOB("A3C_WKS_XCD", 0);
+    static const int env_wx = (int)A3C_AB_KNOB("A3C_WKS_XCD", 1);
     gf.xcd = env_wx ? 1 : 0;
   }
   // dl2[B][2592] = (dl3 W^T) * (l2 > 0)
