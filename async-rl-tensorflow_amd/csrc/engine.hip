@@ -41,6 +41,7 @@ struct Slot {
   float *act_l1, *act_l2, *act_l3;
   uint32_t* l2m;           // act_l2's ReLU mask as bits [n*E][81], written by the forward's conv2
   float *scr_l2, *scr_l3;  // bootstrap / target forward scratch
+  float* fcboot;           // boot_bwd: the bootstrap state's fc partials, read by the slot's backward
   uint8_t* prep;           // forward weights of P prepared for the kernels (k_prep_fwd)
   // C5 LSTM head: per step h_t, c_t, masked inputs hp, cp [n][E][U], gates [n][E][4U];
   // bootstrap-step h, c [E][U]
@@ -288,6 +289,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     ALLOC(sl.scr_l2, scrB * FLAT * 4);
     ALLOC(sl.scr_l3, scrB * FC * 4);
     ALLOC(sl.prep, PREP_BYTES);
+    if (e->overlap) ALLOC(sl.fcboot, (int64_t)FC_NS * E * FC * 4);
     if (L.lstm) {
       ALLOC(sl.lh, nE * LSTM_U * 4);
       ALLOC(sl.lc, nE * LSTM_U * 4);
@@ -496,6 +498,14 @@ static bool conv_fused(const a3c_engine* e) { return e->fuse_conv && !e->ext && 
 // the fused rollout's fc as K-slice partials folded by the head (feed-forward head only)
 // (the LSTM head: the cell kernel folds them, k_lstm_fwd)
 static bool fc_split(const a3c_engine* e) { return conv_fused(e) && e->fc_split; }
+// Overlap, A3C feed-forward head: the bootstrap state's head (the fold of its fc partials, V(s_n))
+// runs as the first kernel of the slot's backward on the caller's stream instead of as the
+// rollout's last kernel; the rollout ends with the fc of s_n (into the slot's own partial buffer,
+// which the next rollout does not touch), which also advances tau.
+static bool boot_bwd(const a3c_engine* e) {
+  static const int env = (int)A3C_AB_KNOB("A3C_BOOT_BWD", 0);
+  return env != 0 && e->overlap && fc_split(e) && !e->L.lstm && e->L.algo == A3C_ALGO_A3C;
+}
 
 __global__ void k_advance_tau(int64_t* counters, int n) { counters[0] += n; }
 
@@ -658,6 +668,8 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
 static int enqueue_rollout_end(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const NetLayout& L = e->L;
   const int E = e->E, n = e->n;
+  if (boot_bwd(e))      // the fc of s_n (conv ran in the last step's kernel) + the tau advance
+    return a3c_fc_part_launch(sl.scr_l2, (const float*)(sl.prep + PREP_W1S_BYTES), sl.fcboot, E, s, e->counters, n);
   if (L.algo != A3C_ALGO_Q) {
     const int64_t lastE = (int64_t)(n - 1) * E;
     HeadSelect none = {};
@@ -902,6 +914,10 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
                             sl.scr_l3, e->zt, none, s);
     if (rc) return rc;
     rc = a3c_td_target_launch(sl.rewards, sl.terms, e->zt, e->nE, L.A, zs, c.discount, sl.R_buf, s, qsel);
+    if (rc) return rc;
+  }
+  if (boot_bwd(e)) {   // V(s_n) of the slot (its fc partials: the rollout's last kernel)
+    rc = a3c_head_fold_launch(L, sl.P, sl.fcboot, E, sl.z + e->nE * zs, s);
     if (rc) return rc;
   }
   ReturnsArgs ra = {};
@@ -1404,6 +1420,7 @@ static std::vector<StateRegion> state_regions(const a3c_engine* e) {
       add(sl.z, (nE + E) * zs * 4); add(sl.R_buf, nE * 4);
       add(sl.act_l1, nE * C1_P * C1_N * 4); add(sl.act_l2, nE * FLAT * 4); add(sl.act_l3, nE * FC * 4);
       add(sl.l2m, nE * C2_Q * 4);     // (the pending backward's dl2 mask)
+      add(sl.fcboot, (int64_t)FC_NS * E * FC * 4);   // (boot_bwd: the pending backward's V(s_n) partials)
     }
     if (e->L.lstm) {
       add(sl.lh, nE * LSTM_U * 4); add(sl.lc, nE * LSTM_U * 4);

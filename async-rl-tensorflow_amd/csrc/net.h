@@ -161,7 +161,14 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
                        hipStream_t s, const LstmStep* ls = nullptr, bool skip_conv12 = false,
                        const Conv12Next* next = nullptr, float* fc_part = nullptr, uint32_t* l2m = nullptr);
 // fc layer as FC_NS K-slice partials part[x][M][FC] (folded by k_head_screen_conv12's head)
-int a3c_fc_part_launch(const float* A, const float* Wp, float* part, int64_t M, hipStream_t s);
+// adv_ptr: the launch also advances the device tau counter by adv_n (thread 0 of block 0; the fc
+// reads no tau) -- the rollout's last kernel when the bootstrap head runs on the backward stream
+int a3c_fc_part_launch(const float* A, const float* Wp, float* part, int64_t M, hipStream_t s,
+                       int64_t* adv_ptr = nullptr, int adv_n = 0);
+// the policy / value head of B states from the fc's K-slice partials (fold + bias + ReLU + head,
+// k_head_fwd): z rows, no action draw
+int a3c_head_fold_launch(const NetLayout& L, const float* P, const float* fc_part, int64_t B, float* z,
+                         hipStream_t s);
 int a3c_fcp_split();
 void a3c_set_fcp_split(int ks);
 // tau_src / tau_dst (nullable): *tau_dst = *tau_src as well (the overlap rollout's tau snapshot);

@@ -1244,8 +1244,10 @@ __device__ inline int fcp_c0(int x) { return (FC_CH * x) / FC_NS; }
 // workgroup either way.  Measured (M1 / M2 env-steps/s): KS 1 4.67M / 5.82M, KS 2 4.78M / 6.07M.
 template <int KS>
 __global__ void __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(KS == 4 ? 8 : 1)))
-k_fc_part(const float* __restrict__ A, const float* __restrict__ Wp, float* __restrict__ part, int M) {
+k_fc_part(const float* __restrict__ A, const float* __restrict__ Wp, float* __restrict__ part, int M,
+          int64_t* adv_ptr, int adv_n) {
   WGLOG(2);
+  if (adv_ptr && blockIdx.x == 0 && threadIdx.x == 0) *adv_ptr += adv_n;   // (reads no tau)
   __shared__ __attribute__((aligned(16))) float as[FCP_RB * FCP_LD];
   constexpr int NT = 256 * KS;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1342,15 +1344,32 @@ static thread_local int t_fcp_split = 2;
 int a3c_fcp_split() { return t_fcp_split; }
 void a3c_set_fcp_split(int ks) { t_fcp_split = ks; }
 
-int a3c_fc_part_launch(const float* A, const float* Wp, float* part, int64_t M, hipStream_t s) {
+int a3c_fc_part_launch(const float* A, const float* Wp, float* part, int64_t M, hipStream_t s, int64_t* adv_ptr,
+                       int adv_n) {
   if (M <= 0) return 0;
   const int nrb = (int)((M + FCP_RB - 1) / FCP_RB);
   static const int env_ks = (int)A3C_AB_KNOB("A3C_FCP_KS", 0);
   const int ks = env_ks ? env_ks : a3c_fcp_split();
   const dim3 grid((unsigned)(FC_NS * nrb * (FC / FCP_CB)));
-  if (ks == 4) hipLaunchKernelGGL(k_fc_part<4>, grid, dim3(1024), 0, s, A, Wp, part, (int)M);
-  else if (ks == 2) hipLaunchKernelGGL(k_fc_part<2>, grid, dim3(512), 0, s, A, Wp, part, (int)M);
-  else hipLaunchKernelGGL(k_fc_part<1>, grid, dim3(256), 0, s, A, Wp, part, (int)M);
+  if (ks == 4) hipLaunchKernelGGL(k_fc_part<4>, grid, dim3(1024), 0, s, A, Wp, part, (int)M, adv_ptr, adv_n);
+  else if (ks == 2) hipLaunchKernelGGL(k_fc_part<2>, grid, dim3(512), 0, s, A, Wp, part, (int)M, adv_ptr, adv_n);
+  else hipLaunchKernelGGL(k_fc_part<1>, grid, dim3(256), 0, s, A, Wp, part, (int)M, adv_ptr, adv_n);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+int a3c_head_fold_launch(const NetLayout& L, const float* P, const float* fc_part, int64_t B, float* z,
+                         hipStream_t s) {
+  if (B <= 0) return 0;
+  HeadSelect hs = {};
+  hs.mode = -1;
+  hs.E = (int)B;
+  hs.fc_part = fc_part;
+  hs.fc_bias = P + L.off[T_FCB];
+  const float* Wv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VW] : nullptr;
+  const float* bv = L.algo == A3C_ALGO_A3C ? P + L.off[T_VB] : nullptr;
+  hipLaunchKernelGGL(k_head_fwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, nullptr, B, P + L.off[T_HW],
+                     P + L.off[T_HB], Wv, bv, L.A, L.zs, z, hs);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
