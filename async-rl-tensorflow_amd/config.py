@@ -75,9 +75,12 @@ def get_config(FLAGS):
   """config.py:52-66: the model's config class with every matching flag written onto it.
   ``gpu`` picks the conv layout.  (An unknown model is an UnboundLocalError in the
   reference; here a ValueError.)"""
-  config = _MODELS.get(FLAGS.model)
-  if config is None:
+  base = _MODELS.get(FLAGS.model)
+  if base is None:
     raise ValueError('unknown model: %s' % FLAGS.model)
+  # the flags go onto a per-call subclass: the reference writes them onto the model class itself,
+  # which in one process (several main() calls, the tests) would carry one run's flags into the next
+  config = type(base.__name__, (base,), {})
   for name, value in _flag_items(FLAGS):
     if name == 'gpu':
       config.cnn_format = 'NCHW' if value else 'NHWC'

@@ -75,7 +75,6 @@ struct a3c_engine {
   float* sumsq;
   float* zt;               // q: target-net q values [nE][zs]
   uint8_t* prep_t;         // q: prepared forward weights of the target network
-  float* eps;              // q: per env epsilon
   float* ep_end;           // q: per env final epsilon
   float* ws;               // backward workspace
   float* fcpart;           // fused overlap rollout: the fc as FC_NS K-slice partials [FC_NS][E][FC]
@@ -308,7 +307,6 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   ALLOC(e->prep_t, PREP_BYTES);
   ALLOC(e->spans, 2 * (size_t)SPAN_RECS * SPAN_WGS * 2 * sizeof(unsigned long long));
   ALLOC(e->zt, scrB * zs * 4);
-  ALLOC(e->eps, E * 4);
   ALLOC(e->ep_end, E * 4);
   BwdPlan bp = a3c_bwd_plan(L, nE);
   ALLOC(e->ws, bp.total * 4);
@@ -461,18 +459,14 @@ __global__ void __launch_bounds__(256) k_stats(const float* __restrict__ rraw, c
   }
 }
 
-__global__ void k_eps(float* __restrict__ eps, const float* __restrict__ ep_end, int E,
-                      const int64_t* __restrict__ counters, int t, float ep_start, int64_t ep_end_t,
-                      int64_t learn_start) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= E) return;
-  // agent.py:142-144 at the worker's own step (agent.py:55 loop counter): the workers' base step
-  // plus the env steps taken so far (tau - (HIST-1)) plus rollout step t
-  const double step = (double)(counters[2] + counters[0] - (HIST - 1) + t);
-  const double ee = ep_end[i];
-  double d = (double)ep_end_t - fmax(0.0, step - (double)learn_start);
-  double v = ee + fmax(0.0, ((double)ep_start - ee) * d / (double)ep_end_t);
-  eps[i] = (float)v;
+// the epsilon schedule of agent.py:142-144 at the worker's own step, evaluated by the head kernel
+// (sel_eps in net_fwd.hip): the workers' base step counters[2] plus the env steps taken so far
+// (tau - (HIST-1)).  A separate per-step schedule kernel cost Q sync 3% (round-5 bisect).
+static void set_eps_schedule(const a3c_engine* e, HeadSelect& sel) {
+  sel.ep_end = e->ep_end;
+  sel.ep_start = e->cfg.ep_start;
+  sel.ep_end_t = e->cfg.ep_end_t;
+  sel.learn_start = e->cfg.learn_start;
 }
 
 static StateAddr ring_addr(const a3c_engine* e, int tau_offset, const int64_t* tau_ptr) {
@@ -600,13 +594,8 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
   sel.k0 = e->k0; sel.k1 = e->k1;
   sel.tau_ptr = e->counters; sel.tau_add = t;
   sel.env_ids = nullptr; sel.env_id_base = c.env_id_base; sel.E = E;
-  sel.eps = e->eps;
+  if (q) set_eps_schedule(e, sel);   // epsilon of this step, in the head (q engines are synchronous)
   const int64_t o = (int64_t)t * E;
-  if (q) {        // epsilon of this step (agent.py:142-144; q engines are synchronous: tau is live)
-    hipLaunchKernelGGL(k_eps, dim3((E + 255) / 256), dim3(256), 0, s, e->eps, e->ep_end, E, e->counters, t,
-                       c.ep_start, c.ep_end_t, c.learn_start);
-    A3C_CHECK(hipGetLastError());
-  }
   sel.actions = sl.actions + o;
   sel.env_on = dev_env ? 1 : 0;
   if (dev_env) {
@@ -1605,7 +1594,7 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
         sel.k0 = e->k0; sel.k1 = e->k1;
         sel.tau_ptr = e->counters; sel.tau_add = 0;
         sel.env_id_base = e->cfg.env_id_base; sel.E = E; sel.par_E = E;
-        sel.eps = e->eps;
+        if (sel.mode) set_eps_schedule(e, sel);
         sel.actions = sl.actions;
         sel.env_on = 1;
         sel.envp = e->envp; sel.envb = e->env;

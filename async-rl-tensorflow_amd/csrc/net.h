@@ -97,6 +97,12 @@ struct HeadSelect {
   int env_id_base;
   int E;
   const float* eps;         // mode 1: per env (index b % E)
+  // mode 1, when set: the head computes the env's epsilon at the worker's own step instead of
+  // reading eps (agent.py:142-144, step = tau_ptr[2] + tau - (HIST-1); one launch fewer per
+  // rollout step than a separate schedule kernel: Q sync 3.447M -> 3.547M env-steps/s)
+  const float* ep_end;      // per env final epsilon (index b % E)
+  float ep_start;
+  int64_t ep_end_t, learn_start;
   int32_t* actions;         // [B]
   // fused env step (engine rollout): act() on the drawn action right after predict, as the
   // reference worker does (agent.py:59-62); env state double-buffered by (tau & 1)

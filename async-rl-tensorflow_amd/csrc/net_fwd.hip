@@ -534,9 +534,22 @@ __device__ inline int32_t select_with(float myz, int lane, int A, int mode, u32x
   }
 }
 
+// the exploration rate of env e at step tau (Q mode): the linear schedule of agent.py:142-144 at
+// the worker's own step (agent.py:55 loop counter) when sel.ep_end is set, else sel.eps[e]
+__device__ inline float sel_eps(const HeadSelect& sel, int e, int64_t tau) {
+  if (sel.mode == 0) return 0.f;
+  if (sel.ep_end) {
+    const double step = (double)(sel.tau_ptr[2] + tau - (HIST - 1));
+    const double ee = sel.ep_end[e];
+    const double d = (double)sel.ep_end_t - fmax(0.0, step - (double)sel.learn_start);
+    return (float)(ee + fmax(0.0, ((double)sel.ep_start - ee) * d / (double)sel.ep_end_t));
+  }
+  return sel.eps ? sel.eps[e] : 0.f;
+}
+
 __device__ inline int32_t select_from_lanes(float myz, int lane, int A, const HeadSelect& sel, int64_t b) {
   const int64_t tau = (sel.tau_ptr ? *sel.tau_ptr : 0) + sel.tau_add;
-  const float eps = sel.mode != 0 && sel.eps ? sel.eps[b % sel.E] : 0.f;
+  const float eps = sel_eps(sel, (int)(b % sel.E), tau);
   return select_with(myz, lane, A, sel.mode, action_draw(sel, b, tau), eps);
 }
 
@@ -669,7 +682,7 @@ __device__ inline int32_t head_act_env(const float* __restrict__ h3, const float
   const int e = (int)b;
   const int64_t nxt = ((tau + 1) & 1) * (int64_t)sel.par_E + e;
   if (wid == 0) {
-    const float eps = sel.mode != 0 && sel.eps ? sel.eps[e] : 0.f;
+    const float eps = sel_eps(sel, e, tau);
     u32x4 x;
     // the action draw does not depend on the head: computed under its load latency
     // (hrow: the layer-output row, already folded into LDS by the caller)

@@ -11,10 +11,14 @@ def test_flags_and_config():
     f = main.parse_flags(['--env_name', 'Pong-v0', '--double_q', 'true', '--mode', 'agent', '--beta', '0.02'])
     assert f.env_name == 'Pong-v0' and f.double_q is True and f.mode == 'agent'
     cfg = C.get_config(f)
-    assert cfg is C.M1 and cfg.env_name == 'Pong-v0' and cfg.double_q is True and cfg.beta == 0.02
+    assert issubclass(cfg, C.M1) and cfg.env_name == 'Pong-v0' and cfg.double_q is True and cfg.beta == 0.02
     assert cfg.learning_rate == 0.0007 and cfg.target_q_update_step == 40000   # config.py defaults
     with pytest.raises(ValueError):
         C.get_config(main.parse_flags(['--model', 'm9']))
+    # one call's flags do not leak into the next (main() runs several times in one test process)
+    C.get_config(main.parse_flags(['--max_step', '14', '--n_step', '7']))
+    fresh = C.get_config(main.parse_flags([]))
+    assert fresh.max_step == C.M1.max_step != 14 and fresh.n_step == C.M1.n_step
 
 
 def test_base_model_attrs_and_model_dir():
