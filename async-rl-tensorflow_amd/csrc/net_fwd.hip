@@ -1360,6 +1360,10 @@ void a3c_set_fcp_split(int ks) { t_fcp_split = ks; }
 int a3c_fc_part_launch(const float* A, const float* Wp, float* part, int64_t M, hipStream_t s, int64_t* adv_ptr,
                        int adv_n) {
   if (M <= 0) return 0;
+#ifdef A3C_MARKERS
+  static const bool ablate = getenv("A3C_ABL_FC") != nullptr;   // measurement only: no fc
+  if (ablate && !adv_ptr) return 0;
+#endif
   const int nrb = (int)((M + FCP_RB - 1) / FCP_RB);
   static const int env_ks = (int)A3C_AB_KNOB("A3C_FCP_KS", 0);
   const int ks = env_ks ? env_ks : a3c_fcp_split();
