@@ -6,6 +6,6 @@ LOG=$1; TO=$2; CMD=$3
 for i in $(seq 1 20); do
   timeout $((TO + 900)) /usr/local/graft/bin/gpurun --timeout "$TO" -- "$CMD" > "$LOG" 2>&1
   rc=$?
-  if grep -q "status=transient rc=None" "$LOG" && [ $rc -ne 0 ]; then sleep 150; continue; fi
+  if grep -q "status=transient rc=None" "$LOG"; then sleep 200; continue; fi
   exit $rc
 done
