@@ -760,6 +760,8 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s);
 // co-bounds it and the single 1,420-workgroup launch costs the rollout more than it saves
 // (net_bwd.hip's knobs).
 static bool bwd_bound(const a3c_engine* e) {
+  static const int env = (int)A3C_AB_KNOB("A3C_BWD_BOUND", -1);   // A/B override
+  if (env >= 0) return e->overlap && env != 0;
   return e->overlap && (e->frame84 || e->cfg.world_size > 1);
 }
 static int enqueue_grad(a3c_engine* e, const Slot& sl, hipStream_t s) {
