@@ -1,3 +1,3 @@
 #!/bin/bash
 # round 5: Q bisect + C5 trace, then the boot-bwd A/B
-bash tools/r5_gpu4.sh && bash tools/r5_gpu5.sh
+bash tools/runs/r5_gpu4.sh && bash tools/runs/r5_gpu5.sh
