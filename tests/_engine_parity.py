@@ -25,7 +25,7 @@ def rel_l2(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
 
 
-REF_KEYS = ('target_q_update_step', 'learning_rate', 'frame84', 'double_q')
+REF_KEYS = ('target_q_update_step', 'learning_rate', 'frame84', 'double_q', 'ep_start', 'ep_end_t', 'learn_start')
 
 
 def build(algo, A, E, n, lives, seed, frames=48, use_graph=False, scale=4.0, **kw):

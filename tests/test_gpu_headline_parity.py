@@ -10,7 +10,9 @@ against oracle/engine_ref.py:
     and the synchronous update (k_head_screen, k_conv12_fwd, k_fc_fwd, k_conv_bwd<true,8>);
   * C3 per-GPU shard: Breakout (A=4, 5 lives), 256 envs;
   * C4 per-GPU shard: Pong, 512 envs, sync, overlap and Hogwild at world 1;
-  * C5 per-GPU shard: SpaceInvaders LSTM head, 256 envs (build-defined head, oracle restated).
+  * C5 per-GPU shard: SpaceInvaders LSTM head, 256 envs (build-defined head, oracle restated);
+  * async one-step Q-learning at bench.py's Q shape (256 envs, train_frequency 32), plain and
+    double-Q, with an epsilon schedule that crosses the greedy / random split inside the run.
 Initial weights are the reference's init (stddev 0.02, agent.py:214 / ops.py:36-37) and the
 optimizer constants the reference's (config.py:11-16, main.py:64-65), so the shapes, weights and
 update rule are the headline's.  Tolerances: see tests/_engine_parity.py."""
@@ -115,3 +117,14 @@ def test_c5_lstm_shard_matches_oracle():
         for name, _ in ns:
             d = np.abs(P[name] - ref.params[name]).max()
             assert d <= 1e-5 * max(1.0, np.abs(ref.params[name]).max()), (it, name, d)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize('double_q', [False, True])
+def test_q_bench_shape_matches_oracle(double_q):
+    """bench.py --algo q --n-step 32 --update sync: 256 envs, 32 steps per update, the target copy
+    every 40 updates' worth of steps.  The epsilon schedule (agent.py:142-144, evaluated per env and
+    step inside the head kernel) starts at 0.5 and decays over 2,000 steps toward each env's own
+    final epsilon (0.1 / 0.01 / 0.5, main.py:68), so both the greedy argmax and the random draw run."""
+    check_sync_vs_oracle('q', 6, 256, 32, 0, iters=2, seed=66, frames=FRAMES, scale=4.0, learning_rate=2e-3,
+                         ep_start=0.5, ep_end_t=2000, learn_start=0, double_q=double_q)
