@@ -128,3 +128,12 @@ def test_q_bench_shape_matches_oracle(double_q):
     final epsilon (0.1 / 0.01 / 0.5, main.py:68), so both the greedy argmax and the random draw run."""
     check_sync_vs_oracle('q', 6, 256, 32, 0, iters=2, seed=66, frames=FRAMES, scale=4.0, learning_rate=2e-3,
                          ep_start=0.5, ep_end_t=2000, learn_start=0, double_q=double_q)
+
+
+@pytest.mark.timeout(900)
+def test_q_overlap_bench_shape_matches_oracle():
+    """bench.py --algo q --n-step 32 (the overlapped pipeline): 256 envs, stale-1 acting, the TD
+    targets of rollout k-1 formed by its backward with the target network as it stands then, a
+    target sync inside the run (target_q_update_step 16,384 = two updates of 8,192 env-steps)."""
+    check_overlap_vs_oracle(6, 256, 32, 0, rollouts=4, seed=67, frames=FRAMES, scale=4.0, learning_rate=2e-3,
+                            algo='q', target_q_update_step=16384, ep_start=0.5, ep_end_t=2000, learn_start=0)
