@@ -137,3 +137,11 @@ def test_q_overlap_bench_shape_matches_oracle():
     target sync inside the run (target_q_update_step 16,384 = two updates of 8,192 env-steps)."""
     check_overlap_vs_oracle(6, 256, 32, 0, rollouts=4, seed=67, frames=FRAMES, scale=4.0, learning_rate=2e-3,
                             algo='q', target_q_update_step=16384, ep_start=0.5, ep_end_t=2000, learn_start=0)
+
+
+@pytest.mark.timeout(900)
+def test_1024_env_overlap_matches_oracle():
+    """bench.py --envs 1024 (overlap): 32 row blocks in the partial fc, the fc weight GEMM's
+    in-workgroup split-K form (B = 5,120 > 2,560: the slab form), the conv backward over 5,120
+    samples -- the variants the 1,024-env line launches, against the oracle."""
+    check_overlap_vs_oracle(6, 1024, 5, 0, rollouts=3, seed=88, frames=2048, scale=4.0, learning_rate=2e-3)
