@@ -196,6 +196,7 @@ extern "C" int a3c_engine_destroy(a3c_engine* e) {
 
 static int frame_bytes(const a3c_engine* e) { return e->frame84 ? PLANE : SCREEN_H * SCREEN_W * 3; }
 
+static bool boot_bwd(const a3c_engine* e);
 static int l2bits_choice(const a3c_engine* e);
 extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out) {
   if (!cfg || !out) return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "null");
@@ -288,7 +289,7 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     ALLOC(sl.scr_l2, scrB * FLAT * 4);
     ALLOC(sl.scr_l3, scrB * FC * 4);
     ALLOC(sl.prep, PREP_BYTES);
-    if (e->overlap) ALLOC(sl.fcboot, (int64_t)FC_NS * E * FC * 4);
+    if (boot_bwd(e)) ALLOC(sl.fcboot, (int64_t)FC_NS * E * FC * 4);   // (only the A/B knob's form reads it)
     if (L.lstm) {
       ALLOC(sl.lh, nE * LSTM_U * 4);
       ALLOC(sl.lc, nE * LSTM_U * 4);
@@ -1384,7 +1385,8 @@ struct StateHeader {
   int64_t total, bytes, iter;
   uint64_t seed;
   int32_t grad_ready, grad_applied;
-  int32_t l2bits, pad;   // whether the rollout in flight wrote the l2 ReLU bits its backward reads
+  int32_t l2bits;        // whether the rollout in flight wrote the l2 ReLU bits its backward reads
+  int32_t boot_bwd;      // whether the pending backward folds V(s_n) from the slot's fc partials
 };
 constexpr uint32_t STATE_MAGIC = 0x53433341u;   // "A3CS"
 }
@@ -1411,7 +1413,7 @@ static std::vector<StateRegion> state_regions(const a3c_engine* e) {
       add(sl.z, (nE + E) * zs * 4); add(sl.R_buf, nE * 4);
       add(sl.act_l1, nE * C1_P * C1_N * 4); add(sl.act_l2, nE * FLAT * 4); add(sl.act_l3, nE * FC * 4);
       add(sl.l2m, nE * C2_Q * 4);     // (the pending backward's dl2 mask)
-      add(sl.fcboot, (int64_t)FC_NS * E * FC * 4);   // (boot_bwd: the pending backward's V(s_n) partials)
+      if (boot_bwd(e)) add(sl.fcboot, (int64_t)FC_NS * E * FC * 4);   // (the pending backward's V(s_n) partials)
     }
     if (e->L.lstm) {
       add(sl.lh, nE * LSTM_U * 4); add(sl.lc, nE * LSTM_U * 4);
@@ -1427,12 +1429,14 @@ static std::vector<StateRegion> state_regions(const a3c_engine* e) {
 
 static StateHeader state_header(const a3c_engine* e) {
   StateHeader h = {};
-  h.magic = STATE_MAGIC; h.version = 3;   // 2: + the l2 ReLU bits of the rollout in flight; 3: + l2bits
+  // 2: + the l2 ReLU bits of the rollout in flight; 3: + l2bits; 4: + boot_bwd, fcboot only with it
+  h.magic = STATE_MAGIC; h.version = 4;
   h.E = e->E; h.n = e->n; h.R = e->R; h.algo = e->L.algo; h.A = e->L.A; h.lstm = e->L.lstm ? 1 : 0;
   h.overlap = e->overlap; h.world = e->cfg.world_size; h.frame84 = e->frame84;
   h.env_id_base = e->cfg.env_id_base; h.seed = e->cfg.seed;   // the env shard and its random streams
   h.total = e->L.total;
   h.l2bits = l2bits_on(e) ? 1 : 0;
+  h.boot_bwd = boot_bwd(e) ? 1 : 0;
   int64_t b = sizeof(StateHeader);
   for (const StateRegion& x : state_regions(e)) b += (int64_t)x.bytes;
   h.bytes = b;
@@ -1489,7 +1493,7 @@ extern "C" int a3c_engine_state_load(a3c_engine* e, const void* host, int64_t by
   if (h.E != want.E || h.n != want.n || h.R != want.R || h.algo != want.algo || h.A != want.A ||
       h.lstm != want.lstm || h.overlap != want.overlap || h.world != want.world || h.frame84 != want.frame84 ||
       h.env_id_base != want.env_id_base || h.seed != want.seed || h.total != want.total || h.bytes != want.bytes ||
-      h.l2bits != want.l2bits || bytes != want.bytes)
+      h.l2bits != want.l2bits || h.boot_bwd != want.boot_bwd || bytes != want.bytes)
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_state_load", "state of a different engine configuration");
   hipStream_t s = (hipStream_t)stream;
   A3C_CHECK(hipStreamSynchronize(s));

@@ -213,7 +213,7 @@ __device__ inline uint2 u8x4_to_bf16x4(uint32_t d) {
 // written transposed, tmpT[X][y] (4 consecutive y per lane: one dword).  Vertical: C[x][yy] =
 // sum_k tmpT[x][vbase + k] V[k][yy] over 6 x 6 tiles, 4 consecutive x per lane: one dword of the
 // output row.  The B fragments (the tap digits) are compile-time tables in constant memory.
-// Lane layout of 16x16x64 i8 (tools/probes/mfma_i8_layout.hip): lane l holds A[l&15][16(l>>4)+j],
+// Lane layout of 16x16x64 i8 (tools/archive/probes/mfma_i8_layout.hip): lane l holds A[l&15][16(l>>4)+j],
 // B[16(l>>4)+j][l&15], j = 0..15, and C[4(l>>4)+i][l&15], i = 0..3.
 // ---------------------------------------------------------------------------------------
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -395,7 +395,14 @@ __device__ inline void vpass_mfma(const uint8_t* __restrict__ tmpT, uint8_t* __r
 #define SCREEN_FRAME_SMEM_NOKV (210 * 160 + 210 * 84 + 96)   // the tap table elsewhere (kvs_at)
 #define SCREEN_FRAME_SMEM (SCREEN_FRAME_SMEM_NOKV + SCREEN_KV_BYTES)
 #else
-#define SCREEN_FRAME_SMEM_NOKV (210 * 160 + 84 * 224)        // gray | tmpT
+// gray | slack | tmpT | slack: each pass's last K window reads up to 64 bytes from its 16-aligned
+// start, past the end of the last source row (gray row 209, tmpT row 83); the slack keeps those
+// reads inside the allocation and off the region other waves write (their taps are zero, so the
+// bytes read there never reach a result)
+constexpr int SCREEN_SLACK = 64;
+static_assert(kTab.hbase[MT_N - 1] + 64 <= IW + SCREEN_SLACK, "horizontal K window past gray's slack");
+static_assert(kTab.vbase[MT_N - 1] + 64 <= TMPT_LD + SCREEN_SLACK, "vertical K window past tmpT's slack");
+#define SCREEN_FRAME_SMEM_NOKV (210 * 160 + 64 + 84 * 224 + 64)
 #define SCREEN_FRAME_SMEM SCREEN_FRAME_SMEM_NOKV
 #endif
 
@@ -410,7 +417,11 @@ __device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __
                                     uint64_t* dbg = nullptr, uint16_t* lds_bf16 = nullptr, Mid mid = Mid(),
                                     int* kvs_at = nullptr) {
   uint8_t* gray = smem;
+#ifdef SCREEN_VALU
   uint8_t* tmp = smem + IH * IW;
+#else
+  uint8_t* tmp = smem + IH * IW + SCREEN_SLACK;
+#endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr int NWV = NT / 64;

@@ -185,10 +185,25 @@ def lib():
     return _lib
 
 
+ERR_INVALID, ERR_STATE = 10001, 10002      # include/a3c_hip.h A3C_ERR_*; other codes are hipError_t
+
+
+class A3CError(RuntimeError):
+    """A failed C-ABI call; ``rc`` is its status (A3C_ERR_* or a hipError_t)."""
+
+    def __init__(self, msg, rc):
+        super().__init__(msg)
+        self.rc = rc
+
+    @property
+    def device_fault(self):
+        return self.rc not in (ERR_INVALID, ERR_STATE)
+
+
 def check(rc, what=''):
     if rc != 0:
         msg = lib().a3c_last_error().decode(errors='replace')
-        raise RuntimeError(f'{what} failed ({rc}): {msg}')
+        raise A3CError(f'{what} failed ({rc}): {msg}', rc)
 
 
 def require_device():

@@ -31,6 +31,8 @@ a run of the same size (each rank's env shard); any other run resumes from param
 import glob
 import json
 import os
+import sys
+import zipfile
 
 import numpy as np
 
@@ -294,15 +296,34 @@ def restore_engine(saver, eng, names_shapes, rank=0, world=1):
     if not all_ok(arrays is not None):
         raise RuntimeError('restore_engine: a rank cannot read %s (%s)' % (path, err or 'another rank'))
     if plan[1] == 'exact':
-        ok = False
+        from . import _lib
+        ok, unusable, fatal = False, None, None
         try:
             state = arrays.get(STATE_KEY) if rank == 0 else load(path[:-4] + '.rank%d.npz' % rank).get(STATE_KEY)
             if state is not None:
                 eng.reset()
                 eng.load_state(state)
                 ok = True
-        except Exception:
-            ok = False
+            else:
+                unusable = 'no engine state in the file'
+        except _lib.A3CError as e:
+            # a state of another engine configuration / format version is unusable (fall back to
+            # parameters + step); a HIP failure is a device fault and must not be papered over
+            if e.device_fault:
+                fatal = e
+            else:
+                unusable = e
+        except (OSError, EOFError, KeyError, ValueError, zipfile.BadZipFile) as e:    # missing / damaged file
+            unusable = e
+        except Exception as e:             # programming errors are not a reason to fall back either
+            fatal = e
+        # every rank reaches both agreements, so a failure on one rank never strands the others
+        if not all_ok(fatal is None):
+            raise RuntimeError('restore_engine: rank %d: restoring the engine state from %s failed (%s)'
+                               % (rank, path, fatal if fatal is not None else 'on another rank')) from fatal
+        if unusable is not None:
+            print('[rank %d] restore_engine: the engine state of %s is unusable (%s); resuming from parameters '
+                  '+ step' % (rank, path, unusable), file=sys.stderr, flush=True)
         if all_ok(ok):
             return int(arrays[STEP_KEY])
     step = engine_restore(eng, names_shapes, arrays, None)

@@ -111,22 +111,67 @@ def host_cpu():
         allowed = len(os.sched_getaffinity(0))
     except AttributeError:
         allowed = None
-    return dict(model=model, nproc=os.cpu_count(), affinity=allowed)
+    quota = cgroup_cpu_quota()
+    limit = min(x for x in (allowed, os.cpu_count(), quota['cpus'] if quota else None) if x)
+    return dict(model=model, nproc=os.cpu_count(), affinity=allowed, cgroup=quota, cpu_limit=limit)
+
+
+def cgroup_cpu_quota():
+    """The CPU bandwidth limit of this process's cgroup, as CPUs (ceil(quota / period)), or None
+    when unlimited: cgroup v2 `cpu.max`, else v1 `cpu.cfs_quota_us` / `cpu.cfs_period_us`."""
+    import math
+    rel = '/'
+    try:
+        with open('/proc/self/cgroup') as f:
+            for line in f:
+                parts = line.strip().split(':', 2)
+                if len(parts) == 3 and (parts[0] == '0' or 'cpu' in parts[1].split(',')):
+                    rel = parts[2]
+                    if parts[0] == '0':
+                        break
+    except OSError:
+        pass
+    cands = [('/sys/fs/cgroup' + rel).rstrip('/') + '/cpu.max', '/sys/fs/cgroup/cpu.max']
+    for path in cands:
+        try:
+            q, p = open(path).read().split()[:2]
+        except (OSError, ValueError):
+            continue
+        if q == 'max':
+            return dict(source=path, quota=None, period=int(p), cpus=None)
+        return dict(source=path, quota=int(q), period=int(p), cpus=math.ceil(int(q) / int(p)))
+    for base in (('/sys/fs/cgroup/cpu' + rel).rstrip('/'), '/sys/fs/cgroup/cpu', '/sys/fs/cgroup/cpu,cpuacct'):
+        try:
+            q = int(open(base + '/cpu.cfs_quota_us').read())
+            p = int(open(base + '/cpu.cfs_period_us').read())
+        except (OSError, ValueError):
+            continue
+        return dict(source=base, quota=None if q < 0 else q, period=p, cpus=None if q < 0 else math.ceil(q / p))
+    return None
 
 
 def cpu_baseline(seconds, game, algo, frame84=False):
     """The reference's ps/worker algorithm restated on the CPU (oracle/ps_worker.py: shared-memory
     PS, W worker processes with Hogwild RMSProp, one numpy thread each) on the same synthetic
-    env: 1 ps / 1 worker (BASELINE config 1) and W = min(nproc - 1, 15) workers.  Runs before
-    the GPU is initialised (the workers are spawned processes)."""
+    env: 1 ps / 1 worker (BASELINE config 1) and W = (the box's CPU limit) - 1 workers.  Runs
+    before the GPU is initialised (the workers are spawned processes)."""
     from oracle import ps_worker
     A, lives = GAMES[game]
     n = 5 if algo == 'a3c' else 32
     host = host_cpu()
-    # W = nproc - 1 workers (SURVEY 8(d)), capped by the CPUs this process may use and by the
-    # box's CPU share (16 per GPU on the gpurun pool: nproc reports the whole host)
-    avail = host['affinity'] or host['nproc'] or 2
-    W = max(1, min(avail - 1, 15))
+    # W = limit - 1 workers plus the PS process (SURVEY 8(d): nproc - 1 workers), where the limit is
+    # the smallest of nproc, the affinity mask and the cgroup CPU quota -- the CPUs this process
+    # can actually run on at once -- and of the pool's per-GPU CPU share: a gpurun box is one GPU's
+    # share of a larger host (16 CPUs per GPU) that neither its affinity mask nor its cgroup states
+    # (BENCH_CPU_SHARE overrides the per-GPU figure).  Every figure is recorded in host_cpu.
+    import torch                        # device_count() does not initialise HIP on this image
+    gpus = max(1, torch.cuda.device_count())
+    per_gpu = int(os.environ.get('BENCH_CPU_SHARE', '16'))
+    host['gpu_share'] = dict(visible_gpus=gpus, cpus_per_gpu=per_gpu, cpus=per_gpu * gpus)
+    limit = min(host['cpu_limit'] or 2, per_gpu * gpus)
+    W = max(1, limit - 1)
+    host['limit_used'] = limit
+    host['workers'] = W
     one = ps_worker.run(seconds=seconds / 2, workers=1, envs_per_worker=8, n_step=n, action_size=A, algo=algo,
                         start_lives=lives, frame84=frame84)
     many = ps_worker.run(seconds=seconds / 2, workers=W, envs_per_worker=8, n_step=n, action_size=A, algo=algo,
@@ -138,28 +183,115 @@ def cpu_baseline(seconds, game, algo, frame84=False):
                        f'{many["iterations"]} iterations; 1 ps/1 worker: {one["value"]:.1f} env-steps/s')
 
 
+CPU_FILE_ENV = 'BENCH_CPU_BASELINE_FILE'    # the spawning parent's CPU baseline, for rank 0's line
+
+
+def spawn_ranks(args, cpu, cmd=None):
+    """`bench.py --gpus N` (N > 1) started without a launcher: run N fresh child processes, one
+    rank per GPU, with torch.distributed.run's environment contract (RANK, LOCAL_RANK, WORLD_SIZE,
+    MASTER_ADDR=127.0.0.1, MASTER_PORT), the same arguments, and wait for them.  This parent never
+    initialises the GPU (it only ran the CPU baseline, which rank 0 then puts in its line), so no
+    process that touched the device is replaced or forked.  Reference: main.py:50-66 (one process
+    per ps / worker task of the cluster).  cmd: the child command (default: this script with the
+    same arguments; tests substitute a CPU-only child)."""
+    import socket
+    import subprocess
+    import tempfile
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    fd, cpu_path = tempfile.mkstemp(prefix='bench_cpu_', suffix='.json')
+    with os.fdopen(fd, 'w') as f:
+        json.dump(cpu, f)
+    procs = []
+    try:
+        for r in range(args.gpus):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                       LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK='0', MASTER_ADDR='127.0.0.1',
+                       MASTER_PORT=str(port), BENCH_LAUNCHER='bench.py spawn')
+            env[CPU_FILE_ENV] = cpu_path
+            procs.append(subprocess.Popen(cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        rc = 0
+        pending = list(procs)
+        while pending:                 # the first failing rank ends the job (as torch.distributed.run)
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in pending:
+                        q.terminate()
+            time.sleep(0.05)
+        return rc
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        os.unlink(cpu_path)
+
+
+def dist_record(args, torch, dist, local):
+    """What the process group saw: backend, world size, launcher, every rank's device (index, name,
+    PCI bus id) and the RCCL version torch was built against."""
+    me = dict(rank=dist.get_rank(), local_rank=local, device=None, name='cpu', pci_bus_id=None, pci_device_id=None,
+              hostname=os.uname().nodename)
+    if torch.cuda.is_available():
+        dev = torch.cuda.current_device()
+        props = torch.cuda.get_device_properties(dev)
+        me.update(device=dev, name=props.name, pci_bus_id=getattr(props, 'pci_bus_id', None),
+                  pci_device_id=getattr(props, 'pci_device_id', None))
+    ranks = [None] * dist.get_world_size()
+    dist.all_gather_object(ranks, me)
+    rccl = None
+    try:
+        v = torch.cuda.nccl.version()
+        rccl = '.'.join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:           # gloo-only builds
+        rccl = None
+    return dict(backend=dist.get_backend(), world_size=dist.get_world_size(),
+                launcher=os.environ.get('BENCH_LAUNCHER', 'torch.distributed.run'),
+                rccl_version=rccl, ranks=ranks,
+                distinct_devices=len({(r['hostname'], r['pci_bus_id'], r['device']) for r in ranks}))
+
+
 def main():
     args = parse()
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit('--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)')
+    if world != args.gpus and world > 1:
+        raise SystemExit(f'--gpus {args.gpus} but WORLD_SIZE={world}')
     cpu = None
-    if world == 1 and rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds, args.game, args.algo, args.frames84)    # before any HIP initialisation
+    if rank == 0 and not args.no_cpu_baseline:
+        if os.environ.get(CPU_FILE_ENV):
+            with open(os.environ[CPU_FILE_ENV]) as f:
+                cpu = json.load(f)                  # measured by the spawning parent
+        else:
+            # rank 0, before any HIP initialisation (the workers are spawned processes); under a
+            # launcher at N > 1 the other ranks wait in the rendezvous meanwhile
+            cpu = cpu_baseline(args.cpu_seconds, args.game, args.algo, args.frames84)
+    if world == 1 and args.gpus > 1:
+        sys.exit(spawn_ranks(args, cpu))
+    # stdout carries exactly the one JSON line: native libraries' chatter (gloo's connection
+    # messages, runtime notices) goes to stderr
+    sys.stdout.flush()
+    line_out = os.fdopen(os.dup(1), 'w')
+    os.dup2(2, 1)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
     ndev = torch.cuda.device_count()
     torch.cuda.set_device(local % max(ndev, 1))
+    dist_rec = None
     if world > 1:
         if args.backend == 'nccl':
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
             dist.init_process_group('gloo')
+        dist_rec = dist_record(args, torch, dist, local)
 
     from src import _lib
     from src.engine import Engine
@@ -388,10 +520,10 @@ def main():
                        'window_ms': [round(w * 1e3, 3) for w in windows],
                        'value_spread': [round(steps_total / max(windows), 1), round(steps_total / min(windows), 1)],
                        'value_mean_over_windows': round(steps_total * len(windows) / sum(windows), 1)},
-            'roofline': roofline, 'cpu_baseline': cpu, 'kernels': kernels,
+            'roofline': roofline, 'cpu_baseline': cpu, 'kernels': kernels, 'dist': dist_rec,
             'final_loss': loss, 'params_finite': finite,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=line_out, flush=True)
     if ps is not None:
         ps.close()
     if world > 1:

@@ -102,18 +102,23 @@ class EngineRef:
         slots = [(tau - 3 + c) % self.R for c in range(4)]
         return np.ascontiguousarray(np.transpose(self.ring[:, slots], (0, 2, 3, 1)))
 
-    def _draw(self, z, t):
+    def draw_words(self, t):
+        """(u, rnd) of rollout step t: the Philox uniform the draw compares against and the
+        random action of the epsilon branch (the words the engine's head kernel uses)."""
         tau = self.tau + t
         x = px.philox4x32(np.uint32(tau & 0xFFFFFFFF), np.uint32(tau >> 32), self.ids, px.P_ACTION,
                           self.k0, self.k1)
+        return px.u01(x[0]), (x[1] % np.uint32(self.A)).astype(np.int32)
+
+    def _draw(self, z, t):
+        u, rnd = self.draw_words(t)
         if self.algo == 'a3c':
             pi, _, _ = R.softmax_stats(z[:, :self.A])
-            return R.sample_categorical(pi.astype(np.float32), px.u01(x[0])), pi
+            return R.sample_categorical(pi.astype(np.float32), u), pi
         eps = self.eps(t)
         q = z[:, :self.A].astype(np.float32)
         greedy = np.argmax(q, axis=1).astype(np.int32)
-        rnd = (x[1] % np.uint32(self.A)).astype(np.int32)
-        return np.where(px.u01(x[0]) < eps, rnd, greedy).astype(np.int32), None
+        return np.where(u < eps, rnd, greedy).astype(np.int32), None
 
     def worker_step(self, t=0, tau=None):
         """agent.py:55's loop counter at rollout step t of the rollout starting at tau."""
@@ -130,19 +135,25 @@ class EngineRef:
     def iterate(self, forced_actions=None, grads=True):
         """One iteration; returns a dict of everything the GPU engine exposes.  grads=False stops
         after the rollout and its targets (no batch forward / backward: for callers that
-        back-propagate the engine's own saved activations instead)."""
+        back-propagate the engine's own saved activations instead); grads='losses' adds the
+        independent batch forward and its losses, without the backward."""
         E, n, A, h = self.E, self.n, self.A, self.h
         acts = np.zeros((n, E), np.int32)
         sampled = np.zeros((n, E), np.int32)
         rewards = np.zeros((n, E), np.float32)
         rewards_raw = np.zeros((n, E), np.float32)
         terms = np.zeros((n, E), np.uint8)
+        us = np.zeros((n, E), np.float32)
+        epss = np.zeros((n, E), np.float32)
         zs, pis, frames = [], [], []
         h0c0 = self.hc
         for t in range(n):
             st = self.states(self.tau + t)
             z, hc = self._step_z(st, self.hc)
             a, pi = self._draw(z, t)
+            us[t] = self.draw_words(t)[0]
+            if self.algo == 'q':
+                epss[t] = self.eps(t)
             sampled[t] = a
             acts[t] = a if forced_actions is None else forced_actions[t]
             zs.append(z)
@@ -162,7 +173,7 @@ class EngineRef:
         states = np.concatenate([self.states(self.tau + t) for t in range(n)])      # b = t*E + e
         B = n * E
         out = dict(actions=acts, sampled=sampled, rewards=rewards, rewards_raw=rewards_raw, terminals=terms,
-                   z=np.stack(zs),
+                   z=np.stack(zs), u=us, eps=epss, h0c0=h0c0,
                    pi=pis, frames=np.stack(frames), tau=self.tau)
         if self.algo == 'a3c':
             zb, _ = self._step_z(self.states(self.tau + n), self.hc)
@@ -195,6 +206,9 @@ class EngineRef:
         else:
             loss, dz = R.q_loss_and_dz(fwd['z'], flat_acts, target.reshape(-1).astype(self.dtype))
             losses = dict(loss=loss, q_mean=fwd['z'][np.arange(B), flat_acts].mean())
+        if grads == 'losses':        # the independent forward's losses, no backward
+            out.update(losses=losses, z_batch=fwd['z'])
+            return out
         if self.lstm:
             g = R.lstm_a3c_backward(self.params, fwd, dz, terms)
         else:

@@ -28,7 +28,8 @@ def _names_shapes(A, algo):
     return R.param_shapes(A, algo)
 
 
-def _worker(wid, E, n, A, algo, lives, seed, seconds, shm_name, layout, start_evt, out_q, frame84=False):
+def _worker(wid, E, n, A, algo, lives, seed, seconds, shm_name, layout, start_evt, out_q, frame84=False,
+            ready_q=None):
     os.environ['OMP_NUM_THREADS'] = '1'
     os.environ['OPENBLAS_NUM_THREADS'] = '1'
     os.environ['MKL_NUM_THREADS'] = '1'
@@ -53,6 +54,8 @@ def _worker(wid, E, n, A, algo, lives, seed, seconds, shm_name, layout, start_ev
                     seed=seed, env_id_base=wid * E, dtype=np.float32, frame84=frame84)
     ref.cache_screens = False
     ref.reset()
+    if ready_q is not None:
+        ready_q.put(wid)
     start_evt.wait()
     t0 = time.perf_counter()
     steps = 0
@@ -98,12 +101,15 @@ def run(seconds=12.0, workers=1, envs_per_worker=8, n_step=5, action_size=6, alg
         ctx = mp.get_context('spawn')
         start_evt = ctx.Event()
         out_q = ctx.Queue()
+        ready_q = ctx.Queue()
         procs = [ctx.Process(target=_worker, args=(w, envs_per_worker, n_step, action_size, algo, start_lives,
-                                                   seed, seconds, shm.name, layout, start_evt, out_q, frame84))
+                                                   seed, seconds, shm.name, layout, start_evt, out_q, frame84,
+                                                   ready_q))
                  for w in range(workers)]
         for p in procs:
             p.start()
-        time.sleep(0.5)
+        for _ in procs:                # every worker built and reset: all start their clocks together
+            ready_q.get(timeout=600)
         start_evt.set()
         res = [out_q.get(timeout=seconds + 600) for _ in procs]
         for p in procs:

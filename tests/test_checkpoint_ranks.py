@@ -42,8 +42,9 @@ class FakeEngine:
     """The restore interface of src/engine.Engine over CPU tensors: state blobs of this rank load,
     others raise RuntimeError (as a3c_engine_state_load rejects another shard's state)."""
 
-    def __init__(self, rank):
+    def __init__(self, rank, fault=False):
         self.rank, self.algo, self.external_env, self.overlap = rank, 'a3c', False, False
+        self.fault = fault
         self.offsets, self.sizes, off = [], [], 0
         for _, shp in NS:
             self.offsets.append(off)
@@ -64,8 +65,11 @@ class FakeEngine:
         return np.array([self.rank, 7], np.uint8)
 
     def load_state(self, buf):
+        from src._lib import A3CError, ERR_INVALID
+        if self.fault:              # a HIP failure inside the load (hipErrorLaunchFailure)
+            raise A3CError('a3c_engine_state_load failed (719): unspecified launch failure', 719)
         if int(buf[0]) != self.rank:
-            raise RuntimeError('state of another env shard')
+            raise A3CError('a3c_engine_state_load failed (10001): state of another env shard', ERR_INVALID)
         self.loaded = 'exact'
 
     def set_step(self, g, w=None):
@@ -95,7 +99,7 @@ def _restore_worker(rank, world, port, out, ckdir, case):
             with open(saver.path(4321), 'wb') as f:
                 f.write(b'not a checkpoint')
         dist.barrier()
-    eng2 = FakeEngine(rank)
+    eng2 = FakeEngine(rank, fault=case == 'device_fault' and rank == 1)
     try:
         step = C.restore_engine(saver, eng2, NS, rank, world)
         res = dict(step=step, how=eng2.loaded, params=eng2.params.numpy().copy())
@@ -115,9 +119,15 @@ def _spawn(fn, world, *args):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize('case', ['exact', 'rank_file_missing', 'unreadable', 'fresh'])
+@pytest.mark.parametrize('case', ['exact', 'rank_file_missing', 'unreadable', 'fresh', 'device_fault'])
 def test_ranks_restore_alike(case, tmp_path):
+    """Every rank takes the same path: exact states, parameters + step when a state is unusable
+    (logged), or one agreed error -- an unreadable file, or a device fault inside a state load on
+    any rank, which must not silently fall back."""
     res = _spawn(_restore_worker, 2, str(tmp_path / 'ck'), case)
+    if case == 'device_fault':
+        assert all('restoring the engine state' in res[r].get('error', '') for r in range(2)), res
+        return
     if case == 'unreadable':
         assert all('cannot read' in res[r].get('error', '') for r in range(2)), res
         return

@@ -214,8 +214,9 @@ class _Oracle:
                 ref.tau += c['n']                 # the rollout owns tau in overlap mode
             assert np.array_equal(sl['rewards'].cpu().numpy(), out['rewards']), (k, r)
             assert np.array_equal(sl['terminals'].cpu().numpy(), out['terminals']), (k, r)
-            agree = (acts == out['sampled']).mean()
-            assert agree >= 0.98, (k, r, agree)
+            from tests._engine_parity import assert_draws_explained
+            z_eng = (sl['z'] if overlap else eng.z).cpu().numpy()[:c['n']].reshape(c['n'], c['E'], -1)
+            assert_draws_explained(acts, out, c['algo'], c['A'], (k, r), z_eng=z_eng)
             self.hist[r].append((Pk, planes, out))
         return Pk
 
@@ -365,19 +366,14 @@ def _hog_worker(rank, world, port, out, lockstep, cfg):
     ps = HogwildPS(eng.params)
     for it in range(ITERS):
         if lockstep:                      # deterministic order for the check: rank 0, then rank 1, ...
-            # (overlap: rollout k and the backward of k-1; the push / pull of k-1's gradient land in
-            # the snapshot of rollout k+1, as iterate_hogwild does)
+            # the production call in each rank's turn: rollout k (overlap: and the backward of k-1),
+            # the push of the clipped gradient, the pull into the next rollout's snapshot, the commit
             for turn in range(world):
                 dist.barrier()
                 if turn == rank:
-                    eng.rollout_grad()
-                    if eng.grad_ready:
-                        ps.push(eng.grads, lr_dev=eng.sched_ptr)
+                    eng.iterate_hogwild(ps)
                     torch.cuda.synchronize()
             dist.barrier()
-            ps.pull(eng.params)
-            eng.apply_commit(None)        # target copy (q) of the pulled params, snapshot, counters
-            torch.cuda.synchronize()
         else:
             eng.iterate_hogwild(ps)
     torch.cuda.synchronize()
@@ -398,10 +394,11 @@ def _hog_worker(rank, world, port, out, lockstep, cfg):
                               'w4-q-breakout-lockstep', 'w2-overlap-lockstep', 'w4-overlap-free',
                               'w2-q-overlap-lockstep'])
 def test_hogwild_sharded_ps(world, lockstep, cfg):
-    """`world` ranks on one GPU push into each other's IPC-mapped shards.  Lock-step order must
-    equal a single process applying every rank's clipped gradient in rank order each iteration
-    (q: and copying the target net at the same global step); free-running (the real unlocked mode)
-    must stay finite with every rank seeing the same shared params."""
+    """`world` ranks on one GPU push into each other's IPC-mapped shards.  Lock-step: each rank runs
+    the production Engine.iterate_hogwild in its turn (rollout, push, pull, commit), which must
+    equal a single process applying every rank's clipped gradient in rank order, each rank pulling
+    right after its own push (q: and copying the target net at the same global step); free-running
+    (the real unlocked mode) must stay finite with every rank seeing the same shared params."""
     c = _cfg(dict(cfg, E=16))
     cfg = dict(cfg, E=16)
     res = _run_ranks(_hog_worker, world, (lockstep, cfg))
@@ -416,26 +413,14 @@ def test_hogwild_sharded_ps(world, lockstep, cfg):
     engs = [_make(r, world, c['ov'], cfg) for r in range(world)]
     w = engs[0].params.clone()
     ms, mom = torch.ones_like(w), torch.zeros_like(w)
-    for it in range(ITERS if c['ov'] else 0):     # overlap: rollout k, push / pull of rollout k-1
-        for e in engs:
+    for it in range(ITERS):
+        for e in engs:          # rank order: each rank's push lands before the next rank's turn
             e.rollout_grad()
-        if not engs[0].grad_ready:
-            continue
-        for e in engs:
+            if not e.grad_ready:                # (overlap: the pipeline's first rollout)
+                continue
             lib().a3c_rmsprop_range(ptr(w), ptr(ms), ptr(mom), ptr(e.grads), w.numel(), ctypes.c_void_p(e.sched_ptr),
                                     0.0, 0.99, 0.0, 0.1, stream_handle())
-        for e in engs:
-            e.params.copy_(w)
-            e.apply_commit(None)
-    for it in range(0 if c['ov'] else ITERS):
-        for e in engs:          # every engine of an iteration uses the start-of-iteration params
-            e.params.copy_(w)
-        for e in engs:
-            e.rollout_grad()
-            lib().a3c_rmsprop_range(ptr(w), ptr(ms), ptr(mom), ptr(e.grads), w.numel(), ctypes.c_void_p(e.sched_ptr),
-                                    0.0, 0.99, 0.0, 0.1, stream_handle())
-        for e in engs:
-            e.params.copy_(w)
+            e.params.copy_(w)   # its pull sees every push so far
             e.apply_commit(None)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(w.cpu().numpy(), res[0]['shared'])

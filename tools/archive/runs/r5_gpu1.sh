@@ -3,7 +3,7 @@
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$ROOT"
 O=gpurun_out/r5g1; mkdir -p $O /tmp/pb
-#/opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 tools/probes/mfma_i8_layout.hip -o /tmp/pb/l 2>/dev/null || exit 1
+#/opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 tools/archive/probes/mfma_i8_layout.hip -o /tmp/pb/l 2>/dev/null || exit 1
 #timeout -k 5 30 /tmp/pb/l > $O/layout.txt || { cat $O/layout.txt; exit 1; }
 #cat $O/layout.txt
 timeout -k 10 900 python3 -u -m pytest tests/test_gpu_engine.py tests/test_gpu_kernels.py -x -q --timeout 300 --timeout-method thread \
