@@ -53,8 +53,8 @@ extern "C" int a3c_z_stride(const a3c_net_desc* net) {
 
 extern "C" int a3c_workspace_bytes(const a3c_net_desc* net, int64_t B, int64_t* bytes) {
   NetLayout L;
-  if (a3c_make_layout(net, &L) || B < 0 || !bytes)
-    return a3c_set_error(A3C_ERR_INVALID, "a3c_workspace_bytes", "bad argument");
+  if (a3c_make_layout(net, &L) || L.trunk != A3C_TRUNK_NIPS || B < 0 || !bytes)
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_workspace_bytes", "bad argument (per-op ops: NIPS trunk)");
   // forward: the bf16-split conv1 weights; backward: its plan (they never run at once)
   BwdPlan p = a3c_bwd_plan(L, B > 0 ? B : 1);
   int64_t m = p.total > PREP_BYTES / 4 ? p.total : PREP_BYTES / 4;
@@ -81,7 +81,7 @@ extern "C" int a3c_forward(const a3c_net_desc* net, const float* params, const u
                            float* act_l1, float* act_l2, float* act_l3, float* z, void* workspace,
                            void* stream) {
   NetLayout L;
-  if (a3c_make_layout(net, &L) || L.lstm || !params || !states || !act_l2 || !act_l3 || !z || B < 0 ||
+  if (a3c_make_layout(net, &L) || L.lstm || L.trunk != A3C_TRUNK_NIPS || !params || !states || !act_l2 || !act_l3 || !z || B < 0 ||
       B > 0x7fffffff || (((uintptr_t)states) & 15))
     return a3c_set_error(A3C_ERR_INVALID, "a3c_forward", "bad argument");
   if (B == 0) return 0;
@@ -136,7 +136,7 @@ extern "C" int a3c_loss_backward(const a3c_net_desc* net, const float* params, c
                                  const int32_t* actions, const float* target, float beta, int literal_adv,
                                  float* grads, float* loss_out, void* workspace, void* stream) {
   NetLayout L;
-  if (a3c_make_layout(net, &L) || L.lstm || !params || !states || !act_l1 || !act_l2 || !act_l3 || !z || !actions ||
+  if (a3c_make_layout(net, &L) || L.lstm || L.trunk != A3C_TRUNK_NIPS || !params || !states || !act_l1 || !act_l2 || !act_l3 || !z || !actions ||
       !target || !grads || !workspace || B <= 0 || B > 0x7fffffff || (((uintptr_t)states) & 15))
     return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "bad argument");
   a3c_init_once();

@@ -18,6 +18,7 @@
 #include "net_bwd.h"
 #include "optim.h"
 #include "gemm.h"
+#include "nature.h"
 
 void a3c_init_once();
 int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* C, int64_t M, hipStream_t s,
@@ -39,6 +40,8 @@ struct Slot {
   float* z;                // [(n+1)][E][zs]
   float* R_buf;            // [n][E] returns / TD targets
   float *act_l1, *act_l2, *act_l3;
+  float* act_l4;           // nature trunk: the fc output [n*E][512] (act_l1..3: its conv outputs)
+  float* nscr;             // nature trunk: the bootstrap state's activations [E][l1 | l2 | l3 | l4]
   uint32_t* l2m;           // act_l2's ReLU mask as bits [n*E][81], written by the forward's conv2
   float *scr_l2, *scr_l3;  // bootstrap / target forward scratch
   float* fcboot;           // boot_bwd: the bootstrap state's fc partials, read by the slot's backward
@@ -79,6 +82,8 @@ struct a3c_engine {
   float* ws;               // backward workspace
   float* fcpart;           // fused overlap rollout: the fc as FC_NS K-slice partials [FC_NS][E][FC]
   int fc_split;            // 1: the fused rollout's fc runs as k_fc_part + the head's fold
+  int nat;                 // the nature trunk (cfg.net.trunk = A3C_TRUNK_NATURE, nature.hip)
+  float* nat_fws;          // nature trunk: the rollout forward's fc split-K slabs
   float* lws;              // LSTM BPTT workspace (a3c_lstm_ws_floats)
   float* ldh;              // LSTM: dL/dh_t from the heads [nE][U]
   double* opt_part;
@@ -233,6 +238,18 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   e->fc_split = 1;
   e->fc_split = A3C_KNOB("A3C_FC_SPLIT", e->fc_split) != 0;
   e->frame84 = cfg->frame84 ? 1 : 0;
+  // the nature trunk (network.py:30-42) runs its own passes (nature.hip): no NIPS fusions; the
+  // screen is its own launch after each step's head, the exchange one-phase
+  e->nat = L.trunk == A3C_TRUNK_NATURE ? 1 : 0;
+  if (e->nat) {
+    e->fused_screen = 0;
+    e->fuse_conv = 0;
+    e->fc_split = 0;
+    if (e->ext) {
+      delete e;
+      return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "the nature trunk runs with device envs");
+    }
+  }
   if (e->frame84 && (e->ext || !e->fused_screen)) {   // the copy lives in the fused head kernels
     delete e;
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "frame84 needs device envs and the fused screen");
@@ -283,9 +300,17 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     ALLOC(sl.terms, nE);
     ALLOC(sl.z, (nE + E) * zs * 4);
     ALLOC(sl.R_buf, nE * 4);
-    ALLOC(sl.act_l1, nE * C1_P * C1_N * 4);
-    ALLOC(sl.act_l2, nE * FLAT * 4);
-    ALLOC(sl.act_l3, nE * FC * 4);
+    if (e->nat) {
+      ALLOC(sl.act_l1, nE * NT_A1 * 4);
+      ALLOC(sl.act_l2, nE * NT_A2 * 4);
+      ALLOC(sl.act_l3, nE * NT_FLAT * 4);
+      ALLOC(sl.act_l4, nE * NT_FC * 4);
+      ALLOC(sl.nscr, E * nat_act_floats() * 4);
+    } else {
+      ALLOC(sl.act_l1, nE * C1_P * C1_N * 4);
+      ALLOC(sl.act_l2, nE * FLAT * 4);
+      ALLOC(sl.act_l3, nE * FC * 4);
+    }
     ALLOC(sl.scr_l2, scrB * FLAT * 4);
     ALLOC(sl.scr_l3, scrB * FC * 4);
     ALLOC(sl.prep, PREP_BYTES);
@@ -309,8 +334,13 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   ALLOC(e->spans, 2 * (size_t)SPAN_RECS * SPAN_WGS * 2 * sizeof(unsigned long long));
   ALLOC(e->zt, scrB * zs * 4);
   ALLOC(e->ep_end, E * 4);
-  BwdPlan bp = a3c_bwd_plan(L, nE);
-  ALLOC(e->ws, bp.total * 4);
+  if (e->nat) {
+    ALLOC(e->ws, a3c_nat_bwd_ws_floats(L, nE) * 4);
+    ALLOC(e->nat_fws, (a3c_nat_fwd_ws_floats(E) > 0 ? a3c_nat_fwd_ws_floats(E) : 1) * 4);
+  } else {
+    BwdPlan bp = a3c_bwd_plan(L, nE);
+    ALLOC(e->ws, bp.total * 4);
+  }
   ALLOC(e->fcpart, (int64_t)FC_NS * E * FC * 4);
   ALLOC(e->opt_part, (int64_t)SS_MAX_BLOCKS * 8);
   ALLOC(e->sched, 64);
@@ -319,7 +349,8 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   // last: the other buffers keep the placement they had before the ReLU bits existed
   for (int k = 0; k < e->nslot; ++k) ALLOC(e->slot[k].l2m, nE * C2_Q * 4);
 #undef ALLOC
-  if (a3c_make_tab(L.nt, L.off, L.size, L.total, &e->tt) || a3c_fused_tab(L, &e->tt_f)) {
+  if (a3c_make_tab(L.nt, L.off, L.size, L.total, &e->tt) ||
+      (e->nat ? a3c_nat_fused_tab(L, &e->tt_f) : a3c_fused_tab(L, &e->tt_f))) {
     a3c_engine_destroy(e);
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "tensor table");
   }
@@ -333,8 +364,8 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
     }
   }
   // the split exchange needs eager launches (its event is recorded mid-backward) and a peer
-  e->split = cfg->split_exchange && cfg->world_size > 1 && !cfg->use_graph;
-  e->l2bits = l2bits_choice(e);
+  e->split = cfg->split_exchange && cfg->world_size > 1 && !cfg->use_graph && !e->nat;
+  e->l2bits = e->nat ? 0 : l2bits_choice(e);
   if (e->split && hipEventCreateWithFlags(&e->ev_head, hipEventDisableTiming) != hipSuccess) {
     a3c_engine_destroy(e);
     return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_create", "event creation failed");
@@ -567,6 +598,9 @@ static bool kernel_go(const a3c_engine* e) {
 // rollout start: forward weights of the rollout's parameters (+ q: the epsilon schedule)
 static int enqueue_rollout_begin(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
+  if (e->nat)   // (no prepared weights: the nature passes read the fp32 parameters)
+    return a3c_nat_prep_launch(e->overlap ? e->counters : nullptr, e->overlap ? sl.tau : nullptr,
+                               kernel_go(e) ? e->xflags + 1 : nullptr, s);
   // params are fixed for the rollout; overlap: the prep kernel also snapshots tau for the slot's
   // backward (sync: the slot's tau is the live counter)
   int rc = a3c_prep_fwd_launch(e->L, sl.P, sl.prep, s, e->overlap ? e->counters : nullptr,
@@ -642,7 +676,13 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
     nx.act_l2 = t + 1 < n ? sl.act_l2 + (o + E) * FLAT : sl.scr_l2;
     nx.l2m = t + 1 < n && l2bits_on(e) ? sl.l2m + (o + E) * C2_Q : nullptr;
   }
-  int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
+  int rc;
+  if (e->nat)
+    rc = a3c_nat_forward_launch(L, sl.P, ring_addr(e, t, e->counters), E, sl.act_l1 + o * NT_A1,
+                                sl.act_l2 + o * NT_A2, sl.act_l3 + o * NT_FLAT, sl.act_l4 + o * NT_FC, sl.z + o * zs, sel,
+                                e->nat_fws, s);
+  else
+    rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
                               sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s,
                               L.lstm ? &ls : nullptr, fuse && t > 0, has_next ? &nx : nullptr,
                               fc_split(e) ? e->fcpart : nullptr, l2bits_on(e) ? sl.l2m + o * C2_Q : nullptr);
@@ -674,6 +714,12 @@ static int enqueue_rollout_end(a3c_engine* e, const Slot& sl, hipStream_t s) {
       ls.wt = sl.lwt;
       ls.h_src = sl.lh + lastE * LSTM_U; ls.c_src = sl.lc + lastE * LSTM_U; ls.prev_terms = sl.terms + lastE;
       ls.h = sl.lhb; ls.c = sl.lcb;
+    }
+    if (e->nat) {
+      float* x = sl.nscr;
+      return a3c_nat_forward_launch(L, sl.P, ring_addr(e, n, e->counters), E, x, x + E * NT_A1,
+                                    x + E * (NT_A1 + NT_A2), x + E * (NT_A1 + NT_A2 + NT_FLAT), sl.z + e->nE * L.zs,
+                                    none, e->nat_fws, s);
     }
     int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, n, e->counters), E, nullptr, sl.scr_l2,
                                 sl.scr_l3, sl.z + e->nE * L.zs, none, s, L.lstm ? &ls : nullptr,
@@ -941,6 +987,10 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
     sp.sumsq_out = e->sumsq;
     sp.cut = L.off[T_FCW];
   }
+  if (e->nat)
+    rc = a3c_nat_backward_launch(L, sl.P, bsa, e->nE, sl.act_l1, sl.act_l2, sl.act_l3, sl.act_l4, sl.z, sl.actions,
+                                 sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra, &sf);
+  else
   rc = a3c_backward_launch(L, sl.P, bsa, e->nE, sl.act_l1, sl.act_l2, sl.act_l3, sl.z,
                            sl.actions, sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra,
                            fork && !e->split ? e->gs : nullptr, fork && !e->split ? e->ev_gfork : nullptr,
@@ -1411,7 +1461,12 @@ static std::vector<StateRegion> state_regions(const a3c_engine* e) {
       add(sl.actions, nE * 4); add(sl.frames, nE * 4); add(sl.rewards, nE * 4); add(sl.rewards_raw, nE * 4);
       add(sl.terms, nE);
       add(sl.z, (nE + E) * zs * 4); add(sl.R_buf, nE * 4);
-      add(sl.act_l1, nE * C1_P * C1_N * 4); add(sl.act_l2, nE * FLAT * 4); add(sl.act_l3, nE * FC * 4);
+      if (e->nat) {
+        add(sl.act_l1, nE * NT_A1 * 4); add(sl.act_l2, nE * NT_A2 * 4); add(sl.act_l3, nE * NT_FLAT * 4);
+        add(sl.act_l4, nE * NT_FC * 4);
+      } else {
+        add(sl.act_l1, nE * C1_P * C1_N * 4); add(sl.act_l2, nE * FLAT * 4); add(sl.act_l3, nE * FC * 4);
+      }
       add(sl.l2m, nE * C2_Q * 4);     // (the pending backward's dl2 mask)
       if (boot_bwd(e)) add(sl.fcboot, (int64_t)FC_NS * E * FC * 4);   // (the pending backward's V(s_n) partials)
     }
@@ -1524,7 +1579,8 @@ extern "C" int a3c_engine_slot_buffers(a3c_engine* e, int slot, a3c_engine_buffe
   b->tau = e->counters; b->global_step = e->counters + 1;
   b->actions = sl.actions; b->rewards = sl.rewards; b->terminals = sl.terms;
   b->z = sl.z; b->returns = sl.R_buf; b->loss = e->loss; b->sumsq = e->sumsq;
-  b->act_l1 = sl.act_l1; b->act_l2 = sl.act_l2; b->act_l3 = sl.act_l3;
+  b->act_l1 = sl.act_l1; b->act_l2 = sl.act_l2; b->act_l3 = sl.act_l3; b->act_l4 = sl.act_l4;
+  b->trunk = e->L.trunk;
   b->frame_pool = e->pool;
   b->env_frame = e->env.frame; b->env_lives = e->env.lives; b->env_episode = e->env.episode;
   b->env_step = e->env.ep_step; b->env_len = e->env.ep_len;
@@ -1571,6 +1627,38 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
   struct ResetShared {
     ~ResetShared() { a3c_set_shared_gpu(false); a3c_set_bwd_bound(false); a3c_set_fcp_split(2); }
   } reset_shared;
+  if (e->nat != (kernel >= A3C_KER_NAT_C1F))
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_time_kernel", "kernel id of another trunk");
+  if (e->nat) {   // one pass of the nature trunk: forward over E states, backward passes over n*E samples
+    const int pass = kernel - A3C_KER_NAT_C1F;
+    const bool fwd = pass <= NAT_FCF;
+    if (!fwd && !e->grad_ready)
+      return a3c_set_error(A3C_ERR_STATE, "a3c_engine_time_kernel", "backward passes: run an iteration first");
+    const Slot& bs = e->slot[e->nslot == 2 ? (int)((e->iter - 2) & 1) : 0];   // the last back-propagated rollout
+    const StateAddr sa = fwd ? ring_addr(e, 0, e->counters) : ring_addr(e, 0, bs.tau);
+    auto go = [&]() -> int {
+      return fwd ? a3c_nat_pass_launch(pass, L, e->params, sa, E, sl.act_l1, sl.act_l2, sl.act_l3, sl.act_l4,
+                                       e->nat_fws, nullptr, s)
+                 : a3c_nat_pass_launch(pass, L, bs.P, sa, e->nE, bs.act_l1, bs.act_l2, bs.act_l3, bs.act_l4, nullptr,
+                                       e->ws, s);
+    };
+    int rc = go();
+    if (rc) return rc;
+    hipEvent_t a, b;
+    A3C_CHECK(hipEventCreate(&a));
+    A3C_CHECK(hipEventCreate(&b));
+    A3C_CHECK(hipEventRecord(a, s));
+    for (int i = 0; i < iters && !rc; ++i) rc = go();
+    A3C_CHECK(hipEventRecord(b, s));
+    A3C_CHECK(hipEventSynchronize(b));
+    float ms = 0.f;
+    A3C_CHECK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (rc) return rc;
+    *avg_ms = ms / (float)iters;
+    return 0;
+  }
   if (kernel == A3C_KER_CONV12_FWD || kernel == A3C_KER_FC_FWD || kernel == A3C_KER_HEAD_SCREEN_CONV12) {
     int rc0 = a3c_prep_fwd_launch(L, e->params, sl.prep, s);
     if (rc0) return rc0;

@@ -1,0 +1,529 @@
+// The "nature" trunk of the reference's A3C Network (network.py:30-42: conv 8x8/4 32, conv 4x4/2
+// 64, conv 3x3/1 64, fc 3136 -> 512, all ReLU; heads network.py:60-79) on gfx950 matrix cores.
+//
+//  k_nat_gemm<MODE, BN>  one implicit-GEMM tile kernel for every convolution pass, operands gathered
+//                        straight from the NHWC activations (no im2col buffer in HBM), staged in LDS
+//                        as 16-deep K slices with a register prefetch of the next slice, and reduced
+//                        on v_mfma_f32_32x32x2f32 (exact fp32 products, fp32 accumulation: the
+//                        reference computes in fp32).  4 waves, each a 32x32 block of a
+//                        64x64 (BN = 64) or 128x32 (BN = 32: the 32-channel layers) tile.
+//    NG_FWD1  conv1: rows = (sample, output pixel), K = (kh, kw, cin) in TF order, A read from the
+//             u8 frame ring (the 4 history planes of the state, history.py:13-24), x / 255 applied to
+//             the accumulator (agent.py:226 / network.py:46); + bias, ReLU
+//    NG_FWD   conv2, conv3 from the fp32 NHWC output of the layer below; + bias, ReLU
+//    NG_DX    dX = col2im(dY W^T) * (X > 0), one stride parity class (py, px) per grid z: the output
+//             pixels y = S i + py, x = S j + px are reached only by taps kh = py + S th, kw = px + S tw,
+//             so K = (th, tw, cout) holds only real taps (conv2: 2x2x64 instead of 4x4x64)
+//    NG_DW    dW[k][cout] = sum over (sample, pixel) of patch(k) dY, the reduction split over grid z
+//             into per-split slabs (+ the column sums of dY: the bias gradient), folded in a fixed
+//             order by k_slab_group + k_finalize (net_bwd.hip) -- deterministic, no atomics
+//    NG_DW1   the same for conv1 (patches from the u8 ring; the 1/255 is the finalize's scale)
+//  fc 3136 -> 512 and its backward: gemm.hip (split-K slabs with the bias + ReLU epilogue; the
+//  weight gradient in-workgroup split-K).  Head (k_nat_head): head_row<512> + the action draw and the
+//  fused env act of net_head.h; head backward: k_head_bwd<512> (net_bwd.hip).
+#include "nature.h"
+#include "net_bwd.h"
+#include "net_head.h"
+
+enum { NG_FWD1 = 0, NG_FWD, NG_DX, NG_DW1, NG_DW };
+
+struct NatConv {
+  int H, W, C, KH, KW, S, OH, OW, OC;
+};
+static NatConv nat_conv(int l) {
+  if (l == 1) return {IMG, IMG, HIST, 8, 8, 4, NT1_O, NT1_O, NT1_N};
+  if (l == 2) return {NT1_O, NT1_O, NT1_N, 4, 4, 2, NT2_O, NT2_O, NT2_N};
+  return {NT2_O, NT2_O, NT2_N, 3, 3, 1, NT3_O, NT3_O, NT3_N};
+}
+
+struct NatGemm {
+  NatConv g;
+  StateAddr sa;        // NG_FWD1 / NG_DW1: the u8 state planes of sample b (b = t E + e)
+  const float* X;      // fp32 NHWC input activation [B][H][W][C] (NG_FWD, NG_DW; NG_DX: its ReLU mask)
+  const float* Wt;     // TF weights [KH][KW][C][OC]
+  const float* bias;   // NG_FWD*: [OC]
+  const float* dY;     // NG_DX, NG_DW*: [B][OH][OW][OC]
+  float* Y;            // NG_FWD*: [B][OH][OW][OC]; NG_DX: dX [B][H][W][C]
+  float* slab;         // NG_DW*: [nsplit][M][N]
+  float* colsum;       // NG_DW*: [nsplit][N]
+  int M, N, K;         // NG_DX: M per parity class; NG_DW*: M = KH KW C, N = OC, K = B OH OW (reduction)
+  int kchunk;          // NG_DW*: reduction rows per split (a multiple of 16)
+  float scale;         // NG_FWD1: 1/255
+};
+
+template <int MODE, int BN>
+__global__ void __launch_bounds__(256) k_nat_gemm(NatGemm a) {
+  constexpr int BM = 4096 / BN, BK = 16, LP = 4;
+  constexpr int WN = BN / 32;                                   // waves along n
+  constexpr bool A_KC = MODE == NG_FWD1 || MODE == NG_FWD || MODE == NG_DX;   // A quads along k
+  constexpr bool B_NC = MODE != NG_DX;                           // B quads along n
+  constexpr bool DW = MODE == NG_DW || MODE == NG_DW1;
+  constexpr bool U8 = MODE == NG_FWD1 || MODE == NG_DW1;
+  constexpr int AQ = BM * BK / 4 / 256;                          // A quads per thread (1 or 2)
+  constexpr int NBQ = BN * BK / 4;                               // B quads per tile (256 or 128)
+  __shared__ __attribute__((aligned(16))) float As[BK][BM + LP];
+  __shared__ __attribute__((aligned(16))) float Bs[BK][BN + LP];
+  const NatConv g = a.g;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int kbeg = DW ? (int)blockIdx.z * a.kchunk : 0;
+  const int kend = DW ? min(a.K, kbeg + a.kchunk) : a.K;
+  const int py = MODE == NG_DX ? (int)blockIdx.z / g.S : 0, px = MODE == NG_DX ? (int)blockIdx.z % g.S : 0;
+  const int NI = (g.H - py + g.S - 1) / g.S, NJ = (g.W - px + g.S - 1) / g.S;   // (NG_DX: the class grid)
+  const int P = g.OH * g.OW;
+  const int64_t tau0 = U8 && a.sa.tau_ptr ? *a.sa.tau_ptr : 0;
+
+  // ---- per-thread operand coordinates (fixed over the K loop) ----
+  int ar[AQ], ac[AQ];          // A_KC: row m (tile-local), k offset; else: k row, m offset
+  int64_t abase[AQ];           // NG_FWD: X offset of the patch origin; NG_DX: sample b
+  int ai[AQ], aj[AQ];          // NG_DX: class grid position; NG_FWD1: pixel origin (y0, x0)
+  const uint8_t* apl[AQ][4];   // NG_FWD1: the sample's 4 planes
+  bool aval[AQ];
+  int mk[AQ][3];               // DW: (kh, kw, c0) of the thread's m quad
+#pragma unroll
+  for (int i = 0; i < AQ; ++i) {
+    const int q = tid + 256 * i;
+    if constexpr (A_KC) { ar[i] = q >> 2; ac[i] = (q & 3) * 4; }
+    else { ar[i] = q / (BM / 4); ac[i] = (q % (BM / 4)) * 4; }
+    aval[i] = false; abase[i] = 0; ai[i] = aj[i] = 0;
+    if constexpr (A_KC) {
+      const int m = m0 + ar[i];
+      aval[i] = m < a.M;
+      const int mm = aval[i] ? m : 0;
+      if constexpr (MODE == NG_DX) {
+        const int b = mm / (NI * NJ), r = mm - b * (NI * NJ);
+        abase[i] = b; ai[i] = r / NJ; aj[i] = r - (r / NJ) * NJ;
+      } else {
+        const int b = mm / P, pos = mm - b * P, oy = pos / g.OW, ox = pos - oy * g.OW;
+        if constexpr (MODE == NG_FWD1) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) apl[i][c] = state_plane(a.sa, b, c, tau0);
+          ai[i] = oy * g.S; aj[i] = ox * g.S;
+        } else {
+          abase[i] = (((int64_t)b * g.H + oy * g.S) * g.W + ox * g.S) * g.C;
+        }
+      }
+    } else {
+      const int m = m0 + ac[i];                                  // TF order k = (kh KW + kw) C + c
+      aval[i] = m < a.M;
+      const int mm = aval[i] ? m : 0;
+      mk[i][0] = mm / (g.KW * g.C);
+      mk[i][1] = (mm / g.C) % g.KW;
+      mk[i][2] = mm % g.C;
+    }
+  }
+  const bool bthr = tid < NBQ;
+  int br, bc;                  // B_NC: k row, n offset; else: n row, k offset
+  if constexpr (B_NC) { br = tid / (BN / 4); bc = (tid % (BN / 4)) * 4; }
+  else { br = tid >> 2; bc = (tid & 3) * 4; }
+  const int TW = g.KW / g.S;   // NG_DX taps per class along x
+
+  auto load_a = [&](int i, int k0) -> f32x4 {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (A_KC) {
+      const int k = k0 + ac[i];
+      if (!aval[i] || k >= kend) return v;
+      if constexpr (MODE == NG_FWD1) {                            // k = (kh 8 + kw) 4 + c: the 4 planes
+        const int kh = k >> 5, kw = (k >> 2) & 7;
+        const int off = (ai[i] + kh) * IMG + aj[i] + kw;
+        v[0] = (float)apl[i][0][off]; v[1] = (float)apl[i][1][off];
+        v[2] = (float)apl[i][2][off]; v[3] = (float)apl[i][3][off];
+      } else if constexpr (MODE == NG_FWD) {
+        const int kh = k / (g.KW * g.C), rem = k - kh * g.KW * g.C, kw = rem / g.C, c0 = rem - kw * g.C;
+        v = *(const f32x4*)(a.X + abase[i] + ((int64_t)kh * g.W + kw) * g.C + c0);
+      } else {                                                     // NG_DX: k = (th TW + tw) OC + oc
+        const int th = k / (TW * g.OC), rem = k - th * TW * g.OC, tw = rem / g.OC, oc0 = rem - tw * g.OC;
+        const int oy = ai[i] - th, ox = aj[i] - tw;
+        if (oy >= 0 && oy < g.OH && ox >= 0 && ox < g.OW)
+          v = *(const f32x4*)(a.dY + ((abase[i] * g.OH + oy) * g.OW + ox) * g.OC + oc0);
+      }
+    } else {                                                       // DW: reduction row r, m quad
+      const int r = k0 + ar[i];
+      if (!aval[i] || r >= kend) return v;
+      const int b = r / P, pos = r - b * P, oy = pos / g.OW, ox = pos - oy * g.OW;
+      const int y = oy * g.S + mk[i][0], x = ox * g.S + mk[i][1];
+      if constexpr (MODE == NG_DW1) {
+        const int off = y * IMG + x;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = (float)state_plane(a.sa, b, c, tau0)[off];
+      } else {
+        v = *(const f32x4*)(a.X + (((int64_t)b * g.H + y) * g.W + x) * g.C + mk[i][2]);
+      }
+    }
+    return v;
+  };
+  auto load_b = [&](int k0) -> f32x4 {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (!bthr) return v;
+    if constexpr (B_NC) {
+      const int k = k0 + br, n = n0 + bc;
+      if (k >= kend || n >= a.N) return v;
+      v = DW ? *(const f32x4*)(a.dY + (int64_t)k * g.OC + n) : *(const f32x4*)(a.Wt + (int64_t)k * g.OC + n);
+    } else {                                                       // NG_DX: B(k, c) = W[kh][kw][c][oc..]
+      const int n = n0 + br, k = k0 + bc;
+      if (n >= a.N || k >= kend) return v;
+      const int th = k / (TW * g.OC), rem = k - th * TW * g.OC, tw = rem / g.OC, oc0 = rem - tw * g.OC;
+      const int kh = py + g.S * th, kw = px + g.S * tw;
+      v = *(const f32x4*)(a.Wt + (((int64_t)kh * g.KW + kw) * g.C + n) * g.OC + oc0);
+    }
+    return v;
+  };
+
+  f32x16 acc = {};
+  float csum = 0.f;
+  const bool do_colsum = DW && a.colsum && blockIdx.y == 0 && tid < BN;
+  f32x4 ra[AQ], rb;
+#pragma unroll
+  for (int i = 0; i < AQ; ++i) ra[i] = load_a(i, kbeg);
+  rb = load_b(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) {
+      if constexpr (A_KC) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) As[ac[i] + c][ar[i]] = ra[i][c];
+      } else {
+        *(f32x4*)&As[ar[i]][ac[i]] = ra[i];
+      }
+    }
+    if (bthr) {
+      if constexpr (B_NC) {
+        *(f32x4*)&Bs[br][bc] = rb;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) Bs[bc + c][br] = rb[c];
+      }
+    }
+    __syncthreads();
+    if (k0 + BK < kend) {
+#pragma unroll
+      for (int i = 0; i < AQ; ++i) ra[i] = load_a(i, k0 + BK);
+      rb = load_b(k0 + BK);
+    }
+    if (do_colsum) {
+#pragma unroll
+      for (int k = 0; k < BK; ++k) csum += Bs[k][tid];
+    }
+    const int kh = lane >> 5, c = lane & 31;
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[2 * kk + kh][wm * 32 + c], Bs[2 * kk + kh][wn * 32 + c], acc, 0,
+                                                 0, 0);
+  }
+
+  const int col = n0 + wn * 32 + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (row >= a.M || col >= a.N) continue;
+    float v = acc[r];
+    if constexpr (MODE == NG_FWD1 || MODE == NG_FWD) {
+      v = fmaxf((MODE == NG_FWD1 ? v * a.scale : v) + a.bias[col], 0.f);
+      a.Y[(int64_t)row * a.N + col] = v;
+    } else if constexpr (MODE == NG_DX) {
+      const int b = row / (NI * NJ), rr = row - b * (NI * NJ), i = rr / NJ, j = rr - (rr / NJ) * NJ;
+      const int64_t o = (((int64_t)b * g.H + py + g.S * i) * g.W + px + g.S * j) * g.C + col;
+      a.Y[o] = a.X[o] > 0.f ? v : 0.f;
+    } else {
+      a.slab[((int64_t)blockIdx.z * a.M + row) * a.N + col] = v;
+    }
+  }
+  if (do_colsum && n0 + tid < a.N) a.colsum[(int64_t)blockIdx.z * a.N + n0 + tid] = csum;
+}
+
+template <int MODE, int BN>
+static int nat_go(const NatGemm& a, unsigned gz, hipStream_t s) {
+  constexpr int BM = 4096 / BN;
+  if (a.M <= 0 || a.N <= 0) return 0;
+  const dim3 grid((unsigned)((a.N + BN - 1) / BN), (unsigned)((a.M + BM - 1) / BM), gz);
+  hipLaunchKernelGGL((k_nat_gemm<MODE, BN>), grid, dim3(256), 0, s, a);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+// the policy / value head of B states (one wave each) on the 512-wide fc output, + the action
+// draw and fused env act when sel.mode >= 0 (agent.py:59-62, network.py:72)
+__global__ void __launch_bounds__(256) k_nat_head(const float* __restrict__ l4, int64_t B, const float* __restrict__ Wp,
+                                                  const float* __restrict__ bp, const float* __restrict__ Wv,
+                                                  const float* __restrict__ bv, int A, int zs, float* __restrict__ z,
+                                                  HeadSelect sel) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float myz = head_row<NoMid, NT_FC>(l4, b, Wp, bp, Wv, bv, A, lane);
+  if (lane < zs) z[b * zs + lane] = myz;
+  if (sel.mode >= 0) (void)head_act(myz, lane, A, sel, b);
+  // the overlap rollout's bootstrap head (its last kernel) advances tau (no tau read here)
+  if (sel.adv_ptr && blockIdx.x == 0 && threadIdx.x == 0) *sel.adv_ptr += sel.adv_n;
+}
+
+// ---------------------------------------------------------------------------------------
+// passes (one launch each, timed individually by a3c_engine_time_kernel)
+// ---------------------------------------------------------------------------------------
+#define NAT_GROUPS 8
+struct NatPlan {
+  int head_split, ns1, ns2, ns3, kc1, kc2, kc3;
+  int64_t dz, dl4, dl3, dl2, dl1, terms, hgrad, hcol, hslab, fccol, s1, s2, s3, c1, c2, c3, g1, g2, g3, total;
+};
+// the reduction split of a weight-gradient pass: ~target workgroups over its m tiles
+static void dw_split(int64_t R, int mtiles, int target, int& ns, int& kc) {
+  int want = target / mtiles;
+  if (want < 1) want = 1;
+  int64_t per = (R + want - 1) / want;
+  per = (per + 15) / 16 * 16;
+  if (per < 16) per = 16;
+  kc = (int)per;
+  ns = (int)((R + per - 1) / per);
+}
+static NatPlan nat_plan(const NetLayout& L, int64_t B) {
+  NatPlan p = {};
+  int64_t o = 0;
+  auto take = [&](int64_t floats) { int64_t r = o; o += (floats + 63) & ~(int64_t)63; return r; };
+  p.head_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(NT_FC, L.zs, (int)B, 128));
+  dw_split(B * NT1_P, 2, 512, p.ns1, p.kc1);      // M = 256 in 128-row tiles
+  dw_split(B * NT2_P, 8, 512, p.ns2, p.kc2);      // M = 512 in 64-row tiles
+  dw_split(B * NT3_P, 9, 512, p.ns3, p.kc3);      // M = 576
+  p.dz = take(B * L.zs);
+  p.dl4 = take(B * NT_FC);
+  p.dl3 = take(B * NT_FLAT);
+  p.dl2 = take(B * NT_A2);
+  p.dl1 = take(B * NT_A1);
+  p.terms = take(B * 4);
+  p.hgrad = take((int64_t)NT_FC * L.zs);
+  p.hcol = take((int64_t)p.head_split * L.zs);
+  p.hslab = take(p.head_split > 1 ? (int64_t)p.head_split * NT_FC * L.zs : 0);
+  p.fccol = take(NT_FC);
+  p.s1 = take((int64_t)p.ns1 * NT_K1 * NT1_N);
+  p.s2 = take((int64_t)p.ns2 * NT_K2 * NT2_N);
+  p.s3 = take((int64_t)p.ns3 * NT_K3 * NT3_N);
+  p.c1 = take((int64_t)p.ns1 * NT1_N);
+  p.c2 = take((int64_t)p.ns2 * NT2_N);
+  p.c3 = take((int64_t)p.ns3 * NT3_N);
+  p.g1 = take((int64_t)NAT_GROUPS * NT_K1 * NT1_N);
+  p.g2 = take((int64_t)NAT_GROUPS * NT_K2 * NT2_N);
+  p.g3 = take((int64_t)NAT_GROUPS * NT_K3 * NT3_N);
+  p.total = o;
+  return p;
+}
+
+static int fc_split(int64_t B) { return a3c_gemm_effective_split(NT_FLAT, a3c_gemm_plan_split((int)B, NT_FC, NT_FLAT, 512)); }
+
+int64_t a3c_nat_fwd_ws_floats(int64_t B) {
+  const int sp = fc_split(B);
+  return sp > 1 ? (int64_t)sp * B * NT_FC : 0;
+}
+int64_t a3c_nat_bwd_ws_floats(const NetLayout& L, int64_t B) { return nat_plan(L, B).total; }
+
+// one pass of the forward (B states) or of the backward (B samples, buffers of the plan in bws)
+int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* l1,
+                        const float* l2, const float* l3, const float* l4, float* fws, float* bws, hipStream_t s) {
+  NatGemm a = {};
+  switch (pass) {
+    case NAT_C1F:
+      a.g = nat_conv(1);
+      a.sa = sa;
+      a.Wt = P + L.off[N_L1W]; a.bias = P + L.off[N_L1B]; a.Y = (float*)l1;
+      a.M = (int)(B * NT1_P); a.N = NT1_N; a.K = NT_K1; a.scale = 1.0f / 255.0f;
+      return nat_go<NG_FWD1, 32>(a, 1, s);
+    case NAT_C2F:
+      a.g = nat_conv(2);
+      a.X = l1; a.Wt = P + L.off[N_L2W]; a.bias = P + L.off[N_L2B]; a.Y = (float*)l2;
+      a.M = (int)(B * NT2_P); a.N = NT2_N; a.K = NT_K2;
+      return nat_go<NG_FWD, 64>(a, 1, s);
+    case NAT_C3F:
+      a.g = nat_conv(3);
+      a.X = l2; a.Wt = P + L.off[N_L3W]; a.bias = P + L.off[N_L3B]; a.Y = (float*)l3;
+      a.M = (int)(B * NT3_P); a.N = NT3_N; a.K = NT_K3;
+      return nat_go<NG_FWD, 64>(a, 1, s);
+    case NAT_FCF: {
+      // l4 = relu(l3 W + b) (network.py:41-42, ops.py:41-44): split-K slabs, the fold applies the epilogue
+      GemmArgs gf = {};
+      gf.A = l3; gf.lda = NT_FLAT;
+      gf.B = P + L.off[N_FCW]; gf.ldb = NT_FC;
+      gf.C = (float*)l4; gf.ldc = NT_FC;
+      gf.M = (int)B; gf.N = NT_FC; gf.K = NT_FLAT;
+      gf.epi = EPI_BIAS_RELU; gf.bias = P + L.off[N_FCB];
+      gf.nsplit = fc_split(B); gf.slab = fws;
+      return a3c_gemm(true, true, gf, s);
+    }
+    default:
+      break;
+  }
+  const NatPlan p = nat_plan(L, B);
+  switch (pass) {
+    case NAT_C3W:     // dW3 (+ db3) over the (sample, pixel) rows
+      a.g = nat_conv(3);
+      a.X = l2; a.dY = bws + p.dl3; a.slab = bws + p.s3; a.colsum = bws + p.c3;
+      a.M = NT_K3; a.N = NT3_N; a.K = (int)(B * NT3_P); a.kchunk = p.kc3;
+      return nat_go<NG_DW, 64>(a, (unsigned)p.ns3, s);
+    case NAT_C3X:     // dl2 = col2im(dl3 W3^T) * (l2 > 0)
+      a.g = nat_conv(3);
+      a.X = l2; a.dY = bws + p.dl3; a.Wt = P + L.off[N_L3W]; a.Y = bws + p.dl2;
+      a.M = (int)(B * NT2_P); a.N = NT2_N; a.K = 3 * 3 * NT3_N;
+      return nat_go<NG_DX, 64>(a, 1, s);
+    case NAT_C2W:
+      a.g = nat_conv(2);
+      a.X = l1; a.dY = bws + p.dl2; a.slab = bws + p.s2; a.colsum = bws + p.c2;
+      a.M = NT_K2; a.N = NT2_N; a.K = (int)(B * NT2_P); a.kchunk = p.kc2;
+      return nat_go<NG_DW, 64>(a, (unsigned)p.ns2, s);
+    case NAT_C2X:     // dl1 = col2im(dl2 W2^T) * (l1 > 0), per stride-2 parity class
+      a.g = nat_conv(2);
+      a.X = l1; a.dY = bws + p.dl2; a.Wt = P + L.off[N_L2W]; a.Y = bws + p.dl1;
+      a.M = (int)(B * (NT1_O / 2) * (NT1_O / 2)); a.N = NT1_N; a.K = 2 * 2 * NT2_N;
+      return nat_go<NG_DX, 32>(a, 4, s);
+    case NAT_C1W:     // dW1 (+ db1) from the u8 planes (the input needs no gradient)
+      a.g = nat_conv(1);
+      a.sa = sa; a.dY = bws + p.dl1; a.slab = bws + p.s1; a.colsum = bws + p.c1;
+      a.M = NT_K1; a.N = NT1_N; a.K = (int)(B * NT1_P); a.kchunk = p.kc1;
+      return nat_go<NG_DW1, 32>(a, (unsigned)p.ns1, s);
+    default:
+      return a3c_set_error(A3C_ERR_INVALID, "a3c_nat_pass_launch", "unknown pass");
+  }
+}
+
+// the rollout's tau snapshot and the backward's go (k_prep_fwd's duties, without the NIPS weight
+// preparation)
+__global__ void k_nat_prep(const int64_t* __restrict__ tau_src, int64_t* __restrict__ tau_dst, uint32_t* sig) {
+  if (tau_dst) *tau_dst = *tau_src;
+  if (sig) (void)__hip_atomic_fetch_add(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+int a3c_nat_prep_launch(const int64_t* tau_src, int64_t* tau_dst, uint32_t* sig, hipStream_t s) {
+  hipLaunchKernelGGL(k_nat_prep, dim3(1), dim3(1), 0, s, tau_src, tau_src ? tau_dst : nullptr, sig);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------------------
+int a3c_nat_forward_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, float* l1, float* l2,
+                           float* l3, float* l4, float* z, const HeadSelect& sel, float* ws, hipStream_t s) {
+  if (L.trunk != A3C_TRUNK_NATURE || B <= 0 || B * NT1_P > 0x7fffffffLL)
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_nat_forward", "nature trunk, 0 < B, B * 400 < 2^31");
+  for (int pass = NAT_C1F; pass <= NAT_FCF; ++pass) {
+    const int rc = a3c_nat_pass_launch(pass, L, P, sa, B, l1, l2, l3, l4, ws, nullptr, s);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(k_nat_head, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, l4, B, P + L.off[N_HW],
+                     P + L.off[N_HB], P + L.off[N_VW], P + L.off[N_VB], L.A, L.zs, z, sel);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// backward
+// ---------------------------------------------------------------------------------------
+// every tensor but the fc weights gets its gradient from a k_finalize segment
+static bool nat_finalized(int t) { return t != N_FCW; }
+
+int a3c_nat_fused_tab(const NetLayout& L, TensorTab* tt) {
+  if (L.nt != N_NT) return -1;
+  tt->n = L.nt;
+  int nb = 0;
+  for (int t = 0; t < L.nt; ++t) {
+    tt->off[t] = L.off[t];
+    tt->size[t] = L.size[t];
+    tt->pb_first[t] = nb;
+    tt->pb_count[t] = nat_finalized(t) ? FIN_X : (int)((L.size[t] + SS_CHUNK - 1) / SS_CHUNK);
+    nb += tt->pb_count[t];
+  }
+  if (nb > SS_MAX_BLOCKS) return -1;
+  tt->nblocks = nb;
+  tt->total = L.total;
+  return 0;
+}
+
+int a3c_nat_backward_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* l1,
+                            const float* l2, const float* l3, const float* l4, const float* z,
+                            const int32_t* actions, const float* target, float beta, int literal, float* grads,
+                            float* loss_out, float* ws, hipStream_t s, const ReturnsArgs* ra_in, const SumsqFused* sf) {
+  if (L.trunk != A3C_TRUNK_NATURE || B <= 0 || B * NT1_P > 0x7fffffffLL)
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_nat_backward", "nature trunk, 0 < B, B * 400 < 2^31");
+  ReturnsArgs ra = {};
+  if (ra_in) ra = *ra_in;
+  const NatPlan p = nat_plan(L, B);
+  float* dz = ws + p.dz;
+  float* dl4 = ws + p.dl4;
+  float* terms = ws + p.terms;
+  // returns (fused), losses, dz, dl4 = (dz [W_p W_v]^T) * (l4 > 0)
+  int rc = a3c_head_bwd_launch(NT_FC, L, z, actions, target, l4, P + L.off[N_HW], P + L.off[N_VW], beta, literal, B, dz,
+                               dl4, terms, ra, 1, s);
+  if (rc) return rc;
+  // head weights: dW[512][zs] = l4^T dz (split-K folded by the finalize), db = colsum(dz)
+  GemmArgs gh = {};
+  gh.A = l4; gh.lda = NT_FC;
+  gh.B = dz; gh.ldb = L.zs;
+  gh.C = ws + p.hgrad; gh.ldc = L.zs;
+  gh.M = NT_FC; gh.N = L.zs; gh.K = (int)B;
+  gh.epi = EPI_STORE; gh.slab = ws + p.hslab; gh.nsplit = p.head_split; gh.colsum = ws + p.hcol;
+  gh.defer_reduce = 1;
+  rc = a3c_gemm(false, true, gh, s);
+  if (rc) return rc;
+  // fc weights: dW[3136][512] = l3^T dl4 straight into grads (split-K inside the workgroups), db = colsum
+  GemmArgs gf = {};
+  gf.A = l3; gf.lda = NT_FLAT;
+  gf.B = dl4; gf.ldb = NT_FC;
+  gf.C = grads + L.off[N_FCW]; gf.ldc = NT_FC;
+  gf.M = NT_FLAT; gf.N = NT_FC; gf.K = (int)B;
+  gf.epi = EPI_STORE; gf.colsum = ws + p.fccol; gf.wg_split = 4; gf.xcd = 1;
+  rc = a3c_gemm(false, true, gf, s);
+  if (rc) return rc;
+  // dl3 = (dl4 W^T) * (l3 > 0)
+  GemmArgs gd = {};
+  gd.A = dl4; gd.lda = NT_FC;
+  gd.B = P + L.off[N_FCW]; gd.ldb = NT_FC;
+  gd.C = ws + p.dl3; gd.ldc = NT_FLAT;
+  gd.M = (int)B; gd.N = NT_FLAT; gd.K = NT_FC;
+  gd.epi = EPI_MASK; gd.mask = l3; gd.ldm = NT_FLAT; gd.nsplit = 1;
+  rc = a3c_gemm(true, false, gd, s);
+  if (rc) return rc;
+  for (int pass = NAT_C3W; pass <= NAT_C1W; ++pass) {
+    rc = a3c_nat_pass_launch(pass, L, P, sa, B, l1, l2, l3, l4, nullptr, ws, s);
+    if (rc) return rc;
+  }
+  // the weight slabs in NAT_GROUPS fixed-order groups, then k_finalize: every segment, the loss
+  // terms, the fused per-tensor norms and the lr schedule
+  const int g1 = p.ns1 < NAT_GROUPS ? p.ns1 : NAT_GROUPS, g2 = p.ns2 < NAT_GROUPS ? p.ns2 : NAT_GROUPS,
+            g3 = p.ns3 < NAT_GROUPS ? p.ns3 : NAT_GROUPS;
+  rc = a3c_slab_group_launch(ws + p.s1, p.ns1, g1, (int64_t)NT_K1 * NT1_N, ws + p.g1, s);
+  if (!rc) rc = a3c_slab_group_launch(ws + p.s2, p.ns2, g2, (int64_t)NT_K2 * NT2_N, ws + p.g2, s);
+  if (!rc) rc = a3c_slab_group_launch(ws + p.s3, p.ns3, g3, (int64_t)NT_K3 * NT3_N, ws + p.g3, s);
+  if (rc) return rc;
+  FinalizeSegs fs = {};
+  fs.dst = grads;
+  auto seg = [&](const float* src, int64_t stride, int nsplit, int rows, int src_ld, int col0, int ncols, int tensor,
+                 int dst_ld, float scale) {
+    FinalizeSeg& q = fs.s[fs.n++];
+    q.src = src; q.split_stride = stride; q.nsplit = nsplit; q.rows = rows; q.src_ld = src_ld;
+    q.col0 = col0; q.ncols = ncols; q.dst_off = L.off[tensor]; q.dst_ld = dst_ld; q.scale = scale;
+    q.slot = sf ? sf->tt->pb_first[tensor] : -1;
+  };
+  // the patch rows of conv1 are raw u8 pixels: dW1 takes the 1/255 of the input scaling here
+  seg(ws + p.g1, (int64_t)NT_K1 * NT1_N, g1, 1, 0, 0, NT_K1 * NT1_N, N_L1W, 0, 1.0f / 255.0f);
+  seg(ws + p.c1, NT1_N, p.ns1, 1, 0, 0, NT1_N, N_L1B, 0, 1.0f);
+  seg(ws + p.g2, (int64_t)NT_K2 * NT2_N, g2, 1, 0, 0, NT_K2 * NT2_N, N_L2W, 0, 1.0f);
+  seg(ws + p.c2, NT2_N, p.ns2, 1, 0, 0, NT2_N, N_L2B, 0, 1.0f);
+  seg(ws + p.g3, (int64_t)NT_K3 * NT3_N, g3, 1, 0, 0, NT_K3 * NT3_N, N_L3W, 0, 1.0f);
+  seg(ws + p.c3, NT3_N, p.ns3, 1, 0, 0, NT3_N, N_L3B, 0, 1.0f);
+  seg(ws + p.fccol, NT_FC, 1, 1, 0, 0, NT_FC, N_FCB, 0, 1.0f);
+  const float* hsrc = p.head_split > 1 ? ws + p.hslab : ws + p.hgrad;
+  const int64_t hstride = (int64_t)NT_FC * L.zs;
+  seg(hsrc, hstride, p.head_split, NT_FC, L.zs, 0, L.A, N_HW, L.A, 1.0f);
+  seg(ws + p.hcol, L.zs, p.head_split, 1, 0, 0, L.A, N_HB, 0, 1.0f);
+  seg(hsrc, hstride, p.head_split, NT_FC, L.zs, L.A, 1, N_VW, 1, 1.0f);
+  seg(ws + p.hcol, L.zs, p.head_split, 1, 0, L.A, 1, N_VB, 0, 1.0f);
+  int nsumblk = 0;
+  if (sf) {
+    fs.part = sf->part;
+    fs.tt = *sf->tt;
+    fs.op = *sf->op;
+    fs.sum_c0[0] = 0;
+    fs.sum_t[0] = N_FCW;
+    fs.sum_c0[1] = fs.tt.pb_count[N_FCW];
+    fs.nsum = 1;
+    nsumblk = fs.sum_c0[1];
+  }
+  return a3c_finalize_launch(fs, nsumblk, terms, B, loss_out, s);
+}

@@ -37,6 +37,7 @@ enum { T_L1W = 0, T_L1B, T_L2W, T_L2B, T_FCW, T_FCB, T_HW, T_HB, T_VW, T_VB, T_L
 
 struct NetLayout {
   int algo, A, zs;
+  int trunk;                // A3C_TRUNK_NIPS (tensor order T_*), A3C_TRUNK_NATURE (nature.h N_*)
   int lstm;                 // 1: LSTM head (tensors T_LW, T_LB; heads read the LSTM's h)
   int nt;
   int64_t off[A3C_MAX_TENSORS], size[A3C_MAX_TENSORS];
@@ -50,16 +51,34 @@ inline int a3c_zs(int algo, int A) {
 
 inline int a3c_make_layout(const a3c_net_desc* d, NetLayout* L) {
   if (!d) return -1;
-  if (d->trunk != A3C_TRUNK_NIPS || d->history_length != HIST || d->screen_h != IMG ||
+  // the nature trunk (network.py:30-42) belongs to the A3C Network only: feed-forward policy /
+  // value heads (the reference's Q-net, agent.py:226-252, is NIPS-only, and has no LSTM)
+  const bool nature = d->trunk == A3C_TRUNK_NATURE;
+  if ((d->trunk != A3C_TRUNK_NIPS && !nature) || d->history_length != HIST || d->screen_h != IMG ||
       d->screen_w != IMG || d->action_size < 1 || d->action_size > 31 ||
       (d->algo != A3C_ALGO_A3C && d->algo != A3C_ALGO_Q) ||
-      (d->lstm_units != 0 && (d->lstm_units != LSTM_U || d->algo != A3C_ALGO_A3C)))
+      (d->lstm_units != 0 && (d->lstm_units != LSTM_U || d->algo != A3C_ALGO_A3C)) ||
+      (nature && (d->algo != A3C_ALGO_A3C || d->lstm_units != 0)))
     return -1;
   const int A = d->action_size;
   L->algo = d->algo;
   L->A = A;
   L->zs = a3c_zs(d->algo, A);
+  L->trunk = d->trunk;
   L->lstm = d->lstm_units != 0;
+  if (nature) {   // l1..l3 conv [kh,kw,cin,cout] + bias, l4 [3136,512] + bias, p [512,A] + bias, q [512,1] + bias
+    const int64_t ns[12] = {8 * 8 * HIST * 32, 32, 4 * 4 * 32 * 64, 64, 3 * 3 * 64 * 64, 64, 3136LL * 512, 512,
+                            512LL * A, A, 512, 1};
+    L->nt = 12;
+    int64_t o = 0;
+    for (int i = 0; i < L->nt; ++i) {
+      L->off[i] = o;
+      L->size[i] = ns[i];
+      o += (ns[i] + 63) & ~(int64_t)63;
+    }
+    L->total = o;
+    return 0;
+  }
   int64_t sizes[12] = {(int64_t)KC1 * C1_N, C1_N, (int64_t)KC2 * C2_N, C2_N, (int64_t)FLAT * FC, FC,
                        (int64_t)FC * A, A, FC, 1, (int64_t)LSTM_K * LSTM_G, LSTM_G};
   L->nt = d->algo == A3C_ALGO_A3C ? (L->lstm ? 12 : 10) : 8;

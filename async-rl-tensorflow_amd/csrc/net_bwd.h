@@ -110,3 +110,12 @@ int a3c_conv12_launch(const NetLayout& L, const float* P, const uint8_t* prep, c
                       float* act_l1, float* act_l2, hipStream_t s, uint32_t* l2m = nullptr);
 int a3c_conv_bwd_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* act_l1,
                         const float* dl2, float* ws, hipStream_t s);
+
+// shared with the nature trunk (nature.hip): the head backward at width 256 (FC) or 512, the
+// deterministic slab grouping, and k_finalize (segments + loss terms + fused norms / schedule)
+int a3c_head_bwd_launch(int width, const NetLayout& L, const float* z, const int32_t* actions, const float* target,
+                        const float* h, const float* Wp, const float* Wv, float beta, int literal, int64_t B,
+                        float* dz, float* dh, float* terms, const ReturnsArgs& ra, int relu, hipStream_t s);
+int a3c_slab_group_launch(const float* src, int nsplit, int groups, int64_t len, float* dst, hipStream_t s);
+int a3c_finalize_launch(const FinalizeSegs& fs, int nsumblk, const float* terms, int64_t B, float* loss_out,
+                        hipStream_t s);

@@ -64,6 +64,8 @@ __global__ void k_td_target(const float* __restrict__ rewards, const uint8_t* __
 }
 
 // ---------------------------------------------------------------------------------------
+// W: the head's input width (FC = 256, NIPS trunk; NT_FC = 512, nature trunk)
+template <int W>
 __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ z, int zs, int A, int algo,
                                                   const int32_t* __restrict__ actions,
                                                   const float* __restrict__ target,
@@ -129,24 +131,53 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ z, i
     }
   }
   if (lane < zs) dz[b * zs + lane] = mydz;
-  // dl3[k] = (sum_j W[k][j] dz_j) * (l3[k] > 0), k = 4*lane + i
-  f32x4 g = {0.f, 0.f, 0.f, 0.f};
-  for (int j = 0; j < A; ++j) {
-    float dj = __shfl(mydz, j, 64);
+  if constexpr (W == FC) {
+    // dl3[k] = (sum_j W[k][j] dz_j) * (l3[k] > 0), k = 4*lane + i
+    f32x4 g = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < A; ++j) {
+      float dj = __shfl(mydz, j, 64);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) g[i] += Wp[(int64_t)(4 * lane + i) * A + j] * dj;
-  }
-  if (Wv) {
-    f32x4 wv = *(const f32x4*)(Wv + 4 * lane);
+      for (int i = 0; i < 4; ++i) g[i] += Wp[(int64_t)(4 * lane + i) * A + j] * dj;
+    }
+    if (Wv) {
+      f32x4 wv = *(const f32x4*)(Wv + 4 * lane);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) g[i] += wv[i] * dV;
-  }
-  if (relu) {    // feed-forward head: through the fc ReLU; LSTM head: dL/dh as is
-    f32x4 h = *(const f32x4*)(h3 + b * FC + 4 * lane);
+      for (int i = 0; i < 4; ++i) g[i] += wv[i] * dV;
+    }
+    if (relu) {    // feed-forward head: through the fc ReLU; LSTM head: dL/dh as is
+      f32x4 h = *(const f32x4*)(h3 + b * FC + 4 * lane);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) g[i] = h[i] > 0.f ? g[i] : 0.f;
+      for (int i = 0; i < 4; ++i) g[i] = h[i] > 0.f ? g[i] : 0.f;
+    }
+    *(f32x4*)(dh3 + b * FC + 4 * lane) = g;
+  } else {
+    // the same per feature k = 256 q + 4 lane + i, q < W / 256
+    constexpr int NQ = W / 256;
+    f32x4 g[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) g[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < A; ++j) {
+      float dj = __shfl(mydz, j, 64);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) g[q][i] += Wp[(int64_t)(256 * q + 4 * lane + i) * A + j] * dj;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (Wv) {
+        f32x4 wv = *(const f32x4*)(Wv + 256 * q + 4 * lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) g[q][i] += wv[i] * dV;
+      }
+      if (relu) {
+        f32x4 h = *(const f32x4*)(h3 + b * W + 256 * q + 4 * lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) g[q][i] = h[i] > 0.f ? g[q][i] : 0.f;
+      }
+      *(f32x4*)(dh3 + b * W + 256 * q + 4 * lane) = g[q];
+    }
   }
-  *(f32x4*)(dh3 + b * FC + 4 * lane) = g;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -851,6 +882,37 @@ __global__ void __launch_bounds__(256) k_finalize(FinalizeSegs fs, const float* 
   sumsq_chunk(fs.dst, fs.tt, t, c, fs.part, fs.tt.pb_first[t] + c);
 }
 
+// host launchers shared with the nature trunk's backward (nature.hip)
+int a3c_head_bwd_launch(int width, const NetLayout& L, const float* z, const int32_t* actions, const float* target,
+                        const float* h, const float* Wp, const float* Wv, float beta, int literal, int64_t B,
+                        float* dz, float* dh, float* terms, const ReturnsArgs& ra, int relu, hipStream_t s) {
+  const dim3 grid((unsigned)((B + 3) / 4));
+  if (width == FC)
+    hipLaunchKernelGGL(k_head_bwd<FC>, grid, dim3(256), 0, s, z, L.zs, L.A, L.algo, actions, target, h, Wp, Wv, beta,
+                       literal, 1.0f / (float)B, B, dz, dh, terms, ra, relu);
+  else if (width == 512)
+    hipLaunchKernelGGL(k_head_bwd<512>, grid, dim3(256), 0, s, z, L.zs, L.A, L.algo, actions, target, h, Wp, Wv, beta,
+                       literal, 1.0f / (float)B, B, dz, dh, terms, ra, relu);
+  else
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_head_bwd_launch", "head width");
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+int a3c_slab_group_launch(const float* src, int nsplit, int groups, int64_t len, float* dst, hipStream_t s) {
+  const int per = (nsplit + groups - 1) / groups;
+  hipLaunchKernelGGL(k_slab_group, dim3((unsigned)((len + 255) / 256), (unsigned)groups), dim3(256), 0, s, src, nsplit,
+                     per, len, dst);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+int a3c_finalize_launch(const FinalizeSegs& fs, int nsumblk, const float* terms, int64_t B, float* loss_out,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize, dim3((unsigned)(FIN_X * fs.n + (fs.no_tail ? 0 : 1) + nsumblk)), dim3(256), 0, s, fs,
+                     terms, B, loss_out);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
 // tensors whose gradient a k_finalize segment writes (a3c_backward_launch's seg() calls)
 static bool finalize_tensor(const NetLayout& L, int t) {
   return t == T_L1W || t == T_L1B || t == T_L2W || t == T_L2B || t == T_FCB || t == T_HW || t == T_HB ||
@@ -1060,7 +1122,7 @@ int a3c_backward_launch(const NetLayout& L, const float* params, const StateAddr
     return a3c_set_error(A3C_ERR_INVALID, "a3c_loss_backward", "the LSTM head needs its rollout sequence");
   // head input: the fc ReLU output, or the LSTM's h (C5)
   const float* head_in = lb ? lb->h : act_l3;
-  hipLaunchKernelGGL(k_head_bwd, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, z, L.zs, L.A, L.algo,
+  hipLaunchKernelGGL(k_head_bwd<FC>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, z, L.zs, L.A, L.algo,
                      actions, target, head_in, P + L.off[T_HW], a3c ? P + L.off[T_VW] : nullptr, beta,
                      literal, 1.0f / (float)B, B, dz, lb ? lb->dh : dh3, terms, ra, lb ? 0 : 1);
   A3C_CHECK(hipGetLastError());

@@ -80,8 +80,8 @@ def parse_flags(argv=None):
   p.add_argument('--lstm', type=str2bool, default=False,
                  help='engine mode, a3c: the 256-cell LSTM policy head (BASELINE config 5, DESIGN §4b)')
   p.add_argument('--dqn_type', choices=['nips', 'nature'], default='nips',
-                 help="conv trunk of network.py:30-50 (Network(DQN_type=...)); the engine fuses the nips "
-                      "trunk, nature runs through src/network.Network only")
+                 help="conv trunk of network.py:30-50 (Network(DQN_type=...)): nips (fused kernels) or nature "
+                      "(implicit-GEMM kernels, nature.hip; --algo a3c)")
   p.add_argument('--logdir', default='./logs')
   return p.parse_args(argv)
 
@@ -92,9 +92,9 @@ def engine_options(flags):
   nature trunk).  Returns the Engine keyword arguments the flags select."""
   if flags.dueling:
     raise ValueError('--dueling (agent.py:234-249) is not fused into the engine: use --mode agent')
-  if flags.dqn_type != 'nips':
-    raise ValueError('--dqn_type %s: the engine fuses the nips trunk (network.py:43-50); the nature trunk '
-                     'runs through src/network.Network' % flags.dqn_type)
+  if flags.dqn_type == 'nature' and (flags.algo != 'a3c' or flags.lstm):
+    raise ValueError('--dqn_type nature: the A3C Network trunk (network.py:30-42) runs with --algo a3c and the '
+                     'feed-forward head (the Q-net of agent.py:226-252 is nips only)')
   if flags.double_q and flags.algo != 'q':
     raise ValueError('--double_q is a Q-learning option (agent.py:176-184): use it with --algo q')
   if flags.lstm and flags.algo != 'a3c':
@@ -102,6 +102,8 @@ def engine_options(flags):
   kw = dict(lstm=bool(flags.lstm))
   if flags.double_q:
     kw['double_q'] = True
+  if flags.dqn_type == 'nature':
+    kw['dqn_type'] = 'nature'
   return kw
 
 
@@ -111,7 +113,7 @@ def initial_params(eng, action_size, algo, seed):
   zero biases (ops.py:24,38-39)."""
   from src.initializers import flatten_host, init_params
   from src.kernels import param_names_shapes
-  ns = param_names_shapes(action_size, algo, lstm=eng.lstm)
+  ns = param_names_shapes(action_size, algo, lstm=eng.lstm, dqn_type=eng.dqn_type)
   return flatten_host(ns, eng.offsets, eng.params.numel(), init_params(ns, seed=seed))
 
 
@@ -179,7 +181,7 @@ def run_engine(config, flags):
   eng = Engine(num_envs=E, n_step=flags.n_step, action_size=A, algo=flags.algo, start_lives=lives,
                num_frames=1 if host else flags.num_frames, seed=flags.random_seed, env_id_base=rank * E,
                world_size=world, overlap=overlap, external_env=host, **net_kw, **opts)
-  ns = param_names_shapes(A, flags.algo, lstm=eng.lstm)
+  ns = param_names_shapes(A, flags.algo, lstm=eng.lstm, dqn_type=eng.dqn_type)
   # checkpoints: <logdir>/<model_dir> as the Supervisor's logdir (main.py:75), Saver max_to_keep
   # (agent.py:29); restored at start as managed_session does (main.py:90)
   ckdir = flags.checkpoint_dir or os.path.join(flags.logdir, BaseModel(config, verbose=False).model_dir)

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get('A3C_LIB') or os.path.join(os.path.dirname(_HERE), 'li
 A3C_ALGO_A3C = 0
 A3C_ALGO_Q = 1
 A3C_TRUNK_NIPS = 0
+A3C_TRUNK_NATURE = 1
 A3C_LSTM_UNITS = 256
 MAX_TENSORS = 16
 
@@ -55,7 +56,7 @@ class EngineBuffers(ctypes.Structure):
                 ('zs', c_int), ('n_tensors', c_int), ('offsets', c_i64 * MAX_TENSORS),
                 ('sizes', c_i64 * MAX_TENSORS), ('sched', c_void_p),
                 ('lstm_h', c_void_p), ('lstm_c', c_void_p), ('lstm_hp', c_void_p), ('lstm_cp', c_void_p),
-                ('lstm_gates', c_void_p), ('lstm_units', c_int)]
+                ('lstm_gates', c_void_p), ('lstm_units', c_int), ('act_l4', c_void_p), ('trunk', c_int)]
 
 
 # name -> (restype, argtypes)
@@ -159,6 +160,9 @@ OPTIONAL_IN_OLD_BUILDS = MEASUREMENT_ONLY + ('a3c_engine_exchange_split', 'a3c_e
                                              'a3c_engine_state_load')
 
 KER_CONV12_FWD, KER_FC_FWD, KER_ENV_STEP, KER_CONV_BWD, KER_HEAD_SCREEN, KER_HEAD_SCREEN_CONV12, KER_FC_PART = 0, 1, 2, 3, 4, 5, 6
+# nature trunk passes (include/a3c_hip.h A3C_KER_NAT_*)
+KER_NAT = {'conv1_fwd': 7, 'conv2_fwd': 8, 'conv3_fwd': 9, 'fc_fwd': 10, 'conv3_dw': 11, 'conv3_dx': 12, 'conv2_dw': 13,
+           'conv2_dx': 14, 'conv1_dw': 15}
 
 _lib = None
 
@@ -223,9 +227,13 @@ def stream_handle(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
-def net_desc(action_size, algo='a3c', lstm=False):
-    """lstm: the C5 LSTM head (a3c only; build-defined, the reference has no recurrent code)."""
-    return NetDesc(A3C_ALGO_A3C if algo == 'a3c' else A3C_ALGO_Q, A3C_TRUNK_NIPS, int(action_size), 4, 84, 84,
+def net_desc(action_size, algo='a3c', lstm=False, dqn_type='nips'):
+    """lstm: the C5 LSTM head (a3c only; build-defined, the reference has no recurrent code);
+    dqn_type: 'nips' (agent.py:226-251, network.py:43-52) or 'nature' (network.py:30-42, A3C heads)."""
+    trunk = {'nips': A3C_TRUNK_NIPS, 'nature': A3C_TRUNK_NATURE}.get(str(dqn_type).lower())
+    if trunk is None:
+        raise ValueError('Wrong DQN type: %s' % dqn_type)                          # network.py:54
+    return NetDesc(A3C_ALGO_A3C if algo == 'a3c' else A3C_ALGO_Q, trunk, int(action_size), 4, 84, 84,
                    A3C_LSTM_UNITS if lstm else 0)
 
 

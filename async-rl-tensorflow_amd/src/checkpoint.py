@@ -153,7 +153,7 @@ def load(path):
 def engine_arrays(eng, names_shapes, with_state=True):
     """The engine's parameters (+ target for q, RMSProp slots, step) keyed by TF names, and its
     whole state blob."""
-    algo = eng.algo
+    algo, dqn = eng.algo, getattr(eng, 'dqn_type', 'nips')
     state = eng.save_state() if with_state else None     # (first: waits for every engine stream)
 
     def tensors(flat):
@@ -163,7 +163,7 @@ def engine_arrays(eng, names_shapes, with_state=True):
     P, MS, MOM = tensors(eng.params), tensors(eng.ms), tensors(eng.mom)
     out = {}
     for name, _ in names_shapes:
-        tn = tf_name(name, algo)
+        tn = tf_name(name, algo, dqn)
         out[tn] = P[name]
         rms, mom = slot_names(tn)
         out[rms], out[mom] = MS[name], MOM[name]
@@ -189,7 +189,7 @@ def engine_restore(eng, names_shapes, arrays, state=None):
     restored ``step`` (agent.py:34,46) -- the worker step at the saved ``__worker_step__`` when the
     file has one.  Returns the global step."""
     import torch
-    algo = eng.algo
+    algo, dqn = eng.algo, getattr(eng, 'dqn_type', 'nips')
     step = int(arrays[STEP_KEY])
     if state is not None and not eng.external_env:
         eng.reset()
@@ -209,16 +209,16 @@ def engine_restore(eng, names_shapes, arrays, state=None):
                 v = default[off:off + sz]
             out[off:off + sz] = np.asarray(v, np.float32).reshape(-1)
         return out
-    P = flat(lambda n: arrays.get(tf_name(n, algo)))
+    P = flat(lambda n: arrays.get(tf_name(n, algo, dqn)))
     if P is None:
-        missing = [tf_name(n, algo) for n, _ in names_shapes if tf_name(n, algo) not in arrays]
+        missing = [tf_name(n, algo, dqn) for n, _ in names_shapes if tf_name(n, algo, dqn) not in arrays]
         raise ValueError('checkpoint lacks %s' % missing)
     eng.reset(P)
     if algo == 'q':
         T = flat(lambda n: arrays.get(tf_target_name(n)), P)
         eng.target_params.copy_(torch.as_tensor(T))
-    ms = flat(lambda n: arrays.get(slot_names(tf_name(n, algo))[0]))
-    mom = flat(lambda n: arrays.get(slot_names(tf_name(n, algo))[1]))
+    ms = flat(lambda n: arrays.get(slot_names(tf_name(n, algo, dqn))[0]))
+    mom = flat(lambda n: arrays.get(slot_names(tf_name(n, algo, dqn))[1]))
     if ms is not None and mom is not None:
         eng.ms.copy_(torch.as_tensor(ms))
         eng.mom.copy_(torch.as_tensor(mom))

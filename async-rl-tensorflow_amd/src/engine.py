@@ -50,13 +50,16 @@ def _view(ptr, shape, dtype):
 class Engine:
     def __init__(self, num_envs=256, n_step=5, action_size=6, algo='a3c', start_lives=0, num_frames=1024,
                  seed=123, env_id_base=0, world_size=1, use_graph=False, overlap=False, lstm=False,
-                 external_env=False, **overrides):
+                 external_env=False, dqn_type='nips', **overrides):
         _lib.require_device()
         if lstm and algo != 'a3c':
             raise ValueError('the LSTM head is an a3c head')
+        self.dqn_type = str(dqn_type).lower()
+        if self.dqn_type == 'nature' and (algo != 'a3c' or lstm or external_env):
+            raise ValueError('the nature trunk (network.py:30-42) runs A3C heads, feed-forward, on device envs')
         cfg = _lib.EngineConfig()
         lib().a3c_engine_config_default(ctypes.byref(cfg))
-        cfg.net = _lib.net_desc(action_size, algo, lstm)
+        cfg.net = _lib.net_desc(action_size, algo, lstm, self.dqn_type)
         self.lstm = bool(lstm)
         cfg.num_envs = int(num_envs)
         cfg.n_step = int(n_step)
@@ -125,14 +128,20 @@ class Engine:
                         lstm_hp=_view(b.lstm_hp, (n, E, U), torch.float32),
                         lstm_cp=_view(b.lstm_cp, (n, E, U), torch.float32),
                         lstm_gates=_view(b.lstm_gates, (n, E, 4 * U), torch.float32))
-        return dict(**lstm, actions=_view(b.actions, (n, E), torch.int32),
+        if self.dqn_type == 'nature':     # conv outputs NHWC [20,20,32] / [9,9,64] / [7,7,64], fc out 512
+            acts = dict(act_l1=_view(b.act_l1, (n * E, 12800), torch.float32),
+                        act_l2=_view(b.act_l2, (n * E, 5184), torch.float32),
+                        act_l3=_view(b.act_l3, (n * E, 3136), torch.float32),
+                        act_l4=_view(b.act_l4, (n * E, 512), torch.float32))
+        else:
+            acts = dict(act_l1=_view(b.act_l1, (n * E, 6400), torch.float32),
+                        act_l2=_view(b.act_l2, (n * E, 2592), torch.float32),
+                        act_l3=_view(b.act_l3, (n * E, 256), torch.float32))
+        return dict(**lstm, **acts, actions=_view(b.actions, (n, E), torch.int32),
                     rewards=_view(b.rewards, (n, E), torch.float32),
                     terminals=_view(b.terminals, (n, E), torch.uint8),
                     z=_view(b.z, (n + 1, E, self.zs), torch.float32),
-                    returns=_view(b.returns, (n, E), torch.float32),
-                    act_l1=_view(b.act_l1, (n * E, 6400), torch.float32),
-                    act_l2=_view(b.act_l2, (n * E, 2592), torch.float32),
-                    act_l3=_view(b.act_l3, (n * E, 256), torch.float32))
+                    returns=_view(b.returns, (n, E), torch.float32))
 
     def slot(self, k):
         """Rollout buffers of slot k (overlap: rollout i lives in slot i & 1)."""

@@ -78,10 +78,19 @@ def history_get(hist, nhwc=True):
     return out
 
 
-def param_names_shapes(action_size, algo='a3c', lstm=False):
+def param_names_shapes(action_size, algo='a3c', lstm=False, dqn_type='nips'):
     """TF variable names/shapes in flat order (agent.py:226-252 q-net, network.py:47-79 a3c);
-    lstm: the C5 LSTM head's gate matrix and bias appended (include/a3c_hip.h layout)."""
+    lstm: the C5 LSTM head's gate matrix and bias appended (include/a3c_hip.h layout);
+    dqn_type='nature': network.py:30-42's trunk (conv 32/64/64, fc 3136 -> 512) under A3C heads."""
     A = int(action_size)
+    if str(dqn_type).lower() == 'nature':
+        if algo != 'a3c' or lstm:
+            raise ValueError('the nature trunk belongs to the A3C Network (network.py:30-42): a3c heads, no LSTM')
+        return [('l1_w', (8, 8, 4, 32)), ('l1_b', (32,)), ('l2_w', (4, 4, 32, 64)), ('l2_b', (64,)),
+                ('l3_w', (3, 3, 64, 64)), ('l3_b', (64,)), ('l4_w', (3136, 512)), ('l4_b', (512,)),
+                ('p_w', (512, A)), ('p_b', (A,)), ('q_w', (512, 1)), ('q_b', (1,))]
+    if str(dqn_type).lower() != 'nips':
+        raise ValueError('Wrong DQN type: %s' % dqn_type)
     fc = 'l4' if algo == 'a3c' else 'l3'
     out = [('l1_w', (8, 8, 4, 16)), ('l1_b', (16,)), ('l2_w', (4, 4, 16, 32)), ('l2_b', (32,)),
            (fc + '_w', (FLAT, FC)), (fc + '_b', (FC,))]

@@ -37,6 +37,11 @@ CONV12_FWD_FLOP = 2 * 400 * 16 * 256 + 2 * 81 * 32 * 256            # 4,603,904
 CONV_BWD_FLOP = 2 * 81 * 32 * 256 * 2 + 2 * 400 * 16 * 256          # 5,931,008
 FC_FWD_FLOP = 2 * 2592 * 256                                        # 1,327,104
 ENV_STEP_BYTES = 210 * 160 * 3 + 84 * 84                            # 107,856
+# nature trunk (network.py:30-42), algorithmic FLOP per sample of each pass (nature.hip): the
+# forward passes run once per rollout step and for the bootstrap state, the backward ones once
+NAT_FLOP = {'conv1_fwd': 2 * 400 * 32 * 256, 'conv2_fwd': 2 * 81 * 64 * 512, 'conv3_fwd': 2 * 49 * 64 * 576,
+            'fc_fwd': 2 * 3136 * 512, 'conv3_dw': 2 * 49 * 64 * 576, 'conv3_dx': 2 * 49 * 64 * 576,
+            'conv2_dw': 2 * 81 * 64 * 512, 'conv2_dx': 2 * 81 * 64 * 512, 'conv1_dw': 2 * 400 * 32 * 256}
 ENV_STEP_BYTES_84 = 84 * 84 + 84 * 84                               # 14,112 (--frames84: copy)
 PEAK_FP32_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix peak (spec)
 PEAK_HBM_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
@@ -58,6 +63,9 @@ def parse():
     ap.add_argument('--host-threads', type=int, default=16)
     ap.add_argument('--host-chunks', type=int, default=2,
                     help='--env host: env ranges per rollout step; the H2D copy of one overlaps stepping the next')
+    ap.add_argument('--dqn-type', default='nips', choices=['nips', 'nature'],
+                    help="the A3C Network's trunk (network.py:30-54): nips 16/32/256 (the default, agent.py's "
+                         "Q-net trunk too) or nature 32/64/64/512 (A3C heads, feed-forward)")
     ap.add_argument('--lstm', action='store_true',
                     help='C5 LSTM policy head (BASELINE config 5: SpaceInvaders-v0, 256-cell LSTM after the fc)')
     ap.add_argument('--frames', type=int, default=16384, help='HBM frame pool (16384 = 1.65 GB > L3)')
@@ -150,7 +158,7 @@ def cgroup_cpu_quota():
     return None
 
 
-def cpu_baseline(seconds, game, algo, frame84=False):
+def cpu_baseline(seconds, game, algo, frame84=False, dqn_type='nips'):
     """The reference's ps/worker algorithm restated on the CPU (oracle/ps_worker.py: shared-memory
     PS, W worker processes with Hogwild RMSProp, one numpy thread each) on the same synthetic
     env: 1 ps / 1 worker (BASELINE config 1) and W = (the box's CPU limit) - 1 workers.  Runs
@@ -173,12 +181,12 @@ def cpu_baseline(seconds, game, algo, frame84=False):
     host['limit_used'] = limit
     host['workers'] = W
     one = ps_worker.run(seconds=seconds / 2, workers=1, envs_per_worker=8, n_step=n, action_size=A, algo=algo,
-                        start_lives=lives, frame84=frame84)
+                        start_lives=lives, frame84=frame84, dqn_type=dqn_type)
     many = ps_worker.run(seconds=seconds / 2, workers=W, envs_per_worker=8, n_step=n, action_size=A, algo=algo,
-                         start_lives=lives, frame84=frame84) if W > 1 else one
+                         start_lives=lives, frame84=frame84, dqn_type=dqn_type) if W > 1 else one
     return dict(value=round(many['value'], 2), unit='env-steps/s', cores=W, kind='port',
                 one_worker=round(one['value'], 2), host_cpu=host,
-                sample=f'oracle/ps_worker.py ({algo} ps/worker, shared-memory PS, unlocked RMSProp, numpy fp32, '
+                sample=f'oracle/ps_worker.py ({algo} {dqn_type} ps/worker, shared-memory PS, unlocked RMSProp, numpy fp32, '
                        f'8 envs x n={n} per worker{", pre-sized 84x84 frames" if frame84 else ""}): {W} workers x {many["seconds"]:.1f} s = '
                        f'{many["iterations"]} iterations; 1 ps/1 worker: {one["value"]:.1f} env-steps/s')
 
@@ -232,6 +240,38 @@ def spawn_ranks(args, cpu, cmd=None):
         os.unlink(cpu_path)
 
 
+def nature_roofline(eng, _lib, E, n, iter_ms):
+    """The nature trunk's passes (nature.hip), each timed alone with HIP events on the stream it is
+    launched on (a3c_engine_time_kernel: forward passes over E states, backward passes over the
+    last rollout's n E samples); the dominant one by time share of the iteration names the roofline
+    (MFMA-bound: algorithmic FLOP per launch / its average launch duration, against the FP32 matrix peak)."""
+    kernels = {}
+    for name, kid in _lib.KER_NAT.items():
+        ms = eng.time_kernel(kid, 10)
+        fwd = name.endswith('_fwd')
+        B = E if fwd else n * E
+        flop = NAT_FLOP[name] * B
+        per_iter = n + 1 if fwd else 1
+        kernels['nat_' + name] = dict(avg_ms=round(ms, 4), per_iter=per_iter, share=round(ms * per_iter / iter_ms, 3),
+                                      bound='mfma', achieved=round(flop / (ms * 1e-3) / 1e12, 2), unit='TFLOP/s',
+                                      flop_per_launch=flop)
+    dom = max(kernels, key=lambda k: kernels[k]['avg_ms'] * kernels[k]['per_iter'])
+    d = kernels[dom]
+    traffic = None
+    pmc = os.path.join(ROOT, 'profiles', 'pmc_hbm_bytes_nature.json')
+    if os.path.exists(pmc):
+        try:
+            t = json.load(open(pmc))['hbm_bytes_per_launch'].get(dom)
+            traffic = None if t is None else int(round(t))
+        except Exception:
+            traffic = None
+    roofline = dict(kernel=dom, bound='mfma', achieved=d['achieved'], peak=PEAK_FP32_TFLOPS, unit='TFLOP/s',
+                    frac=round(d['achieved'] / PEAK_FP32_TFLOPS, 4), traffic=traffic,
+                    timing='isolated (HIP events on the launch stream, a3c_engine_time_kernel)',
+                    avg_us=round(d['avg_ms'] * 1e3, 2), work_per_launch=d['flop_per_launch'], work_unit='FLOP')
+    return roofline, kernels
+
+
 def dist_record(args, torch, dist, local):
     """What the process group saw: backend, world size, launcher, every rank's device (index, name,
     PCI bus id) and the RCCL version torch was built against."""
@@ -271,7 +311,7 @@ def main():
         else:
             # rank 0, before any HIP initialisation (the workers are spawned processes); under a
             # launcher at N > 1 the other ranks wait in the rendezvous meanwhile
-            cpu = cpu_baseline(args.cpu_seconds, args.game, args.algo, args.frames84)
+            cpu = cpu_baseline(args.cpu_seconds, args.game, args.algo, args.frames84, args.dqn_type)
     if world == 1 and args.gpus > 1:
         sys.exit(spawn_ranks(args, cpu))
     # stdout carries exactly the one JSON line: native libraries' chatter (gloo's connection
@@ -302,6 +342,10 @@ def main():
     E, n = args.envs, args.n_step
     if args.lstm and args.algo != 'a3c':
         raise SystemExit('--lstm is an a3c head')
+    nature = args.dqn_type == 'nature'
+    if nature and (args.algo != 'a3c' or args.lstm or args.env != 'device' or args.frames84):
+        raise SystemExit('--dqn-type nature: the A3C Network trunk (network.py:30-42) -- a3c, feed-forward head, '
+                         'device envs, raw RGB frames')
     host = args.env == 'host'
     if host and args.update != 'sync':
         args.update = 'sync'              # host-stepped envs drive a synchronous engine
@@ -310,13 +354,13 @@ def main():
     eng = Engine(num_envs=E, n_step=n, action_size=A, algo=args.algo, start_lives=lives, num_frames=args.frames,
                  seed=123, env_id_base=rank * E, world_size=world, use_graph=args.graph and not args.no_graph,
                  overlap=args.update == 'overlap' or (args.update == 'hogwild' and not args.hogwild_sync),
-                 lstm=args.lstm, external_env=host, frame84=int(args.frames84))
+                 lstm=args.lstm, external_env=host, frame84=int(args.frames84), dqn_type=args.dqn_type)
     hpool = None
     if host:
         from src.host_env import SyntheticHostEnvPool
         hpool = SyntheticHostEnvPool(E, A, lives, num_frames=min(args.frames, 2048), seed=123, env_id_base=rank * E,
                                      threads=args.host_threads, upload_chunks=args.host_chunks)
-    ns = param_names_shapes(A, args.algo, lstm=args.lstm)
+    ns = param_names_shapes(A, args.algo, lstm=args.lstm, dqn_type=args.dqn_type)
     params = flatten_host(ns, eng.offsets, eng.params.numel(), init_params(ns, seed=123))
     eng.reset(params)     # every rank starts from the same parameters
     torch.cuda.synchronize()
@@ -363,7 +407,7 @@ def main():
         step()
     barrier()
     torch.cuda.synchronize()
-    live = not host and (eng.overlap or args.update == 'sync')
+    live = not host and not nature and (eng.overlap or args.update == 'sync')
     if live:                      # live launch spans of the dominant kernels, recorded in-graph
         eng.span_stats(0, reset=True)
         eng.span_stats(1, reset=True)
@@ -385,7 +429,9 @@ def main():
     finite = bool(torch.isfinite(eng.params).all().item())
 
     roofline, kernels = None, {}
-    if rank == 0 and not args.no_kernel_timing and not host:
+    if rank == 0 and not args.no_kernel_timing and nature:
+        roofline, kernels = nature_roofline(eng, _lib, E, n, el / args.steps * 1e3)
+    elif rank == 0 and not args.no_kernel_timing and not host:
         # overlap mode fuses step t+1's conv1+conv2 into step t's head+screen kernel
         # (k_head_screen_conv12, engine.hip conv_fused): conv12 then runs once per rollout
         fused = eng.overlap and os.environ.get('A3C_FUSE_CONV', '1') != '0'
@@ -486,15 +532,15 @@ def main():
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
             'data': (f'synthetic: HBM-resident hashed {"pre-sized 84x84 grey" if args.frames84 else "RGB 210x160x3"} '
                      f'frame pool ({args.frames} frames) stepped by the on-device synthetic Atari env; random-init '
-                     f'NIPS {NETNAME} conv net' if not host else
+                     f'{args.dqn_type.upper()} {NETNAME} conv net' if not host else
                      f'synthetic: host-stepped emulator ({args.host_threads} threads, a3c_hostenv) writing raw RGB '
                      f'210x160x3 frames into pinned buffers, PCIe H2D every step (PCIe-inclusive); random-init '
                      f'NIPS {NETNAME} conv net'),
             'config': {'workload': f'{args.game}, {E} envs batched per MI355X, n-step={n}, '
-                                   f'{"A3C" if args.algo == "a3c" else "one-step Q"} conv net (nips trunk'
+                                   f'{"A3C" if args.algo == "a3c" else "one-step Q"} conv net ({args.dqn_type} trunk'
                                    f'{" + 256-cell LSTM head" if args.lstm else ""})',
                        'frames': 'M2: pre-sized 84x84 (copy)' if args.frames84 else 'M1: raw RGB 210x160x3 + screen',
-                       'game': args.game, 'head': 'lstm' if args.lstm else 'feed-forward', 'env': args.env, 'envs_per_gpu': E, 'n_step': n, 'action_size': A, 'algo': args.algo,
+                       'game': args.game, 'trunk': args.dqn_type, 'head': 'lstm' if args.lstm else 'feed-forward', 'env': args.env, 'envs_per_gpu': E, 'n_step': n, 'action_size': A, 'algo': args.algo,
                        'env_steps_per_step': world * E * n,
                        'parallelism': (f'dp{world} hogwild: unlocked RMSProp pushes into {world} IPC-mapped HBM '
                                        f'shards ({dict(fine="fine-grained", coarse="coarse-grained", uncached="uncached")[args.hogwild_memory]}) '

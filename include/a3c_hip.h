@@ -34,6 +34,7 @@ extern "C" {
 #define A3C_ALGO_Q 1            /* one-step Q-learning head (src/agent.py:251-254) */
 
 #define A3C_TRUNK_NIPS 0        /* 16/32/256 trunk: agent.py:226-251, network.py:43-52 */
+#define A3C_TRUNK_NATURE 1      /* 32/64/64/512 trunk: network.py:30-42 (A3C heads only)   */
 #define A3C_LSTM_UNITS 256      /* C5 LSTM head width (build-defined: the reference has no
                                    recurrent code)                 */
 
@@ -49,13 +50,16 @@ int a3c_device_ok(void);
  * padding floats are zero and stay zero.
  *  a3c : l1_w[8,8,4,16] l1_b l2_w[4,4,16,32] l2_b l4_w[2592,256] l4_b p_w[256,A] p_b q_w[256,1] q_b
  *  q   : l1_w l1_b l2_w l2_b l3_w[2592,256] l3_b q_w[256,A] q_b
+ *  a3c, nature trunk: l1_w[8,8,4,32] l1_b l2_w[4,4,32,64] l2_b l3_w[3,3,64,64] l3_b
+ *        l4_w[3136,512] l4_b p_w[512,A] p_b q_w[512,1] q_b   (network.py:30-42, 62-79)
  *  a3c + LSTM head (lstm_units = 256, BASELINE config 5): the a3c list, then
  *        lstm_w[256+U, 4U] lstm_b[4U]   (TF1 BasicLSTMCell "Matrix"/"Bias", gate columns
  *        i, j, f, o, forget_bias 1.0); the policy / value heads read the LSTM's h.
  * -------------------------------------------------------------------------- */
 typedef struct a3c_net_desc {
   int algo;            /* A3C_ALGO_*                                       */
-  int trunk;           /* A3C_TRUNK_NIPS                                   */
+  int trunk;           /* A3C_TRUNK_NIPS, or A3C_TRUNK_NATURE (algo A3C, no LSTM: the
+                          engine only; the per-op a3c_forward / a3c_loss_backward are NIPS) */
   int action_size;     /* A (<= 31)                                        */
   int history_length;  /* 4 (config.py:22)                                 */
   int screen_h;        /* 84                                               */
@@ -458,6 +462,11 @@ typedef struct a3c_engine_buffers {
    * inputs hp, cp [n][E][U]; activated gates [n][E][4U].  NULL without the LSTM head. */
   float* lstm_h; float* lstm_c; float* lstm_hp; float* lstm_cp; float* lstm_gates;
   int lstm_units;
+  /* nature trunk (net.trunk = A3C_TRUNK_NATURE): act_l1 [n*E][20][20][32], act_l2 [n*E][9][9][64],
+   * act_l3 [n*E][3136] (the conv3 output, (h,w,c)-flattened), act_l4 [n*E][512] (fc out);
+   * NIPS: act_l4 NULL */
+  float* act_l4;
+  int trunk;
 } a3c_engine_buffers;
 int a3c_engine_get_buffers(a3c_engine* eng, a3c_engine_buffers* out);
 /* same, with the rollout buffers (actions .. act_l3) of slot 0 or 1 (overlap: rollout k
@@ -474,6 +483,17 @@ int a3c_engine_slot_buffers(a3c_engine* eng, int slot, a3c_engine_buffers* out);
 #define A3C_KER_HEAD_SCREEN 4  /* fused head + action draw + Environment.screen, B = E    */
 #define A3C_KER_HEAD_SCREEN_CONV12 5  /* ... + conv1+conv2 of the next states (overlap mode) */
 #define A3C_KER_FC_PART 6      /* fc as K-slice partials (overlap mode; the head folds them)  */
+/* nature trunk engines (nature.hip k_nat_gemm passes): forward over E states of the live
+ * parameters, backward passes over the n*E samples of the last back-propagated rollout */
+#define A3C_KER_NAT_C1F 7      /* conv1 8x8/4 4->32 forward (u8 ring -> l1), B = E         */
+#define A3C_KER_NAT_C2F 8      /* conv2 4x4/2 32->64 forward                               */
+#define A3C_KER_NAT_C3F 9      /* conv3 3x3/1 64->64 forward                               */
+#define A3C_KER_NAT_FCF 10     /* fc 3136->512 forward (split-K GEMM + bias/ReLU fold)      */
+#define A3C_KER_NAT_C3W 11     /* conv3 weight gradient (slabs), B = n*E                  */
+#define A3C_KER_NAT_C3X 12     /* conv3 input gradient dl2                                 */
+#define A3C_KER_NAT_C2W 13     /* conv2 weight gradient                                    */
+#define A3C_KER_NAT_C2X 14     /* conv2 input gradient dl1 (4 stride-parity classes)       */
+#define A3C_KER_NAT_C1W 15     /* conv1 weight gradient from the u8 planes                 */
 /* Live launch spans, recorded by the kernels themselves inside the engine's graphs (which 0:
  * k_conv_bwd, 1: k_head_screen_conv12): per launch, last workgroup end - first workgroup start
  * (s_memrealtime).  reset = 1 clears the records (before a timed region); otherwise returns the

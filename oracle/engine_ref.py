@@ -24,7 +24,7 @@ class EngineRef:
                  gamma=0.99, beta=0.01, learning_rate=0.0007, max_step=80_000_000, decay=0.99,
                  momentum=0.0, epsilon=0.1, clip_norm=40.0, literal_adv=False, ep_start=1.0,
                  ep_end_t=4_000_000, learn_start=32, target_q_update_step=40_000, discount=0.99,
-                 dtype=np.float64, lstm=False, frame84=False, double_q=False):
+                 dtype=np.float64, lstm=False, frame84=False, double_q=False, dqn_type='nips'):
         self.algo, self.A, self.E, self.n = algo, int(action_size), int(num_envs), int(n_step)
         self.seed = int(seed)
         self.k0, self.k1 = px.seed_key(seed)
@@ -48,6 +48,9 @@ class EngineRef:
                       target_q_update_step=target_q_update_step, discount=discount)
         self.dtype = dtype
         self.double_q = bool(double_q)     # agent.py:176-184 (q only)
+        self.dqn_type = str(dqn_type).lower()   # network.py:30-54 trunk: 'nips' or 'nature' (a3c heads)
+        if self.dqn_type == 'nature' and (algo != 'a3c' or lstm):
+            raise ValueError('the nature trunk is an A3C Network trunk (network.py:30-42)')
         if self.double_q and algo != 'q':
             raise ValueError('double_q is a Q-learning option')
         # C5 LSTM head (ref_cpu.lstm_*): recurrent state carried across iterations, zeroed after a
@@ -89,7 +92,7 @@ class EngineRef:
     def _step_z(self, st, carry):
         """per-step forward: z [E, zs] (and the LSTM head's new state when lstm)."""
         if not self.lstm:
-            return R.forward(self.params, st, self.algo, dtype=self.dtype, keep=False)['z'], None
+            return R.forward(self.params, st, self.algo, self.dqn_type, dtype=self.dtype, keep=False)['z'], None
         P, dt = self.params, self.dtype
         h3 = R.forward(P, st, 'a3c', dtype=dt, keep=False)['h3']
         h, c, _ = R.lstm_cell(h3, carry[0], carry[1], P['lstm_w'], P['lstm_b'])
@@ -198,7 +201,7 @@ class EngineRef:
             fwd = R.lstm_a3c_forward(self.params, states, n, h0c0[0], h0c0[1], terms, dtype=self.dtype)
             out['lstm'] = fwd['lstm']
         else:
-            fwd = R.forward(self.params, states, self.algo, dtype=self.dtype)
+            fwd = R.forward(self.params, states, self.algo, self.dqn_type, dtype=self.dtype)
         flat_acts = acts.reshape(-1)
         if self.algo == 'a3c':
             losses, dz = R.a3c_loss_and_dz(fwd['z'], flat_acts, target.reshape(-1).astype(self.dtype),
@@ -212,7 +215,7 @@ class EngineRef:
         if self.lstm:
             g = R.lstm_a3c_backward(self.params, fwd, dz, terms)
         else:
-            g = R.backward(self.params, fwd, dz, self.algo)
+            g = R.backward(self.params, fwd, dz, self.algo, self.dqn_type)
         grads = {k: np.asarray(v, np.float32).reshape(self.params[k].shape) for k, v in g.items()}
         sumsq = {k: np.float32(np.sum(v.astype(np.float64) ** 2)) for k, v in grads.items()}
         clipped = {k: R.clip_by_norm(v, h['clip_norm']) for k, v in grads.items()}

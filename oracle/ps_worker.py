@@ -23,13 +23,13 @@ import time
 import numpy as np
 
 
-def _names_shapes(A, algo):
+def _names_shapes(A, algo, dqn_type='nips'):
     from . import ref_cpu as R
-    return R.param_shapes(A, algo)
+    return R.param_shapes(A, algo, dqn_type)
 
 
 def _worker(wid, E, n, A, algo, lives, seed, seconds, shm_name, layout, start_evt, out_q, frame84=False,
-            ready_q=None):
+            ready_q=None, dqn_type='nips'):
     os.environ['OMP_NUM_THREADS'] = '1'
     os.environ['OPENBLAS_NUM_THREADS'] = '1'
     os.environ['MKL_NUM_THREADS'] = '1'
@@ -51,7 +51,7 @@ def _worker(wid, E, n, A, algo, lives, seed, seconds, shm_name, layout, start_ev
 
     shared_p, shared_ms, shared_mom = views(P), views(MS), views(MOM)
     ref = EngineRef({k: v.copy() for k, v in shared_p.items()}, E, n, A, algo, lives, num_frames=16384,
-                    seed=seed, env_id_base=wid * E, dtype=np.float32, frame84=frame84)
+                    seed=seed, env_id_base=wid * E, dtype=np.float32, frame84=frame84, dqn_type=dqn_type)
     ref.cache_screens = False
     ref.reset()
     if ready_q is not None:
@@ -77,11 +77,11 @@ def _worker(wid, E, n, A, algo, lives, seed, seconds, shm_name, layout, start_ev
 
 
 def run(seconds=12.0, workers=1, envs_per_worker=8, n_step=5, action_size=6, algo='a3c', start_lives=0,
-        seed=123, frame84=False):
+        seed=123, frame84=False, dqn_type='nips'):
     """Returns dict(value=env-steps/s over all workers, cores, iterations)."""
     from multiprocessing import shared_memory
     from . import ref_cpu as R
-    ns = _names_shapes(action_size, algo)
+    ns = _names_shapes(action_size, algo, dqn_type)
     params = R.init_params(ns, seed=seed)
     layout = {'t': {}}
     off = 0
@@ -104,7 +104,7 @@ def run(seconds=12.0, workers=1, envs_per_worker=8, n_step=5, action_size=6, alg
         ready_q = ctx.Queue()
         procs = [ctx.Process(target=_worker, args=(w, envs_per_worker, n_step, action_size, algo, start_lives,
                                                    seed, seconds, shm.name, layout, start_evt, out_q, frame84,
-                                                   ready_q))
+                                                   ready_q, dqn_type))
                  for w in range(workers)]
         for p in procs:
             p.start()

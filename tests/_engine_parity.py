@@ -25,7 +25,8 @@ def rel_l2(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
 
 
-REF_KEYS = ('target_q_update_step', 'learning_rate', 'frame84', 'double_q', 'ep_start', 'ep_end_t', 'learn_start')
+REF_KEYS = ('target_q_update_step', 'learning_rate', 'frame84', 'double_q', 'ep_start', 'ep_end_t', 'learn_start',
+            'dqn_type')
 
 
 def build(algo, A, E, n, lives, seed, frames=48, use_graph=False, scale=4.0, **kw):
@@ -37,7 +38,7 @@ def build(algo, A, E, n, lives, seed, frames=48, use_graph=False, scale=4.0, **k
     eng_frames = 1 if kw.get('external_env') else frames
     eng = Engine(num_envs=E, n_step=n, action_size=A, algo=algo, start_lives=lives, num_frames=eng_frames, seed=seed,
                  use_graph=use_graph, **kw)
-    ns = param_names_shapes(A, algo)
+    ns = param_names_shapes(A, algo, dqn_type=kw.get('dqn_type', 'nips'))
     p = init_params(ns, seed=seed, stddev=0.02 * scale)
     eng.reset(flatten_host(ns, eng.offsets, eng.params.numel(), p))
     ref = EngineRef(p, E, n, A, algo, lives, frames, seed, **{k: v for k, v in kw.items() if k in REF_KEYS})
@@ -54,20 +55,29 @@ def same_act_grads(slot, planes, P, algo, A, n, E, tgt):
     """oracle loss + backward of one rollout on the engine's saved activations of that rollout
     (slot: Engine.slot(k), or the engine itself in sync mode)."""
     g = (lambda k: slot[k]) if isinstance(slot, dict) else (lambda k: getattr(slot, k))
+    nature = ('act_l4' in slot) if isinstance(slot, dict) else getattr(slot, 'dqn_type', 'nips') == 'nature'
     B = n * E
-    l1 = g('act_l1').cpu().numpy().astype(np.float64).reshape(B, 20, 20, 16)
-    l2 = g('act_l2').cpu().numpy().astype(np.float64)
     zw = A + 1 if algo == 'a3c' else A
     z = g('z').cpu().numpy()[:n].reshape(B, -1)[:, :zw].astype(np.float64)
-    fwd = dict(z=z, h3=g('act_l3').cpu().numpy().astype(np.float64), flat=l2,
-               acts=[Rc.states_nhwc(planes).astype(np.float64) / 255.0, l1, l2.reshape(B, 9, 9, 32)])
+    x0 = Rc.states_nhwc(planes).astype(np.float64) / 255.0
+    if nature:      # network.py:30-42: conv 32 / 64 / 64 (NHWC), flat 3136, fc 512
+        l1 = g('act_l1').cpu().numpy().astype(np.float64).reshape(B, 20, 20, 32)
+        l2 = g('act_l2').cpu().numpy().astype(np.float64).reshape(B, 9, 9, 64)
+        l3 = g('act_l3').cpu().numpy().astype(np.float64)
+        fwd = dict(z=z, h3=g('act_l4').cpu().numpy().astype(np.float64), flat=l3,
+                   acts=[x0, l1, l2, l3.reshape(B, 7, 7, 64)])
+    else:
+        l1 = g('act_l1').cpu().numpy().astype(np.float64).reshape(B, 20, 20, 16)
+        l2 = g('act_l2').cpu().numpy().astype(np.float64)
+        fwd = dict(z=z, h3=g('act_l3').cpu().numpy().astype(np.float64), flat=l2,
+                   acts=[x0, l1, l2.reshape(B, 9, 9, 32)])
     acts = g('actions').cpu().numpy().reshape(-1)
     if algo == 'a3c':
         losses, dz = Rc.a3c_loss_and_dz(z, acts, tgt.reshape(-1).astype(np.float64), 0.01)
     else:
         loss, dz = Rc.q_loss_and_dz(z, acts, tgt.reshape(-1).astype(np.float64))
         losses = dict(loss=loss)
-    gr = Rc.backward(P, fwd, dz, algo)
+    gr = Rc.backward(P, fwd, dz, algo, 'nature' if nature else 'nips')
     return losses, {k: np.asarray(v, np.float32).reshape(P[k].shape) for k, v in gr.items()}
 
 

@@ -23,8 +23,9 @@ STATE_NAMES = ('params', 'target_params', 'ms', 'mom', 'frame_ring', 'counters',
 
 MODES = [dict(algo='a3c', A=6, lives=0), dict(algo='a3c', A=6, lives=0, overlap=True),
          dict(algo='q', A=6, lives=3, n=8), dict(algo='a3c', A=4, lives=5, overlap=True, frame84=1),
-         dict(algo='a3c', A=6, lives=3, lstm=True), dict(algo='a3c', A=6, lives=3, lstm=True, overlap=True)]
-IDS = ['sync', 'overlap', 'q', 'overlap-m2-breakout', 'lstm-sync', 'lstm-overlap']
+         dict(algo='a3c', A=6, lives=3, lstm=True), dict(algo='a3c', A=6, lives=3, lstm=True, overlap=True),
+         dict(algo='a3c', A=6, lives=0, dqn_type='nature'), dict(algo='a3c', A=4, lives=5, overlap=True, dqn_type='nature')]
+IDS = ['sync', 'overlap', 'q', 'overlap-m2-breakout', 'lstm-sync', 'lstm-overlap', 'nature-sync', 'nature-overlap']
 
 
 def _make(mode, seed=61):
@@ -59,7 +60,11 @@ def test_resume_is_bit_continuous(mode, tmp_path):
     step = C.save_engine(saver, b, ns)
     assert saver.latest().endswith('model.ckpt-%d.npz' % step)
     arrays = C.load(saver.latest())
-    want = ['step'] + [C.tf_name(nm, b.algo) for nm, _ in ns] + [C.slot_names(C.tf_name(nm, b.algo))[1] for nm, _ in ns]
+    dqn = mode.get('dqn_type', 'nips')          # nature: the Nature_DQN/ scope of network.py:31
+    want = ['step'] + [C.tf_name(nm, b.algo, dqn) for nm, _ in ns] + \
+        [C.slot_names(C.tf_name(nm, b.algo, dqn))[1] for nm, _ in ns]
+    if dqn == 'nature':
+        assert 'Nature_DQN/l3_conv/w' in arrays and 'policy/linear/Matrix' in arrays
     assert all(w in arrays for w in want), [w for w in want if w not in arrays]
     del b
     with pytest.raises(RuntimeError):           # the state is tied to its env shard and seed

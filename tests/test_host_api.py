@@ -97,10 +97,12 @@ def test_network_value_errors_before_device():
     (['--lstm', 'true'], dict(lstm=True)),
     (['--algo', 'q', '--double_q', 'true'], dict(lstm=False, double_q=True)),
     (['--algo', 'q'], dict(lstm=False)),
+    (['--dqn_type', 'nature'], dict(lstm=False, dqn_type='nature')),
 ])
 def test_engine_mode_honours_reference_options(argv, want):
     """main.py --mode engine passes every reference option it supports into the Engine config:
-    --lstm (config 5), --double_q (agent.py:176-184, implemented in the engine's TD target)."""
+    --lstm (config 5), --double_q (agent.py:176-184, implemented in the engine's TD target), --dqn_type
+    nature (network.py:30-42, nature.hip)."""
     import main
     assert main.engine_options(main.parse_flags(['--mode', 'engine'] + argv)) == want
 
@@ -108,7 +110,8 @@ def test_engine_mode_honours_reference_options(argv, want):
 @pytest.mark.parametrize('argv,match', [
     (['--dueling', 'true'], 'dueling'),
     (['--algo', 'q', '--dueling', 'true'], 'dueling'),
-    (['--dqn_type', 'nature'], 'nature'),
+    (['--dqn_type', 'nature', '--algo', 'q'], 'nature'),
+    (['--dqn_type', 'nature', '--lstm', 'true'], 'nature'),
     (['--double_q', 'true'], 'Q-learning option'),
     (['--algo', 'q', '--lstm', 'true'], 'A3C policy head'),
 ])
