@@ -27,17 +27,13 @@
 
 enum { NG_FWD1 = 0, NG_FWD, NG_DX, NG_DW1, NG_DW };
 
-struct NatConv {
-  int H, W, C, KH, KW, S, OH, OW, OC;
-};
-static NatConv nat_conv(int l) {
-  if (l == 1) return {IMG, IMG, HIST, 8, 8, 4, NT1_O, NT1_O, NT1_N};
-  if (l == 2) return {NT1_O, NT1_O, NT1_N, 4, 4, 2, NT2_O, NT2_O, NT2_N};
-  return {NT2_O, NT2_O, NT2_N, 3, 3, 1, NT3_O, NT3_O, NT3_N};
-}
+// conv layer geometry (NHWC input H x W x C, TF weights [KH][KW][C][OC], VALID, stride S)
+template <int LAYER> struct NG;
+template <> struct NG<1> { static constexpr int H = IMG, W = IMG, C = HIST, KH = 8, KW = 8, S = 4, OH = NT1_O, OW = NT1_O, OC = NT1_N; };
+template <> struct NG<2> { static constexpr int H = NT1_O, W = NT1_O, C = NT1_N, KH = 4, KW = 4, S = 2, OH = NT2_O, OW = NT2_O, OC = NT2_N; };
+template <> struct NG<3> { static constexpr int H = NT2_O, W = NT2_O, C = NT2_N, KH = 3, KW = 3, S = 1, OH = NT3_O, OW = NT3_O, OC = NT3_N; };
 
 struct NatGemm {
-  NatConv g;
   StateAddr sa;        // NG_FWD1 / NG_DW1: the u8 state planes of sample b (b = t E + e)
   const float* X;      // fp32 NHWC input activation [B][H][W][C] (NG_FWD, NG_DW; NG_DX: its ReLU mask)
   const float* Wt;     // TF weights [KH][KW][C][OC]
@@ -47,46 +43,77 @@ struct NatGemm {
   float* slab;         // NG_DW*: [nsplit][M][N]
   float* colsum;       // NG_DW*: [nsplit][N]
   int M, N, K;         // NG_DX: M per parity class; NG_DW*: M = KH KW C, N = OC, K = B OH OW (reduction)
-  int kchunk;          // NG_DW*: reduction rows per split (a multiple of 16)
+  int kchunk;          // NG_DW*: reduction rows per split (a multiple of the K slice); NG_FWD: > 0 splits K
+                       // over grid z into slab partials (the fold applies bias + ReLU)
   float scale;         // NG_FWD1: 1/255
 };
 
-template <int MODE, int BN>
+// the frame-ring planes of sample b = t E + e without 64-bit divisions: slot0 = the ring slot of
+// plane 0 of t = 0, reduced once per launch
+struct RingRows {
+  const uint8_t* base;
+  int64_t env_stride, plane_bytes;
+  int E, R, slot0;
+  uint64_t emagic;     // ceil(2^40 / E): t = b E^-1 by a multiply (b E < 2^40)
+  __device__ void init(const StateAddr& sa, int64_t tau0) {
+    base = sa.base; env_stride = sa.env_stride; plane_bytes = sa.plane_bytes; E = sa.E; R = sa.R;
+    emagic = ((1ull << 40) + (uint64_t)E - 1) / (uint64_t)E;
+    int64_t s0 = (tau0 + sa.tau_offset - (sa.L - 1)) % sa.R;
+    slot0 = (int)(s0 < 0 ? s0 + sa.R : s0);
+  }
+  __device__ int step_of(int b) const { return (int)(((uint64_t)b * emagic) >> 40); }
+  __device__ const uint8_t* plane(int e, int t, int c) const {
+    int s = slot0 + t + c;
+    while (s >= R) s -= R;
+    return base + e * env_stride + s * plane_bytes;
+  }
+};
+
+// One tile of an implicit GEMM on v_mfma_f32_32x32x2f32: 32-deep K slices, double-buffered in LDS
+// (one barrier per slice), the next slice's operands loaded into registers under the current
+// slice's 16 MFMAs per wave.  Geometry at compile time (every index division by a constant).
+template <int MODE, int LAYER, int BN>
 __global__ void __launch_bounds__(256) k_nat_gemm(NatGemm a) {
-  constexpr int BM = 4096 / BN, BK = 16, LP = 4;
+  using G = NG<LAYER>;
+  constexpr int BM = 4096 / BN, BK = 32, LP = 4;
   constexpr int WN = BN / 32;                                   // waves along n
   constexpr bool A_KC = MODE == NG_FWD1 || MODE == NG_FWD || MODE == NG_DX;   // A quads along k
   constexpr bool B_NC = MODE != NG_DX;                           // B quads along n
   constexpr bool DW = MODE == NG_DW || MODE == NG_DW1;
   constexpr bool U8 = MODE == NG_FWD1 || MODE == NG_DW1;
-  constexpr int AQ = BM * BK / 4 / 256;                          // A quads per thread (1 or 2)
-  constexpr int NBQ = BN * BK / 4;                               // B quads per tile (256 or 128)
-  __shared__ __attribute__((aligned(16))) float As[BK][BM + LP];
-  __shared__ __attribute__((aligned(16))) float Bs[BK][BN + LP];
-  const NatConv g = a.g;
+  constexpr int AQ = BM * BK / 4 / 256;                          // A quads per thread (2 or 4)
+  constexpr int BQ = BN * BK / 4 / 256;                          // B quads per thread (2 or 1)
+  constexpr int P = G::OH * G::OW;
+  constexpr int TW = G::KW / G::S;                               // NG_DX taps per class along x
+  constexpr int NI = G::H / G::S, NJ = G::W / G::S;              // NG_DX class grid
+  static_assert(MODE != NG_DX || (G::H % G::S == 0 && G::KH % G::S == 0), "parity classes");
+  static_assert(!U8 || G::C == 4, "u8 planes: the 4 history frames");
+  static_assert(P > BK, "one sample wrap per slice");
+  __shared__ __attribute__((aligned(16))) float As[2][BK][BM + LP];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + LP];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int kbeg = DW ? (int)blockIdx.z * a.kchunk : 0;
-  const int kend = DW ? min(a.K, kbeg + a.kchunk) : a.K;
-  const int py = MODE == NG_DX ? (int)blockIdx.z / g.S : 0, px = MODE == NG_DX ? (int)blockIdx.z % g.S : 0;
-  const int NI = (g.H - py + g.S - 1) / g.S, NJ = (g.W - px + g.S - 1) / g.S;   // (NG_DX: the class grid)
-  const int P = g.OH * g.OW;
-  const int64_t tau0 = U8 && a.sa.tau_ptr ? *a.sa.tau_ptr : 0;
+  const bool split = DW || (MODE == NG_FWD && a.kchunk > 0);
+  const int kbeg = split ? (int)blockIdx.z * a.kchunk : 0;
+  const int kend = split ? min(a.K, kbeg + a.kchunk) : a.K;
+  const int py = MODE == NG_DX ? (int)blockIdx.z / G::S : 0, px = MODE == NG_DX ? (int)blockIdx.z % G::S : 0;
+  RingRows ring;
+  if constexpr (U8) ring.init(a.sa, a.sa.tau_ptr ? *a.sa.tau_ptr : 0);
 
-  // ---- per-thread operand coordinates (fixed over the K loop) ----
-  int ar[AQ], ac[AQ];          // A_KC: row m (tile-local), k offset; else: k row, m offset
+  // ---- per-thread operand coordinates ----
+  int ar[AQ], ac[AQ];          // A_KC: row m (tile-local), k offset; else: reduction row, m offset
+  bool aval[AQ];
   int64_t abase[AQ];           // NG_FWD: X offset of the patch origin; NG_DX: sample b
   int ai[AQ], aj[AQ];          // NG_DX: class grid position; NG_FWD1: pixel origin (y0, x0)
-  const uint8_t* apl[AQ][4];   // NG_FWD1: the sample's 4 planes
-  bool aval[AQ];
+  const uint8_t* apl[AQ][4];   // NG_FWD1: the sample's 4 planes (ring slots wrap: no common stride)
   int mk[AQ][3];               // DW: (kh, kw, c0) of the thread's m quad
 #pragma unroll
   for (int i = 0; i < AQ; ++i) {
     const int q = tid + 256 * i;
-    if constexpr (A_KC) { ar[i] = q >> 2; ac[i] = (q & 3) * 4; }
+    if constexpr (A_KC) { ar[i] = q >> 3; ac[i] = (q & 7) * 4; }
     else { ar[i] = q / (BM / 4); ac[i] = (q % (BM / 4)) * 4; }
-    aval[i] = false; abase[i] = 0; ai[i] = aj[i] = 0;
+    abase[i] = 0; ai[i] = aj[i] = 0;
     if constexpr (A_KC) {
       const int m = m0 + ar[i];
       aval[i] = m < a.M;
@@ -95,122 +122,169 @@ __global__ void __launch_bounds__(256) k_nat_gemm(NatGemm a) {
         const int b = mm / (NI * NJ), r = mm - b * (NI * NJ);
         abase[i] = b; ai[i] = r / NJ; aj[i] = r - (r / NJ) * NJ;
       } else {
-        const int b = mm / P, pos = mm - b * P, oy = pos / g.OW, ox = pos - oy * g.OW;
+        const int b = mm / P, pos = mm - b * P, oy = pos / G::OW, ox = pos - oy * G::OW;
         if constexpr (MODE == NG_FWD1) {
+          const int t = b / ring.E, e = b - t * ring.E;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) apl[i][c] = state_plane(a.sa, b, c, tau0);
-          ai[i] = oy * g.S; aj[i] = ox * g.S;
+          for (int cc = 0; cc < 4; ++cc) apl[i][cc] = ring.plane(e, t, cc);
+          ai[i] = oy * G::S; aj[i] = ox * G::S;
         } else {
-          abase[i] = (((int64_t)b * g.H + oy * g.S) * g.W + ox * g.S) * g.C;
+          abase[i] = (((int64_t)b * G::H + oy * G::S) * G::W + ox * G::S) * G::C;
         }
       }
     } else {
-      const int m = m0 + ac[i];                                  // TF order k = (kh KW + kw) C + c
+      const int m = m0 + ac[i];
       aval[i] = m < a.M;
       const int mm = aval[i] ? m : 0;
-      mk[i][0] = mm / (g.KW * g.C);
-      mk[i][1] = (mm / g.C) % g.KW;
-      mk[i][2] = mm % g.C;
+      if constexpr (U8) {                  // conv1: m = (cin, kh, kw), a quad = kw 4j..4j+3 of plane cin
+        mk[i][0] = (mm >> 3) & 7; mk[i][1] = mm & 7; mk[i][2] = mm >> 6;
+      } else {                             // TF order m = (kh KW + kw) C + c, a quad = 4 channels
+        mk[i][0] = mm / (G::KW * G::C);
+        mk[i][1] = (mm / G::C) % G::KW;
+        mk[i][2] = mm % G::C;
+      }
     }
   }
-  const bool bthr = tid < NBQ;
-  int br, bc;                  // B_NC: k row, n offset; else: n row, k offset
-  if constexpr (B_NC) { br = tid / (BN / 4); bc = (tid % (BN / 4)) * 4; }
-  else { br = tid >> 2; bc = (tid & 3) * 4; }
-  const int TW = g.KW / g.S;   // NG_DX taps per class along x
+  int br[BQ], bc[BQ];          // B_NC: k row, n offset; else: n row, k offset
+#pragma unroll
+  for (int j = 0; j < BQ; ++j) {
+    const int q = tid + 256 * j;
+    if constexpr (B_NC) { br[j] = q / (BN / 4); bc[j] = (q % (BN / 4)) * 4; }
+    else { br[j] = q >> 3; bc[j] = (q & 7) * 4; }
+  }
 
+  // A quad i of the slice at k0
   auto load_a = [&](int i, int k0) -> f32x4 {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if constexpr (A_KC) {
       const int k = k0 + ac[i];
       if (!aval[i] || k >= kend) return v;
-      if constexpr (MODE == NG_FWD1) {                            // k = (kh 8 + kw) 4 + c: the 4 planes
-        const int kh = k >> 5, kw = (k >> 2) & 7;
-        const int off = (ai[i] + kh) * IMG + aj[i] + kw;
-        v[0] = (float)apl[i][0][off]; v[1] = (float)apl[i][1][off];
-        v[2] = (float)apl[i][2][off]; v[3] = (float)apl[i][3][off];
+      if constexpr (MODE == NG_FWD1) {     // conv1's K order (cin, kh, kw): kw 4j..4j+3 of one plane, one dword
+        const int cc = k >> 6, kh = (k >> 3) & 7, kw = k & 7;
+        const uint32_t d = *(const uint32_t*)(apl[i][cc] + (ai[i] + kh) * IMG + aj[i] + kw);
+        v[0] = (float)(d & 255u); v[1] = (float)((d >> 8) & 255u); v[2] = (float)((d >> 16) & 255u); v[3] = (float)(d >> 24);
       } else if constexpr (MODE == NG_FWD) {
-        const int kh = k / (g.KW * g.C), rem = k - kh * g.KW * g.C, kw = rem / g.C, c0 = rem - kw * g.C;
-        v = *(const f32x4*)(a.X + abase[i] + ((int64_t)kh * g.W + kw) * g.C + c0);
+        const int kh = k / (G::KW * G::C), rem = k - kh * (G::KW * G::C), kw = rem / G::C, c0 = rem - kw * G::C;
+        v = *(const f32x4*)(a.X + abase[i] + (kh * G::W + kw) * G::C + c0);
       } else {                                                     // NG_DX: k = (th TW + tw) OC + oc
-        const int th = k / (TW * g.OC), rem = k - th * TW * g.OC, tw = rem / g.OC, oc0 = rem - tw * g.OC;
+        const int th = k / (TW * G::OC), rem = k - th * (TW * G::OC), tw = rem / G::OC, oc0 = rem - tw * G::OC;
         const int oy = ai[i] - th, ox = aj[i] - tw;
-        if (oy >= 0 && oy < g.OH && ox >= 0 && ox < g.OW)
-          v = *(const f32x4*)(a.dY + ((abase[i] * g.OH + oy) * g.OW + ox) * g.OC + oc0);
+        if (oy >= 0 && oy < G::OH && ox >= 0 && ox < G::OW)
+          v = *(const f32x4*)(a.dY + ((abase[i] * G::OH + oy) * G::OW + ox) * G::OC + oc0);
       }
     } else {                                                       // DW: reduction row r, m quad
       const int r = k0 + ar[i];
       if (!aval[i] || r >= kend) return v;
-      const int b = r / P, pos = r - b * P, oy = pos / g.OW, ox = pos - oy * g.OW;
-      const int y = oy * g.S + mk[i][0], x = ox * g.S + mk[i][1];
+      const int b = r / P, pos = r - b * P, oy = pos / G::OW, ox = pos - oy * G::OW;
+      const int y = oy * G::S + mk[i][0], x = ox * G::S + mk[i][1];
       if constexpr (MODE == NG_DW1) {
-        const int off = y * IMG + x;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = (float)state_plane(a.sa, b, c, tau0)[off];
+        const int t = ring.step_of(b);
+        const uint32_t d = *(const uint32_t*)(ring.plane(b - t * ring.E, t, mk[i][2]) + y * IMG + x);
+        v[0] = (float)(d & 255u); v[1] = (float)((d >> 8) & 255u); v[2] = (float)((d >> 16) & 255u); v[3] = (float)(d >> 24);
       } else {
-        v = *(const f32x4*)(a.X + (((int64_t)b * g.H + y) * g.W + x) * g.C + mk[i][2]);
+        v = *(const f32x4*)(a.X + (((int64_t)b * G::H + y) * G::W + x) * G::C + mk[i][2]);
       }
     }
     return v;
   };
-  auto load_b = [&](int k0) -> f32x4 {
+  auto load_b = [&](int j, int k0) -> f32x4 {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (!bthr) return v;
     if constexpr (B_NC) {
-      const int k = k0 + br, n = n0 + bc;
+      const int k = k0 + br[j], n = n0 + bc[j];
       if (k >= kend || n >= a.N) return v;
-      v = DW ? *(const f32x4*)(a.dY + (int64_t)k * g.OC + n) : *(const f32x4*)(a.Wt + (int64_t)k * g.OC + n);
+      const int row = MODE == NG_FWD1 ? ((((k >> 3) & 7) * 8 + (k & 7)) * 4 + (k >> 6)) : k;   // conv1: TF row of k
+      v = DW ? *(const f32x4*)(a.dY + (int64_t)k * G::OC + n) : *(const f32x4*)(a.Wt + (int64_t)row * G::OC + n);
     } else {                                                       // NG_DX: B(k, c) = W[kh][kw][c][oc..]
-      const int n = n0 + br, k = k0 + bc;
+      const int n = n0 + br[j], k = k0 + bc[j];
       if (n >= a.N || k >= kend) return v;
-      const int th = k / (TW * g.OC), rem = k - th * TW * g.OC, tw = rem / g.OC, oc0 = rem - tw * g.OC;
-      const int kh = py + g.S * th, kw = px + g.S * tw;
-      v = *(const f32x4*)(a.Wt + (((int64_t)kh * g.KW + kw) * g.C + n) * g.OC + oc0);
+      const int th = k / (TW * G::OC), rem = k - th * (TW * G::OC), tw = rem / G::OC, oc0 = rem - tw * G::OC;
+      const int kh = py + G::S * th, kw = px + G::S * tw;
+      v = *(const f32x4*)(a.Wt + (((int64_t)kh * G::KW + kw) * G::C + n) * G::OC + oc0);
     }
     return v;
+  };
+  auto store = [&](int buf, const f32x4 (&ra)[AQ], const f32x4 (&rbv)[BQ]) {
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) {
+      if constexpr (A_KC) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) As[buf][ac[i] + c][ar[i]] = ra[i][c];
+      } else {
+        *(f32x4*)&As[buf][ar[i]][ac[i]] = ra[i];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BQ; ++j) {
+      if constexpr (B_NC) {
+        *(f32x4*)&Bs[buf][br[j]][bc[j]] = rbv[j];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) Bs[buf][bc[j] + c][br[j]] = rbv[j][c];
+      }
+    }
   };
 
   f32x16 acc = {};
   float csum = 0.f;
   const bool do_colsum = DW && a.colsum && blockIdx.y == 0 && tid < BN;
-  f32x4 ra[AQ], rb;
+  const int kh = lane >> 5, c = lane & 31;
+  auto load_all = [&](int k0, f32x4 (&ra)[AQ], f32x4 (&rbv)[BQ]) {
 #pragma unroll
-  for (int i = 0; i < AQ; ++i) ra[i] = load_a(i, kbeg);
-  rb = load_b(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    __syncthreads();
+    for (int i = 0; i < AQ; ++i) ra[i] = load_a(i, k0);
 #pragma unroll
-    for (int i = 0; i < AQ; ++i) {
-      if constexpr (A_KC) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) As[ac[i] + c][ar[i]] = ra[i][c];
-      } else {
-        *(f32x4*)&As[ar[i]][ac[i]] = ra[i];
-      }
-    }
-    if (bthr) {
-      if constexpr (B_NC) {
-        *(f32x4*)&Bs[br][bc] = rb;
-      } else {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) Bs[bc + c][br] = rb[c];
-      }
-    }
-    __syncthreads();
-    if (k0 + BK < kend) {
-#pragma unroll
-      for (int i = 0; i < AQ; ++i) ra[i] = load_a(i, k0 + BK);
-      rb = load_b(k0 + BK);
-    }
+    for (int j = 0; j < BQ; ++j) rbv[j] = load_b(j, k0);
+  };
+  auto compute = [&](int buf) {
     if (do_colsum) {
 #pragma unroll
-      for (int k = 0; k < BK; ++k) csum += Bs[k][tid];
+      for (int k = 0; k < BK; ++k) csum += Bs[buf][k][tid];
     }
-    const int kh = lane >> 5, c = lane & 31;
 #pragma unroll
     for (int kk = 0; kk < BK / 2; ++kk)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[2 * kk + kh][wm * 32 + c], Bs[2 * kk + kh][wn * 32 + c], acc, 0,
-                                                 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[buf][2 * kk + kh][wm * 32 + c], Bs[buf][2 * kk + kh][wn * 32 + c],
+                                                 acc, 0, 0, 0);
+  };
+  if constexpr (DW) {
+    // the weight-gradient passes (long reductions, ~110-120 VGPRs anyway): two register sets keep
+    // two slices in flight beyond the one in LDS, slice s loading while slices s-2 and s-1 compute
+    // (measured: conv1/2/3 dW 188/91/66 -> 175/87/63 us; the forward passes lose occupancy with it)
+    f32x4 ra0[AQ], rb0[BQ], ra1[AQ], rb1[BQ];
+    load_all(kbeg, ra0, rb0);
+    store(0, ra0, rb0);
+    if (kbeg + BK < kend) load_all(kbeg + BK, ra1, rb1);
+    if (kbeg + 2 * BK < kend) load_all(kbeg + 2 * BK, ra0, rb0);
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += 2 * BK) {
+      // LDS buffer 0: slice k0; set 1: slice k0 + BK; set 0: slice k0 + 2 BK
+      compute(0);
+      if (k0 + BK < kend) {
+        store(1, ra1, rb1);
+        if (k0 + 3 * BK < kend) load_all(k0 + 3 * BK, ra1, rb1);
+      }
+      __syncthreads();
+      if (k0 + BK >= kend) break;
+      compute(1);
+      if (k0 + 2 * BK < kend) {
+        store(0, ra0, rb0);
+        if (k0 + 4 * BK < kend) load_all(k0 + 4 * BK, ra0, rb0);
+      }
+      __syncthreads();
+    }
+  } else {
+    // one register set: the next slice loads under this slice's MFMAs
+    f32x4 ra[AQ], rbv[BQ];
+    load_all(kbeg, ra, rbv);
+    store(0, ra, rbv);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+      const bool more = k0 + BK < kend;
+      if (more) load_all(k0 + BK, ra, rbv);
+      compute(buf);
+      if (more) store(buf ^ 1, ra, rbv);        // (the other buffer: last read before the previous barrier)
+      __syncthreads();
+      buf ^= 1;
+    }
   }
 
   const int col = n0 + wn * 32 + (lane & 31);
@@ -220,25 +294,31 @@ __global__ void __launch_bounds__(256) k_nat_gemm(NatGemm a) {
     if (row >= a.M || col >= a.N) continue;
     float v = acc[r];
     if constexpr (MODE == NG_FWD1 || MODE == NG_FWD) {
+      if (MODE == NG_FWD && split) {            // a K-split partial: the fold adds bias + ReLU
+        a.slab[((int64_t)blockIdx.z * a.M + row) * a.N + col] = v;
+        continue;
+      }
       v = fmaxf((MODE == NG_FWD1 ? v * a.scale : v) + a.bias[col], 0.f);
       a.Y[(int64_t)row * a.N + col] = v;
     } else if constexpr (MODE == NG_DX) {
       const int b = row / (NI * NJ), rr = row - b * (NI * NJ), i = rr / NJ, j = rr - (rr / NJ) * NJ;
-      const int64_t o = (((int64_t)b * g.H + py + g.S * i) * g.W + px + g.S * j) * g.C + col;
+      const int64_t o = (((int64_t)b * G::H + py + G::S * i) * G::W + px + G::S * j) * G::C + col;
       a.Y[o] = a.X[o] > 0.f ? v : 0.f;
     } else {
-      a.slab[((int64_t)blockIdx.z * a.M + row) * a.N + col] = v;
+      // conv1's m = (cin, kh, kw) -> the TF row (kh 8 + kw) 4 + cin of dW1 [8][8][4][32]
+      const int trow = MODE == NG_DW1 ? ((((row >> 3) & 7) * 8 + (row & 7)) * 4 + (row >> 6)) : row;
+      a.slab[((int64_t)blockIdx.z * a.M + trow) * a.N + col] = v;
     }
   }
   if (do_colsum && n0 + tid < a.N) a.colsum[(int64_t)blockIdx.z * a.N + n0 + tid] = csum;
 }
 
-template <int MODE, int BN>
+template <int MODE, int LAYER, int BN>
 static int nat_go(const NatGemm& a, unsigned gz, hipStream_t s) {
   constexpr int BM = 4096 / BN;
   if (a.M <= 0 || a.N <= 0) return 0;
   const dim3 grid((unsigned)((a.N + BN - 1) / BN), (unsigned)((a.M + BM - 1) / BM), gz);
-  hipLaunchKernelGGL((k_nat_gemm<MODE, BN>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((k_nat_gemm<MODE, LAYER, BN>), grid, dim3(256), 0, s, a);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
@@ -272,8 +352,8 @@ static void dw_split(int64_t R, int mtiles, int target, int& ns, int& kc) {
   int want = target / mtiles;
   if (want < 1) want = 1;
   int64_t per = (R + want - 1) / want;
-  per = (per + 15) / 16 * 16;
-  if (per < 16) per = 16;
+  per = (per + 31) / 32 * 32;               // whole K slices
+  if (per < 32) per = 32;
   kc = (int)per;
   ns = (int)((R + per - 1) / per);
 }
@@ -309,10 +389,29 @@ static NatPlan nat_plan(const NetLayout& L, int64_t B) {
 }
 
 static int fc_split(int64_t B) { return a3c_gemm_effective_split(NT_FLAT, a3c_gemm_plan_split((int)B, NT_FC, NT_FLAT, 512)); }
+// conv2 / conv3 forward: few output tiles at the rollout's B = E (324 / 196 of 64 x 64 at 256
+// envs), each a long K chain -- split K in two so twice the workgroups run half the chain
+#define NAT_FWD_SPLIT 2
 
 int64_t a3c_nat_fwd_ws_floats(int64_t B) {
   const int sp = fc_split(B);
-  return sp > 1 ? (int64_t)sp * B * NT_FC : 0;
+  const int64_t fc = sp > 1 ? (int64_t)sp * B * NT_FC : 0;
+  const int64_t cv = (int64_t)NAT_FWD_SPLIT * B * (NT2_P * NT2_N > NT3_P * NT3_N ? NT2_P * NT2_N : NT3_P * NT3_N);
+  return fc > cv ? fc : cv;
+}
+
+// a split conv forward: partials into fws, then the fold with bias + ReLU into Y (gemm.hip)
+template <int LAYER>
+static int nat_fwd_split(NatGemm a, float* fws, hipStream_t s) {
+  constexpr int S = NAT_FWD_SPLIT;
+  a.kchunk = ((a.K + S - 1) / S + 31) / 32 * 32;
+  const int ns = (a.K + a.kchunk - 1) / a.kchunk;
+  a.slab = fws;
+  int rc = nat_go<NG_FWD, LAYER, 64>(a, (unsigned)ns, s);
+  if (rc) return rc;
+  GemmArgs g = {};
+  g.slab = fws; g.nsplit = ns; g.M = a.M; g.N = a.N; g.C = a.Y; g.ldc = a.N; g.epi = EPI_BIAS_RELU; g.bias = a.bias;
+  return a3c_gemm_reduce(g, s);
 }
 int64_t a3c_nat_bwd_ws_floats(const NetLayout& L, int64_t B) { return nat_plan(L, B).total; }
 
@@ -322,21 +421,18 @@ int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const Stat
   NatGemm a = {};
   switch (pass) {
     case NAT_C1F:
-      a.g = nat_conv(1);
       a.sa = sa;
       a.Wt = P + L.off[N_L1W]; a.bias = P + L.off[N_L1B]; a.Y = (float*)l1;
       a.M = (int)(B * NT1_P); a.N = NT1_N; a.K = NT_K1; a.scale = 1.0f / 255.0f;
-      return nat_go<NG_FWD1, 32>(a, 1, s);
+      return nat_go<NG_FWD1, 1, 32>(a, 1, s);
     case NAT_C2F:
-      a.g = nat_conv(2);
       a.X = l1; a.Wt = P + L.off[N_L2W]; a.bias = P + L.off[N_L2B]; a.Y = (float*)l2;
       a.M = (int)(B * NT2_P); a.N = NT2_N; a.K = NT_K2;
-      return nat_go<NG_FWD, 64>(a, 1, s);
+      return nat_fwd_split<2>(a, fws, s);
     case NAT_C3F:
-      a.g = nat_conv(3);
       a.X = l2; a.Wt = P + L.off[N_L3W]; a.bias = P + L.off[N_L3B]; a.Y = (float*)l3;
       a.M = (int)(B * NT3_P); a.N = NT3_N; a.K = NT_K3;
-      return nat_go<NG_FWD, 64>(a, 1, s);
+      return nat_fwd_split<3>(a, fws, s);
     case NAT_FCF: {
       // l4 = relu(l3 W + b) (network.py:41-42, ops.py:41-44): split-K slabs, the fold applies the epilogue
       GemmArgs gf = {};
@@ -354,30 +450,25 @@ int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const Stat
   const NatPlan p = nat_plan(L, B);
   switch (pass) {
     case NAT_C3W:     // dW3 (+ db3) over the (sample, pixel) rows
-      a.g = nat_conv(3);
       a.X = l2; a.dY = bws + p.dl3; a.slab = bws + p.s3; a.colsum = bws + p.c3;
       a.M = NT_K3; a.N = NT3_N; a.K = (int)(B * NT3_P); a.kchunk = p.kc3;
-      return nat_go<NG_DW, 64>(a, (unsigned)p.ns3, s);
+      return nat_go<NG_DW, 3, 64>(a, (unsigned)p.ns3, s);
     case NAT_C3X:     // dl2 = col2im(dl3 W3^T) * (l2 > 0)
-      a.g = nat_conv(3);
       a.X = l2; a.dY = bws + p.dl3; a.Wt = P + L.off[N_L3W]; a.Y = bws + p.dl2;
       a.M = (int)(B * NT2_P); a.N = NT2_N; a.K = 3 * 3 * NT3_N;
-      return nat_go<NG_DX, 64>(a, 1, s);
+      return nat_go<NG_DX, 3, 64>(a, 1, s);
     case NAT_C2W:
-      a.g = nat_conv(2);
       a.X = l1; a.dY = bws + p.dl2; a.slab = bws + p.s2; a.colsum = bws + p.c2;
       a.M = NT_K2; a.N = NT2_N; a.K = (int)(B * NT2_P); a.kchunk = p.kc2;
-      return nat_go<NG_DW, 64>(a, (unsigned)p.ns2, s);
+      return nat_go<NG_DW, 2, 64>(a, (unsigned)p.ns2, s);
     case NAT_C2X:     // dl1 = col2im(dl2 W2^T) * (l1 > 0), per stride-2 parity class
-      a.g = nat_conv(2);
       a.X = l1; a.dY = bws + p.dl2; a.Wt = P + L.off[N_L2W]; a.Y = bws + p.dl1;
       a.M = (int)(B * (NT1_O / 2) * (NT1_O / 2)); a.N = NT1_N; a.K = 2 * 2 * NT2_N;
-      return nat_go<NG_DX, 32>(a, 4, s);
+      return nat_go<NG_DX, 2, 32>(a, 4, s);
     case NAT_C1W:     // dW1 (+ db1) from the u8 planes (the input needs no gradient)
-      a.g = nat_conv(1);
       a.sa = sa; a.dY = bws + p.dl1; a.slab = bws + p.s1; a.colsum = bws + p.c1;
       a.M = NT_K1; a.N = NT1_N; a.K = (int)(B * NT1_P); a.kchunk = p.kc1;
-      return nat_go<NG_DW1, 32>(a, (unsigned)p.ns1, s);
+      return nat_go<NG_DW1, 1, 32>(a, (unsigned)p.ns1, s);
     default:
       return a3c_set_error(A3C_ERR_INVALID, "a3c_nat_pass_launch", "unknown pass");
   }
@@ -526,4 +617,60 @@ int a3c_nat_backward_launch(const NetLayout& L, const float* P, const StateAddr&
     nsumblk = fs.sum_c0[1];
   }
   return a3c_finalize_launch(fs, nsumblk, terms, B, loss_out, s);
+}
+
+// ---------------------------------------------------------------------------------------
+// C-ABI: the nature trunk as stateless per-op calls (include/a3c_hip.h), for src/network.py
+// ---------------------------------------------------------------------------------------
+static int nat_layout(const a3c_net_desc* net, NetLayout* L, const char* what) {
+  if (a3c_make_layout(net, L) || L->trunk != A3C_TRUNK_NATURE)
+    return a3c_set_error(A3C_ERR_INVALID, what, "a nature-trunk net description (a3c, no LSTM)");
+  return 0;
+}
+static StateAddr nat_states(const uint8_t* states, int64_t B) {
+  StateAddr sa;
+  sa.base = states; sa.env_stride = (int64_t)HIST * PLANE; sa.plane_bytes = PLANE;
+  sa.E = (int)B; sa.R = HIST; sa.L = HIST; sa.tau_offset = HIST - 1; sa.tau_ptr = nullptr;
+  return sa;
+}
+static float* nat_align(void* ws) { return (float*)(((uintptr_t)ws + 255) & ~(uintptr_t)255); }
+
+extern "C" int a3c_nature_workspace_bytes(const a3c_net_desc* net, int64_t B, int64_t* bytes) {
+  NetLayout L;
+  if (int rc = nat_layout(net, &L, "a3c_nature_workspace_bytes")) return rc;
+  if (B < 1 || !bytes) return a3c_set_error(A3C_ERR_INVALID, "a3c_nature_workspace_bytes", "bad argument");
+  const int64_t f = a3c_nat_fwd_ws_floats(B), b = a3c_nat_bwd_ws_floats(L, B);
+  *bytes = (f > b ? f : b) * 4 + 256;
+  return 0;
+}
+
+extern "C" int a3c_nature_forward(const a3c_net_desc* net, const float* params, const uint8_t* states, int64_t B,
+                                  float* l1, float* l2, float* l3, float* l4, float* z, void* workspace,
+                                  void* stream) {
+  NetLayout L;
+  if (int rc = nat_layout(net, &L, "a3c_nature_forward")) return rc;
+  if (!params || !states || !l1 || !l2 || !l3 || !l4 || !z || !workspace || B < 0 || B * NT1_P > 0x7fffffffLL ||
+      (((uintptr_t)params | (uintptr_t)l1 | (uintptr_t)l2 | (uintptr_t)l3 | (uintptr_t)l4) & 15))
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_nature_forward", "bad argument");
+  if (B == 0) return 0;
+  HeadSelect sel = {};
+  sel.mode = -1;
+  sel.E = 1;
+  return a3c_nat_forward_launch(L, params, nat_states(states, B), B, l1, l2, l3, l4, z, sel, nat_align(workspace),
+                                (hipStream_t)stream);
+}
+
+extern "C" int a3c_nature_loss_backward(const a3c_net_desc* net, const float* params, const uint8_t* states,
+                                        int64_t B, const float* l1, const float* l2, const float* l3, const float* l4,
+                                        const float* z, const int32_t* actions, const float* target, float beta,
+                                        int literal_adv, float* grads, float* loss_out, void* workspace,
+                                        void* stream) {
+  NetLayout L;
+  if (int rc = nat_layout(net, &L, "a3c_nature_loss_backward")) return rc;
+  if (!params || !states || !l1 || !l2 || !l3 || !l4 || !z || !actions || !target || !grads || !workspace ||
+      B <= 0 || B * NT1_P > 0x7fffffffLL || (((uintptr_t)grads | (uintptr_t)l3 | (uintptr_t)l4) & 15))
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_nature_loss_backward", "bad argument");
+  return a3c_nat_backward_launch(L, params, nat_states(states, B), B, l1, l2, l3, l4, z, actions, target, beta,
+                                 literal_adv, grads, loss_out, nat_align(workspace), (hipStream_t)stream, nullptr,
+                                 nullptr);
 }

@@ -83,6 +83,12 @@ SIGNATURES = {
     'a3c_loss_backward': (c_int, [ctypes.POINTER(NetDesc), c_void_p, c_void_p, c_i64, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p,
                                   c_void_p, c_void_p, c_void_p]),
+    'a3c_nature_workspace_bytes': (c_int, [ctypes.POINTER(NetDesc), c_i64, ctypes.POINTER(c_i64)]),
+    'a3c_nature_forward': (c_int, [ctypes.POINTER(NetDesc), c_void_p, c_void_p, c_i64, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_void_p]),
+    'a3c_nature_loss_backward': (c_int, [ctypes.POINTER(NetDesc), c_void_p, c_void_p, c_i64, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p,
+                                         c_void_p, c_void_p, c_void_p]),
     'a3c_optim_workspace_bytes': (c_int, [c_i64, ctypes.POINTER(c_i64)]),
     'a3c_clip_grads': (c_int, [c_void_p, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), c_float,
                                c_void_p, c_void_p, c_void_p]),

@@ -143,6 +143,60 @@ def lstm_bptt(w, x, hp, cp, gates, c, terms, dh):
     return dx, dw, db
 
 
+class NatureNet:
+    """The nature trunk (network.py:30-42) + A3C heads on the nature.hip kernels: flat parameters
+    in the C-ABI layout (include/a3c_hip.h), history_length 4."""
+
+    def __init__(self, action_size):
+        self.algo = 'a3c'
+        self.A = int(action_size)
+        self.desc = _lib.net_desc(self.A, 'a3c', dqn_type='nature')
+        self.offsets, self.sizes, self.total = _lib.param_layout(self.desc)
+        self.zs = _lib.z_stride(self.desc)
+        self.names_shapes = param_names_shapes(self.A, 'a3c', dqn_type='nature')
+        assert [int(torch.Size(s).numel()) for _, s in self.names_shapes] == self.sizes
+
+    def workspace(self, B, device='cuda'):
+        n = _lib.c_i64()
+        check(lib().a3c_nature_workspace_bytes(ctypes.byref(self.desc), max(int(B), 1), ctypes.byref(n)),
+              'a3c_nature_workspace_bytes')
+        return torch.empty(int(n.value), dtype=torch.uint8, device=device)
+
+    def forward(self, params, states, workspace=None):
+        """states [B,4,84,84] u8 (oldest frame first).  Returns dict z/l1/l2/l3/l4."""
+        _dev(params, torch.float32, 'params')
+        _dev(states, torch.uint8, 'states')
+        B = int(states.shape[0])
+        dev = states.device
+        out = dict(l1=torch.empty((B, 12800), dtype=torch.float32, device=dev),
+                   l2=torch.empty((B, 5184), dtype=torch.float32, device=dev),
+                   l3=torch.empty((B, 3136), dtype=torch.float32, device=dev),
+                   l4=torch.empty((B, 512), dtype=torch.float32, device=dev),
+                   z=torch.empty((B, self.zs), dtype=torch.float32, device=dev))
+        ws = workspace if workspace is not None else self.workspace(B, dev)
+        check(lib().a3c_nature_forward(ctypes.byref(self.desc), ptr(params), ptr(states), B, ptr(out['l1']),
+                                       ptr(out['l2']), ptr(out['l3']), ptr(out['l4']), ptr(out['z']), ptr(ws),
+                                       stream_handle()), 'a3c_nature_forward')
+        return out
+
+    def loss_backward(self, params, states, fwd, actions, target, beta=0.01, literal_adv=False, grads=None,
+                      workspace=None):
+        _dev(actions, torch.int32, 'actions')
+        _dev(target, torch.float32, 'target')
+        B = int(states.shape[0])
+        dev = states.device
+        if grads is None:
+            grads = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        loss = torch.zeros(4, dtype=torch.float32, device=dev)
+        ws = workspace if workspace is not None else self.workspace(B, dev)
+        check(lib().a3c_nature_loss_backward(ctypes.byref(self.desc), ptr(params), ptr(states), B, ptr(fwd['l1']),
+                                             ptr(fwd['l2']), ptr(fwd['l3']), ptr(fwd['l4']), ptr(fwd['z']),
+                                             ptr(actions), ptr(target), float(beta), 1 if literal_adv else 0,
+                                             ptr(grads), ptr(loss), ptr(ws), stream_handle()),
+              'a3c_nature_loss_backward')
+        return grads, loss
+
+
 class Net:
     """Flat-parameter description of the NIPS trunk + head for ``algo`` in {'a3c','q'}."""
 

@@ -3,8 +3,10 @@
 * ``DQN_type='nips'`` (network.py:43-52: conv 16/32 + fc 256) runs on the fused HIP kernels of
   the batched engine (a3c_forward / a3c_loss_backward, include/a3c_hip.h) over one flat fp32
   parameter buffer in the C-ABI layout.
-* ``DQN_type='nature'`` (network.py:30-42: conv 32/64/64 + fc 512) runs on the generic HIP
-  conv2d/matmul kernels (src/ops.py) with torch.autograd over them.
+* ``DQN_type='nature'`` (network.py:30-42: conv 32/64/64 + fc 512) runs on the nature trunk's
+  implicit-GEMM MFMA kernels (a3c_nature_forward / a3c_nature_loss_backward, nature.hip) with
+  history_length 4 and NHWC (main.py:45); other history lengths and NCHW (whose fc weights follow
+  the (c,h,w) flatten) take the generic HIP conv2d/matmul kernels (src/ops.py) with torch.autograd.
 
 The loss follows network.py:81-94 with the SURVEY §8 A11 fixes: V squeezed to [B], log pi(a)
 gathered from log_softmax (no placeholder), advantage stop-gradient unless ``literal_adv``.
@@ -63,11 +65,18 @@ class Network(object):
     self.global_network, self.global_optim = global_network, global_optim
     self.device = device
 
+    self._ws = {}
+    self.nat = None
     if self.dqn_type == 'nips':
       self.net = K.Net(self.action_size, 'a3c')
       self.names_shapes = self.net.names_shapes
       self.offsets, self.sizes, total = self.net.offsets, self.net.sizes, self.net.total
-      self._ws = {}
+    elif self.history_length == 4 and data_format == 'NHWC':   # the nature trunk's kernels (nature.hip):
+      # their fc reads the (h,w,c) flatten of NHWC (agent.py:231-232); NCHW flattens (c,h,w)
+      self.net = None
+      self.nat = K.NatureNet(self.action_size)
+      self.names_shapes = self.nat.names_shapes
+      self.offsets, self.sizes, total = self.nat.offsets, self.nat.sizes, self.nat.total
     else:
       self.net = None
       self.names_shapes = nature_names_shapes(self.history_length, self.action_size)
@@ -105,7 +114,7 @@ class Network(object):
 
   def _workspace(self, B):
     if B not in self._ws:
-      self._ws[B] = self.net.workspace(B, self.device)
+      self._ws[B] = (self.net or self.nat).workspace(B, self.device)
     return self._ws[B]
 
   def _nature_z(self, flat, planes):
@@ -126,8 +135,8 @@ class Network(object):
   def forward(self, s_t):
     """network.py:60-79 evaluated: policy_logits, policy, log_policy, policy_entropy, value."""
     planes = self._planes(s_t)
-    if self.net is not None:
-      z = self.net.forward(self.flat, planes, save_l1=False, workspace=self._workspace(int(planes.shape[0])))['z']
+    if self.net is not None or self.nat is not None:
+      z = self.z(planes)
       logits, value = z[:, :self.action_size], z[:, self.action_size]
     else:
       with torch.no_grad():
@@ -142,6 +151,8 @@ class Network(object):
     planes = self._planes(s_t)
     if self.net is not None:
       return self.net.forward(self.flat, planes, save_l1=False, workspace=self._workspace(int(planes.shape[0])))['z']
+    if self.nat is not None:
+      return self.nat.forward(self.flat, planes, workspace=self._workspace(int(planes.shape[0])))['z']
     with torch.no_grad():
       logits, value = self._nature_z(self.flat, planes)
     zs = (self.action_size + 1 + 3) // 4 * 4
@@ -161,11 +172,13 @@ class Network(object):
     B = int(planes.shape[0])
     a = torch.as_tensor(actions, dtype=torch.int32, device=self.device).reshape(B).contiguous()
     R = torch.as_tensor(R, dtype=torch.float32, device=self.device).reshape(B).contiguous()
-    if self.net is not None:
-      ws = self._workspace(B)
-      fwd = self.net.forward(self.flat, planes, save_l1=True, workspace=ws)
-      return self.net.loss_backward(self.flat, planes, fwd, a, R, beta=self.beta, literal_adv=self.literal_adv,
-                                    workspace=ws)
+    if self.net is not None or self.nat is not None:
+      net, ws = self.net or self.nat, self._workspace(B)
+      fwd = self.net.forward(self.flat, planes, save_l1=True, workspace=ws) if self.net is not None else \
+          self.nat.forward(self.flat, planes, workspace=ws)
+      self.last_forward = fwd       # (the activations the gradients were taken at: tests)
+      return net.loss_backward(self.flat, planes, fwd, a, R, beta=self.beta, literal_adv=self.literal_adv,
+                               workspace=ws)
     flat = self.flat.detach().requires_grad_(True)
     logits, V = self._nature_z(flat, planes)
     logp = torch.log_softmax(logits, dim=1)

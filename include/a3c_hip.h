@@ -78,6 +78,23 @@ int a3c_param_layout(const a3c_net_desc* net, int* n_tensors, int64_t* offsets, 
 int a3c_workspace_bytes(const a3c_net_desc* net, int64_t B, int64_t* bytes);
 
 /* ----------------------------------------------------------------------------
+ * The nature trunk (network.py:30-42, Network(DQN_type='nature')): net->trunk =
+ * A3C_TRUNK_NATURE, algo A3C, history_length 4.  Stateless forward / loss + backward over B
+ * states (u8 planes [B][4][84][84], 16-B aligned), implicit-GEMM kernels of nature.hip:
+ *   l1 [B][20][20][32], l2 [B][9][9][64], l3 [B][3136] (conv3 out, (h,w,c) flatten),
+ *   l4 [B][512] (fc out), z [B][zs] (logits, value).  The backward (network.py:81-94 with the
+ *   A11 fixes) reads the forward's activations; grads [total] in the flat layout, loss_out[4].
+ * Replace network.py:30-42 + 81-94 (the TF graph of the nature trunk, its compute_gradients).
+ * -------------------------------------------------------------------------- */
+int a3c_nature_workspace_bytes(const a3c_net_desc* net, int64_t B, int64_t* bytes);
+int a3c_nature_forward(const a3c_net_desc* net, const float* params, const uint8_t* states, int64_t B,
+                       float* l1, float* l2, float* l3, float* l4, float* z, void* workspace, void* stream);
+int a3c_nature_loss_backward(const a3c_net_desc* net, const float* params, const uint8_t* states, int64_t B,
+                             const float* l1, const float* l2, const float* l3, const float* l4, const float* z,
+                             const int32_t* actions, const float* target, float beta, int literal_adv,
+                             float* grads, float* loss_out, void* workspace, void* stream);
+
+/* ----------------------------------------------------------------------------
  * K1  Environment.screen (environment.py:49-53): fp64 luminance truncated to u8, then
  *     Pillow BILINEAR fixed-point resample (scipy.misc.imresize, environment.py:5-8).
  *     rgb frames [*, in_h, in_w, 3] u8; frame i reads rgb + (frame_idx ? frame_idx[i] : i)

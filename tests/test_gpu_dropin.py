@@ -228,7 +228,21 @@ def test_network_forward_loss_grads_match_oracle(dqn_type):
         assert abs(loss[i] - losses[key]) <= 1e-4 * max(abs(losses[key]), 1.0), key
     g = grads.cpu().numpy()
     for (name, shp), o, n in zip(net.names_shapes, net.offsets, net.sizes):
-        assert rel_l2(g[o:o + n].reshape(shp), g_ref[name]) < 2e-2, name
+        assert rel_l2(g[o:o + n].reshape(shp), g_ref[name]) < 2e-2, name      # independent forward (ReLU flips)
+    # and at 1e-4 against the oracle backward on the kernels' own activations (the same ReLU masks)
+    fa = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in net.last_forward.items() if v is not None}
+    x0 = states.astype(np.float64) / 255.0
+    zs = fa['z'][:, :7]
+    if dqn_type == 'nature':
+        same = dict(z=zs, h3=fa['l4'], flat=fa['l3'], acts=[x0, fa['l1'].reshape(B, 20, 20, 32),
+                                                           fa['l2'].reshape(B, 9, 9, 64), fa['l3'].reshape(B, 7, 7, 64)])
+    else:
+        same = dict(z=zs, h3=fa['l3'], flat=fa['l2'], acts=[x0, fa['l1'].reshape(B, 20, 20, 16),
+                                                           fa['l2'].reshape(B, 9, 9, 32)])
+    _, dz_same = R.a3c_loss_and_dz(zs, actions, Rt, 0.01)
+    g_same = R.backward(p, same, dz_same, 'a3c', dqn_type)
+    for (name, shp), o, n in zip(net.names_shapes, net.offsets, net.sizes):
+        assert rel_l2(g[o:o + n].reshape(shp), g_same[name]) < 1e-4, (name, rel_l2(g[o:o + n].reshape(shp), g_same[name]))
     acts = net.sample_action(torch.as_tensor(planes).cuda(), seed=1, step=3)
     assert acts.shape == (B,) and int(acts.min()) >= 0 and int(acts.max()) < 6
 
