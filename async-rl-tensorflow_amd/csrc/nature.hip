@@ -229,6 +229,11 @@ __global__ void __launch_bounds__(256) k_nat_gemm(NatGemm a) {
   const bool do_colsum = DW && a.colsum && blockIdx.y == 0 && tid < BN;
   const int kh = lane >> 5, c = lane & 31;
   auto load_all = [&](int k0, f32x4 (&ra)[AQ], f32x4 (&rbv)[BQ]) {
+#if defined(NAT_ABL) && NAT_ABL == 2      // measurement only: no operand loads
+    for (int i = 0; i < AQ; ++i) ra[i] = (f32x4){(float)k0, 1.f, 2.f, 3.f};
+    for (int j = 0; j < BQ; ++j) rbv[j] = (f32x4){(float)k0, 1.f, 2.f, 3.f};
+    return;
+#endif
 #pragma unroll
     for (int i = 0; i < AQ; ++i) ra[i] = load_a(i, k0);
 #pragma unroll
@@ -239,6 +244,10 @@ __global__ void __launch_bounds__(256) k_nat_gemm(NatGemm a) {
 #pragma unroll
       for (int k = 0; k < BK; ++k) csum += Bs[buf][k][tid];
     }
+#if defined(NAT_ABL) && NAT_ABL == 1      // measurement only: LDS operand reads, no MFMA
+    for (int kk = 0; kk < BK / 2; ++kk) acc[kk] += As[buf][2 * kk + kh][wm * 32 + c] * Bs[buf][2 * kk + kh][wn * 32 + c];
+    return;
+#endif
 #pragma unroll
     for (int kk = 0; kk < BK / 2; ++kk)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[buf][2 * kk + kh][wm * 32 + c], Bs[buf][2 * kk + kh][wn * 32 + c],

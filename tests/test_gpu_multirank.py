@@ -38,7 +38,7 @@ TQ = 2000       # q target period: with 64 envs x 5 steps x 4 ranks (1,280 per u
 
 
 def _cfg(cfg):
-    c = dict(A=A, lives=0, lstm=False, algo='a3c', E=E, n=N, tq=TQ, split=1, ov=False)
+    c = dict(A=A, lives=0, lstm=False, algo='a3c', E=E, n=N, tq=TQ, split=1, ov=False, dqn='nips')
     c.update(cfg or {})
     return c
 
@@ -55,8 +55,8 @@ def _make(rank, world, overlap, cfg=None):
     kw['split_exchange'] = c['split']      # (several ranks: the two-phase exchange, PartitionedPS)
     eng = Engine(num_envs=c['E'], n_step=c['n'], action_size=c['A'], algo=c['algo'], num_frames=64, seed=11,
                  env_id_base=rank * c['E'], world_size=world, overlap=overlap, start_lives=c['lives'],
-                 lstm=c['lstm'], **kw)
-    ns = param_names_shapes(c['A'], c['algo'], lstm=c['lstm'])
+                 lstm=c['lstm'], dqn_type=c['dqn'], **kw)
+    ns = param_names_shapes(c['A'], c['algo'], lstm=c['lstm'], dqn_type=c['dqn'])
     eng.reset(flatten_host(ns, eng.offsets, eng.params.numel(), _init(ns)))
     return eng
 
@@ -192,7 +192,8 @@ class _Oracle:
         self.c, self.ns, self.world = c, ns, world
         kw = dict(target_q_update_step=c['tq']) if c['algo'] == 'q' else {}
         self.refs = [EngineRef(_init(ns), c['E'], c['n'], c['A'], c['algo'], c['lives'], 64, 11,
-                               env_id_base=r * c['E'], world_size=world, **kw) for r in range(world)]
+                               env_id_base=r * c['E'], world_size=world, dqn_type=c['dqn'], **kw)
+                     for r in range(world)]
         for ref in self.refs:
             ref.reset()
         self.hist = [[] for _ in range(world)]
@@ -268,9 +269,11 @@ class _Oracle:
     (4, True, dict(A=4, lives=5), True), (4, False, dict(A=6, lives=3, lstm=True, E=16), False),
     (4, False, dict(algo='q', A=6, lives=3), True), (2, False, dict(algo='q', A=4, lives=5, n=8), False),
     (4, True, dict(split=0), False), (2, False, dict(split=0), False),
-    (2, True, dict(algo='q', A=6, lives=3, tq=700), True), (4, True, dict(algo='q', A=4, lives=5, tq=700), False)],
+    (2, True, dict(algo='q', A=6, lives=3, tq=700), True), (4, True, dict(algo='q', A=4, lives=5, tq=700), False),
+    (2, False, dict(dqn='nature', split=0, E=24), True), (2, True, dict(dqn='nature', split=0, E=24, A=4, lives=5), True)],
     ids=['w2-sync', 'w2-overlap', 'w4-sync', 'w4-overlap', 'w4-breakout-overlap', 'w4-lstm-sync', 'w4-q-sync',
-         'w2-q-breakout-sync', 'w4-overlap-onephase', 'w2-sync-onephase', 'w2-q-overlap', 'w4-q-breakout-overlap'])
+         'w2-q-breakout-sync', 'w4-overlap-onephase', 'w2-sync-onephase', 'w2-q-overlap', 'w4-q-breakout-overlap',
+         'w2-nature-sync', 'w2-nature-breakout-overlap'])
 def test_partitioned_ps_ranks(world, overlap, cfg, oracle):
     """`world` ranks on one GPU (gloo, host-staged collectives) run the default multi-GPU exchange:
     all-to-all of the clipped gradients, each rank's W sequential RMSProp steps on its range,
@@ -291,7 +294,7 @@ def test_partitioned_ps_ranks(world, overlap, cfg, oracle):
     for r in range(1, world):
         assert np.array_equal(res[0]['params'], res[r]['params']), r
         assert res[0]['step'] == res[r]['step'] == ITERS * per_update - (per_update if overlap else 0)
-    ns = param_names_shapes(c['A'], c['algo'], lstm=c['lstm'])
+    ns = param_names_shapes(c['A'], c['algo'], lstm=c['lstm'], dqn_type=c['dqn'])
     names = [nm for nm, _ in ns]
     engs = [_make(r, world, overlap, cfg) for r in range(world)]
     orc = _Oracle(world, cfg, ns) if oracle else None
