@@ -598,9 +598,9 @@ static bool kernel_go(const a3c_engine* e) {
 // rollout start: forward weights of the rollout's parameters (+ q: the epsilon schedule)
 static int enqueue_rollout_begin(a3c_engine* e, const Slot& sl, hipStream_t s) {
   const a3c_engine_config& c = e->cfg;
-  if (e->nat)   // (no prepared weights: the nature passes read the fp32 parameters)
-    return a3c_nat_prep_launch(e->overlap ? e->counters : nullptr, e->overlap ? sl.tau : nullptr,
-                               kernel_go(e) ? e->xflags + 1 : nullptr, s);
+  if (e->nat)   // (prepared: conv1's bf16 weight terms; the other passes read the fp32 parameters)
+    return a3c_nat_prep_launch(e->L, sl.P, (uint16_t*)sl.prep, e->overlap ? e->counters : nullptr,
+                               e->overlap ? sl.tau : nullptr, kernel_go(e) ? e->xflags + 1 : nullptr, s);
   // params are fixed for the rollout; overlap: the prep kernel also snapshots tau for the slot's
   // backward (sync: the slot's tau is the live counter)
   int rc = a3c_prep_fwd_launch(e->L, sl.P, sl.prep, s, e->overlap ? e->counters : nullptr,
@@ -680,7 +680,7 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
   if (e->nat)
     rc = a3c_nat_forward_launch(L, sl.P, ring_addr(e, t, e->counters), E, sl.act_l1 + o * NT_A1,
                                 sl.act_l2 + o * NT_A2, sl.act_l3 + o * NT_FLAT, sl.act_l4 + o * NT_FC, sl.z + o * zs, sel,
-                                e->nat_fws, s);
+                                (const uint16_t*)sl.prep, e->nat_fws, s);
   else
     rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, t, e->counters), E, sl.act_l1 + o * C1_P * C1_N,
                               sl.act_l2 + o * FLAT, sl.act_l3 + o * FC, sl.z + o * zs, sel, s,
@@ -719,7 +719,7 @@ static int enqueue_rollout_end(a3c_engine* e, const Slot& sl, hipStream_t s) {
       float* x = sl.nscr;
       return a3c_nat_forward_launch(L, sl.P, ring_addr(e, n, e->counters), E, x, x + E * NT_A1,
                                     x + E * (NT_A1 + NT_A2), x + E * (NT_A1 + NT_A2 + NT_FLAT), sl.z + e->nE * L.zs,
-                                    none, e->nat_fws, s);
+                                    none, (const uint16_t*)sl.prep, e->nat_fws, s);
     }
     int rc = a3c_forward_launch(L, sl.P, sl.prep, ring_addr(e, n, e->counters), E, nullptr, sl.scr_l2,
                                 sl.scr_l3, sl.z + e->nE * L.zs, none, s, L.lstm ? &ls : nullptr,
@@ -1638,9 +1638,9 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
     const StateAddr sa = fwd ? ring_addr(e, 0, e->counters) : ring_addr(e, 0, bs.tau);
     auto go = [&]() -> int {
       return fwd ? a3c_nat_pass_launch(pass, L, e->params, sa, E, sl.act_l1, sl.act_l2, sl.act_l3, sl.act_l4,
-                                       e->nat_fws, nullptr, s)
+                                       (const uint16_t*)sl.prep, e->nat_fws, nullptr, s)
                  : a3c_nat_pass_launch(pass, L, bs.P, sa, e->nE, bs.act_l1, bs.act_l2, bs.act_l3, bs.act_l4, nullptr,
-                                       e->ws, s);
+                                       nullptr, e->ws, s);
     };
     int rc = go();
     if (rc) return rc;

@@ -32,10 +32,12 @@ inline int64_t nat_act_floats() { return (int64_t)NT_A1 + NT_A2 + NT_FLAT + NT_F
 // forward of B states s_{tau0 + b / E} (sa) with parameters P.  Activations [B][...] NHWC:
 // l1 [B][12800], l2 [B][5184], l3 [B][3136] (the (h,w,c) flatten of network.py's linear), l4 [B][512];
 // z [B][zs] (logits, value); sel.mode >= 0: action draw + fused env act (as the NIPS head kernels).
-// ws: a3c_nat_fwd_ws_floats(B) floats (the fc's split-K slabs).
+// ws: a3c_nat_fwd_ws_floats(B) floats (split-K slabs; with w1t null, also conv1's bf16 weight terms,
+// prepared there first).  w1t: the terms a3c_nat_prep_launch made from P (the engine's rollouts).
 int64_t a3c_nat_fwd_ws_floats(int64_t B);
 int a3c_nat_forward_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, float* l1, float* l2,
-                           float* l3, float* l4, float* z, const HeadSelect& sel, float* ws, hipStream_t s);
+                           float* l3, float* l4, float* z, const HeadSelect& sel, const uint16_t* w1t, float* ws,
+                           hipStream_t s);
 
 struct ReturnsArgs;
 struct SumsqFused;
@@ -53,6 +55,10 @@ int a3c_nat_fused_tab(const NetLayout& L, TensorTab* tt);
 // (valid after a backward of the same B has filled them)
 enum { NAT_C1F = 0, NAT_C2F, NAT_C3F, NAT_FCF, NAT_C3W, NAT_C3X, NAT_C2W, NAT_C2X, NAT_C1W };
 int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* l1,
-                        const float* l2, const float* l3, const float* l4, float* fws, float* bws, hipStream_t s);
-// the rollout start on the nature trunk: tau snapshot (overlap) and the backward's go
-int a3c_nat_prep_launch(const int64_t* tau_src, int64_t* tau_dst, uint32_t* sig, hipStream_t s);
+                        const float* l2, const float* l3, const float* l4, const uint16_t* w1t, float* fws,
+                        float* bws, hipStream_t s);
+// the rollout start on the nature trunk: conv1's bf16 weight terms of P into w1t (A3C_NAT_W1T_BYTES),
+// tau snapshot (overlap) and the backward's go
+#define A3C_NAT_W1T_BYTES (3 * NT1_N * NT_K1 * 2)
+int a3c_nat_prep_launch(const NetLayout& L, const float* P, uint16_t* w1t, const int64_t* tau_src, int64_t* tau_dst,
+                        uint32_t* sig, hipStream_t s);

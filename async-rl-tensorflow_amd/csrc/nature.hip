@@ -332,6 +332,139 @@ static int nat_go(const NatGemm& a, unsigned gz, hipStream_t s) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// conv1 forward on the bf16 matrix cores.  A u8 pixel is exact in bf16, and the fp32 weight is
+// three round-to-nearest bf16 terms (w = hi + mid + lo to ~2^-24 relative, as the NIPS conv1,
+// net_fwd.hip): acc += x hi + x mid + x lo, every product exact in the fp32 accumulator -- three
+// v_mfma_f32_32x32x16_bf16 (32 cycles each) per 16-deep K step instead of eight 64-cycle fp32 ones.
+// ---------------------------------------------------------------------------------------
+#define W1T_ELEMS (3 * NT1_N * NT_K1)     // bf16: [term][cout][k'], k' = (cin, kh, kw)
+#define C1B_LD 40                          // bf16 per LDS row: 32 + 8 (16-byte aligned, rows 80 B apart)
+
+__device__ inline uint32_t nat_bf16_rn(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+__global__ void __launch_bounds__(256) k_nat_w1_terms(const float* __restrict__ W1, uint16_t* __restrict__ w1t) {
+#pragma clang fp contract(off)
+  const int i = blockIdx.x * 256 + threadIdx.x;     // (cout, k')
+  if (i >= NT1_N * NT_K1) return;
+  const int n = i / NT_K1, k = i - n * NT_K1;
+  const int c = k >> 6, kh = (k >> 3) & 7, kw = k & 7;
+  const float w = W1[((kh * 8 + kw) * HIST + c) * NT1_N + n];
+  const uint32_t h = nat_bf16_rn(w);
+  const float r1 = w - __uint_as_float(h << 16);
+  const uint32_t m = nat_bf16_rn(r1);
+  const float r2 = r1 - __uint_as_float(m << 16);
+  const uint32_t l = nat_bf16_rn(r2);
+  w1t[(0 * NT1_N + n) * NT_K1 + k] = (uint16_t)h;
+  w1t[(1 * NT1_N + n) * NT_K1 + k] = (uint16_t)m;
+  w1t[(2 * NT1_N + n) * NT_K1 + k] = (uint16_t)l;
+}
+
+__device__ inline uint2 nat_u8x4_bf16(uint32_t d) {   // 4 pixels -> 4 bf16 (exact: the upper halves of their f32)
+  const float f0 = (float)(d & 255u), f1 = (float)((d >> 8) & 255u);
+  const float f2 = (float)((d >> 16) & 255u), f3 = (float)(d >> 24);
+  return make_uint2(__builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u),
+                    __builtin_amdgcn_perm(__float_as_uint(f3), __float_as_uint(f2), 0x07060302u));
+}
+
+// tile: 128 rows (sample, pixel) x 32 channels, 4 waves of 32 rows; K = 256 in 8 slices of 32 (k' =
+// (cin, kh, kw): a row's 32 k' of a slice are 4 kernel rows of 8 pixels of one plane), LDS double-buffered
+__global__ void __launch_bounds__(256) k_nat_conv1_bf(StateAddr sa, const uint16_t* __restrict__ w1t,
+                                                      const float* __restrict__ bias, float* __restrict__ Y, int M,
+                                                      float scale) {
+  constexpr int BM = 128, BK = 32, P = NT1_P, OW = NT1_O;
+  __shared__ __attribute__((aligned(16))) uint16_t As[2][BM][C1B_LD];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][3][NT1_N][C1B_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int m0 = blockIdx.x * BM;
+  RingRows ring;
+  ring.init(sa, sa.tau_ptr ? *sa.tau_ptr : 0);
+  int ar[4], ac[4], ai[4], aj[4];
+  bool aval[4];
+  const uint8_t* apl[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = tid + 256 * i;
+    ar[i] = q >> 3; ac[i] = (q & 7) * 4;
+    const int m = m0 + ar[i];
+    aval[i] = m < M;
+    const int mm = aval[i] ? m : 0;
+    const int b = mm / P, pos = mm - b * P, oy = pos / OW, ox = pos - oy * OW;
+    const int t = ring.step_of(b), e = b - t * ring.E;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) apl[i][c] = ring.plane(e, t, c);
+    ai[i] = oy * 4; aj[i] = ox * 4;
+  }
+  auto load_a = [&](int i, int k0) -> uint32_t {
+    const int k = k0 + ac[i];
+    if (!aval[i]) return 0u;
+    const int c = k >> 6, kh = (k >> 3) & 7, kw = k & 7;
+    return *(const uint32_t*)(apl[i][c] + (ai[i] + kh) * IMG + aj[i] + kw);
+  };
+  // B: 3 terms x 32 couts x 32 k' per slice = 384 chunks of 8 bf16
+  auto load_b = [&](int q, int k0) -> uint4 {
+    const int term = q >> 7, n = (q >> 2) & 31, kc = (q & 3) * 8;
+    return *(const uint4*)(w1t + (term * NT1_N + n) * NT_K1 + k0 + kc);
+  };
+  uint32_t ra[4];
+  uint4 rb0, rb1;
+  const bool b2 = tid < 128;
+  auto load_all = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ra[i] = load_a(i, k0);
+    rb0 = load_b(tid, k0);
+    if (b2) rb1 = load_b(256 + tid, k0);
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *(uint2*)&As[buf][ar[i]][ac[i]] = nat_u8x4_bf16(ra[i]);
+    {
+      const int q = tid, term = q >> 7, n = (q >> 2) & 31, kc = (q & 3) * 8;
+      *(uint4*)&Bs[buf][term][n][kc] = rb0;
+    }
+    if (b2) {
+      const int q = 256 + tid, term = q >> 7, n = (q >> 2) & 31, kc = (q & 3) * 8;
+      *(uint4*)&Bs[buf][term][n][kc] = rb1;
+    }
+  };
+  f32x16 acc = {};
+  const int r = lane & 31, h = lane >> 5;
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const bf16x8 a = *(const bf16x8*)&As[buf][wid * 32 + r][16 * s + 8 * h];
+#pragma unroll
+      for (int term = 0; term < 3; ++term) {
+        const bf16x8 bv = *(const bf16x8*)&Bs[buf][term][r][16 * s + 8 * h];
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bv, acc, 0, 0, 0);
+      }
+    }
+  };
+  load_all(0);
+  store(0);
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < NT_K1; k0 += BK) {
+    const bool more = k0 + BK < NT_K1;
+    if (more) load_all(k0 + BK);
+    compute(buf);
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  const int col = lane & 31;
+  const float bc = bias[col];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int row = m0 + wid * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+    if (row < M) Y[(int64_t)row * NT1_N + col] = fmaxf(acc[q] * scale + bc, 0.f);
+  }
+}
+
 // the policy / value head of B states (one wave each) on the 512-wide fc output, + the action
 // draw and fused env act when sel.mode >= 0 (agent.py:59-62, network.py:72)
 __global__ void __launch_bounds__(256) k_nat_head(const float* __restrict__ l4, int64_t B, const float* __restrict__ Wp,
@@ -402,11 +535,16 @@ static int fc_split(int64_t B) { return a3c_gemm_effective_split(NT_FLAT, a3c_ge
 // envs), each a long K chain -- split K in two so twice the workgroups run half the chain
 #define NAT_FWD_SPLIT 2
 
-int64_t a3c_nat_fwd_ws_floats(int64_t B) {
+static int64_t nat_fwd_slab_floats(int64_t B) {
   const int sp = fc_split(B);
   const int64_t fc = sp > 1 ? (int64_t)sp * B * NT_FC : 0;
   const int64_t cv = (int64_t)NAT_FWD_SPLIT * B * (NT2_P * NT2_N > NT3_P * NT3_N ? NT2_P * NT2_N : NT3_P * NT3_N);
-  return fc > cv ? fc : cv;
+  return ((fc > cv ? fc : cv) + 63) / 64 * 64;
+}
+int64_t a3c_nat_fwd_ws_floats(int64_t B) { return nat_fwd_slab_floats(B) + A3C_NAT_W1T_BYTES / 4; }
+static int nat_c1_bf() {
+  static const int v = (int)A3C_AB_KNOB("A3C_NAT_C1_BF", 1);   // A/B: 0 = the fp32 MFMA conv1 forward
+  return v;
 }
 
 // a split conv forward: partials into fws, then the fold with bias + ReLU into Y (gemm.hip)
@@ -426,10 +564,18 @@ int64_t a3c_nat_bwd_ws_floats(const NetLayout& L, int64_t B) { return nat_plan(L
 
 // one pass of the forward (B states) or of the backward (B samples, buffers of the plan in bws)
 int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* l1,
-                        const float* l2, const float* l3, const float* l4, float* fws, float* bws, hipStream_t s) {
+                        const float* l2, const float* l3, const float* l4, const uint16_t* w1t, float* fws,
+                        float* bws, hipStream_t s) {
   NatGemm a = {};
   switch (pass) {
     case NAT_C1F:
+      if (w1t && nat_c1_bf()) {
+        const int M = (int)(B * NT1_P);
+        hipLaunchKernelGGL(k_nat_conv1_bf, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, sa, w1t,
+                           P + L.off[N_L1B], (float*)l1, M, 1.0f / 255.0f);
+        A3C_CHECK(hipGetLastError());
+        return 0;
+      }
       a.sa = sa;
       a.Wt = P + L.off[N_L1W]; a.bias = P + L.off[N_L1B]; a.Y = (float*)l1;
       a.M = (int)(B * NT1_P); a.N = NT1_N; a.K = NT_K1; a.scale = 1.0f / 255.0f;
@@ -489,7 +635,14 @@ __global__ void k_nat_prep(const int64_t* __restrict__ tau_src, int64_t* __restr
   if (tau_dst) *tau_dst = *tau_src;
   if (sig) (void)__hip_atomic_fetch_add(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-int a3c_nat_prep_launch(const int64_t* tau_src, int64_t* tau_dst, uint32_t* sig, hipStream_t s) {
+static int nat_w1_terms_launch(const NetLayout& L, const float* P, uint16_t* w1t, hipStream_t s) {
+  hipLaunchKernelGGL(k_nat_w1_terms, dim3((NT1_N * NT_K1 + 255) / 256), dim3(256), 0, s, P + L.off[N_L1W], w1t);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+int a3c_nat_prep_launch(const NetLayout& L, const float* P, uint16_t* w1t, const int64_t* tau_src, int64_t* tau_dst,
+                        uint32_t* sig, hipStream_t s) {
+  if (int rc = nat_w1_terms_launch(L, P, w1t, s)) return rc;
   hipLaunchKernelGGL(k_nat_prep, dim3(1), dim3(1), 0, s, tau_src, tau_src ? tau_dst : nullptr, sig);
   A3C_CHECK(hipGetLastError());
   return 0;
@@ -499,11 +652,17 @@ int a3c_nat_prep_launch(const int64_t* tau_src, int64_t* tau_dst, uint32_t* sig,
 // forward
 // ---------------------------------------------------------------------------------------
 int a3c_nat_forward_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, float* l1, float* l2,
-                           float* l3, float* l4, float* z, const HeadSelect& sel, float* ws, hipStream_t s) {
+                           float* l3, float* l4, float* z, const HeadSelect& sel, const uint16_t* w1t, float* ws,
+                           hipStream_t s) {
   if (L.trunk != A3C_TRUNK_NATURE || B <= 0 || B * NT1_P > 0x7fffffffLL)
     return a3c_set_error(A3C_ERR_INVALID, "a3c_nat_forward", "nature trunk, 0 < B, B * 400 < 2^31");
+  if (!w1t) {   // one-off forward: the weight terms into the workspace's tail first
+    uint16_t* t = (uint16_t*)(ws + nat_fwd_slab_floats(B));
+    if (int rc = nat_w1_terms_launch(L, P, t, s)) return rc;
+    w1t = t;
+  }
   for (int pass = NAT_C1F; pass <= NAT_FCF; ++pass) {
-    const int rc = a3c_nat_pass_launch(pass, L, P, sa, B, l1, l2, l3, l4, ws, nullptr, s);
+    const int rc = a3c_nat_pass_launch(pass, L, P, sa, B, l1, l2, l3, l4, w1t, ws, nullptr, s);
     if (rc) return rc;
   }
   hipLaunchKernelGGL(k_nat_head, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, l4, B, P + L.off[N_HW],
@@ -580,7 +739,7 @@ int a3c_nat_backward_launch(const NetLayout& L, const float* P, const StateAddr&
   rc = a3c_gemm(true, false, gd, s);
   if (rc) return rc;
   for (int pass = NAT_C3W; pass <= NAT_C1W; ++pass) {
-    rc = a3c_nat_pass_launch(pass, L, P, sa, B, l1, l2, l3, l4, nullptr, ws, s);
+    rc = a3c_nat_pass_launch(pass, L, P, sa, B, l1, l2, l3, l4, nullptr, nullptr, ws, s);
     if (rc) return rc;
   }
   // the weight slabs in NAT_GROUPS fixed-order groups, then k_finalize: every segment, the loss
@@ -665,8 +824,8 @@ extern "C" int a3c_nature_forward(const a3c_net_desc* net, const float* params, 
   HeadSelect sel = {};
   sel.mode = -1;
   sel.E = 1;
-  return a3c_nat_forward_launch(L, params, nat_states(states, B), B, l1, l2, l3, l4, z, sel, nat_align(workspace),
-                                (hipStream_t)stream);
+  return a3c_nat_forward_launch(L, params, nat_states(states, B), B, l1, l2, l3, l4, z, sel, nullptr,
+                                nat_align(workspace), (hipStream_t)stream);
 }
 
 extern "C" int a3c_nature_loss_backward(const a3c_net_desc* net, const float* params, const uint8_t* states,
