@@ -333,6 +333,362 @@ static int nat_go(const NatGemm& a, unsigned gz, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------
+// The same passes on the bf16 matrix cores (v_mfma_f32_32x32x16_bf16, 32 cycles per 32x32x16 vs 512
+// for the 32x32x2f32 chain of the same depth).  Each fp32 operand is split at the LDS store into
+// three round-to-nearest bf16 terms x = hi + mid + lo (v_cvt_pk_bf16_f32; exact to ~2^-24 relative)
+// and the tile sums the six products hi.hi, hi.mid, mid.hi, mid.mid, hi.lo, lo.hi (the dropped
+// ones are below 2^-24 of the product): fp32-class results, as the NIPS conv2 (net_fwd.hip).
+// conv1's dW (TA = 1): a u8 pixel is exact in one bf16 term, three products.
+// LDS holds the terms k-contiguous ([row][k], 40 bf16 a row) for the MFMA's 8-deep lane fragments;
+// operands that arrive along rows (the dW passes' A and B, the forward's weights) are loaded as
+// quad pairs at k and k + 1 and stored as packed (k, k + 1) dwords.
+// ---------------------------------------------------------------------------------------
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+
+// NT terms (1 or 3) of the pair (x0, x1), each a packed bf16x2 dword
+template <int NT>
+__device__ inline void nat_split2(float x0, float x1, uint32_t (&o)[NT]) {
+  const f32x2v v = {x0, x1};
+  const bf16x2v h = __builtin_convertvector(v, bf16x2v);
+  o[0] = __builtin_bit_cast(uint32_t, h);
+  if constexpr (NT == 3) {
+    const f32x2v r1 = v - __builtin_convertvector(h, f32x2v);
+    const bf16x2v m = __builtin_convertvector(r1, bf16x2v);
+    const f32x2v r2 = r1 - __builtin_convertvector(m, f32x2v);
+    o[1] = __builtin_bit_cast(uint32_t, m);
+    o[2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r2, bf16x2v));
+  }
+}
+
+template <int MODE, int LAYER, int BN, int TA, int NBUF>
+__global__ void __launch_bounds__(256) k_nat_gemm_bf(NatGemm a) {
+  using G = NG<LAYER>;
+  constexpr int BM = 4096 / BN, BK = 32, LD = 40;
+  constexpr int WN = BN / 32;
+  constexpr bool A_KC = MODE == NG_FWD || MODE == NG_DX;         // A quads along k (else pairs of row quads)
+  constexpr bool B_NC = MODE != NG_DX;                           // B quads along n: pairs of row quads
+  constexpr bool DW = MODE == NG_DW || MODE == NG_DW1;
+  constexpr bool U8 = MODE == NG_DW1;
+  static_assert(MODE != NG_FWD1, "conv1 forward: k_nat_conv1_bf");
+  static_assert(TA == 3 || (TA == 1 && U8), "one A term only for the exact u8 pixels");
+  constexpr int AQ = BM * BK / 4 / 256;                          // A quads per thread (2 or 4)
+  constexpr int BQ0 = BN * BK / 4 / 256;
+  constexpr int BQ = B_NC && BQ0 < 2 ? 2 : BQ0;                  // B quads per thread (pairs: >= 2)
+  constexpr int BPAIRS = BN * BK / 8;                            // B_NC: quad pairs per slice
+  constexpr int P = G::OH * G::OW;
+  constexpr int TW = G::KW / G::S;
+  constexpr int NI = G::H / G::S, NJ = G::W / G::S;
+  static_assert(MODE != NG_DX || (G::H % G::S == 0 && G::KH % G::S == 0), "parity classes");
+  static_assert(!U8 || G::C == 4, "u8 planes: the 4 history frames");
+  static_assert((BM / 4) % 4 == 0 && (BN / 4) % 4 == 0, "pair mapping: 4 quads of a row per lane group");
+  __shared__ __attribute__((aligned(16))) uint16_t As[NBUF][TA][BM][LD];   // NBUF 1: a third of the LDS,
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[NBUF][3][BN][LD];    // two barriers per slice
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const bool split = DW || (MODE == NG_FWD && a.kchunk > 0);
+  const int kbeg = split ? (int)blockIdx.z * a.kchunk : 0;
+  const int kend = split ? min(a.K, kbeg + a.kchunk) : a.K;
+  const int py = MODE == NG_DX ? (int)blockIdx.z / G::S : 0, px = MODE == NG_DX ? (int)blockIdx.z % G::S : 0;
+  RingRows ring;
+  if constexpr (U8) ring.init(a.sa, a.sa.tau_ptr ? *a.sa.tau_ptr : 0);
+  // pair p of row quads: 4 lanes along the row's quads (64 contiguous bytes), then 16 k pairs
+  auto pair_q = [](int p, int nrowq) { (void)nrowq; return ((p >> 2) / (BK / 2)) * 4 + (p & 3); };
+  auto pair_k = [](int p) { return ((p >> 2) % (BK / 2)) * 2; };
+
+  int ar[AQ], ac[AQ];          // A_KC: tile row m, k offset; else: reduction row, m offset
+  bool aval[AQ];
+  int64_t abase[AQ];
+  int ai[AQ], aj[AQ];
+  int mk[AQ][3];
+#pragma unroll
+  for (int i = 0; i < AQ; ++i) {
+    if constexpr (A_KC) {
+      const int q = tid + 256 * i;
+      ar[i] = q >> 3; ac[i] = (q & 7) * 4;
+    } else {
+      const int pp = tid + 256 * (i >> 1);
+      ar[i] = pair_k(pp) + (i & 1); ac[i] = pair_q(pp, BM / 4) * 4;
+    }
+    abase[i] = 0; ai[i] = aj[i] = 0;
+    if constexpr (A_KC) {
+      const int m = m0 + ar[i];
+      aval[i] = m < a.M;
+      const int mm = aval[i] ? m : 0;
+      if constexpr (MODE == NG_DX) {
+        const int b = mm / (NI * NJ), r = mm - b * (NI * NJ);
+        abase[i] = b; ai[i] = r / NJ; aj[i] = r - (r / NJ) * NJ;
+      } else {
+        const int b = mm / P, pos = mm - b * P, oy = pos / G::OW, ox = pos - oy * G::OW;
+        abase[i] = (((int64_t)b * G::H + oy * G::S) * G::W + ox * G::S) * G::C;
+      }
+    } else {
+      const int m = m0 + ac[i];
+      aval[i] = m < a.M;
+      const int mm = aval[i] ? m : 0;
+      if constexpr (U8) {
+        mk[i][0] = (mm >> 3) & 7; mk[i][1] = mm & 7; mk[i][2] = mm >> 6;
+      } else {
+        mk[i][0] = mm / (G::KW * G::C);
+        mk[i][1] = (mm / G::C) % G::KW;
+        mk[i][2] = mm % G::C;
+      }
+    }
+  }
+  int br[BQ], bc[BQ];          // B_NC: k row, n offset; else: n row, k offset
+  bool bok[BQ];
+#pragma unroll
+  for (int j = 0; j < BQ; ++j) {
+    if constexpr (B_NC) {
+      const int pp = tid + 256 * (j >> 1);
+      bok[j] = pp < BPAIRS;
+      br[j] = pair_k(pp) + (j & 1); bc[j] = pair_q(pp, BN / 4) * 4;
+    } else {
+      const int q = tid + 256 * j;
+      bok[j] = true;
+      br[j] = q >> 3; bc[j] = (q & 7) * 4;
+    }
+  }
+
+  auto load_a = [&](int i, int k0) -> f32x4 {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (A_KC) {
+      const int k = k0 + ac[i];
+      if (!aval[i] || k >= kend) return v;
+      if constexpr (MODE == NG_FWD) {
+        const int kh = k / (G::KW * G::C), rem = k - kh * (G::KW * G::C), kw = rem / G::C, c0 = rem - kw * G::C;
+        v = *(const f32x4*)(a.X + abase[i] + (kh * G::W + kw) * G::C + c0);
+      } else {
+        const int th = k / (TW * G::OC), rem = k - th * (TW * G::OC), tw = rem / G::OC, oc0 = rem - tw * G::OC;
+        const int oy = ai[i] - th, ox = aj[i] - tw;
+        if (oy >= 0 && oy < G::OH && ox >= 0 && ox < G::OW)
+          v = *(const f32x4*)(a.dY + ((abase[i] * G::OH + oy) * G::OW + ox) * G::OC + oc0);
+      }
+    } else {
+      const int r = k0 + ar[i];
+      if (!aval[i] || r >= kend) return v;
+      const int b = r / P, pos = r - b * P, oy = pos / G::OW, ox = pos - oy * G::OW;
+      const int y = oy * G::S + mk[i][0], x = ox * G::S + mk[i][1];
+      if constexpr (U8) {
+        const int t = ring.step_of(b);
+        const uint32_t d = *(const uint32_t*)(ring.plane(b - t * ring.E, t, mk[i][2]) + y * IMG + x);
+        v[0] = (float)(d & 255u); v[1] = (float)((d >> 8) & 255u); v[2] = (float)((d >> 16) & 255u); v[3] = (float)(d >> 24);
+      } else {
+        v = *(const f32x4*)(a.X + (((int64_t)b * G::H + y) * G::W + x) * G::C + mk[i][2]);
+      }
+    }
+    return v;
+  };
+  auto load_b = [&](int j, int k0) -> f32x4 {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (!bok[j]) return v;
+    if constexpr (B_NC) {
+      const int k = k0 + br[j], n = n0 + bc[j];
+      if (k >= kend || n >= a.N) return v;
+      v = DW ? *(const f32x4*)(a.dY + (int64_t)k * G::OC + n) : *(const f32x4*)(a.Wt + (int64_t)k * G::OC + n);
+    } else {
+      const int n = n0 + br[j], k = k0 + bc[j];
+      if (n >= a.N || k >= kend) return v;
+      const int th = k / (TW * G::OC), rem = k - th * (TW * G::OC), tw = rem / G::OC, oc0 = rem - tw * G::OC;
+      const int kh = py + G::S * th, kw = px + G::S * tw;
+      v = *(const f32x4*)(a.Wt + (((int64_t)kh * G::KW + kw) * G::C + n) * G::OC + oc0);
+    }
+    return v;
+  };
+
+  // bias gradient: column sums of dY from the B registers (before the split), one fixed order
+  const bool do_colsum = DW && a.colsum && blockIdx.y == 0;
+  constexpr int CSN = BQ / 2 > 0 ? BQ / 2 : 1;
+  float cs[CSN][4];
+#pragma unroll
+  for (int jj = 0; jj < CSN; ++jj)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) cs[jj][c] = 0.f;
+
+  auto store = [&](int buf, const f32x4 (&ra)[AQ], const f32x4 (&rbv)[BQ]) {
+    if constexpr (A_KC) {
+#pragma unroll
+      for (int i = 0; i < AQ; ++i) {
+        uint32_t lo[TA], hi[TA];
+        nat_split2<TA>(ra[i][0], ra[i][1], lo);
+        nat_split2<TA>(ra[i][2], ra[i][3], hi);
+#pragma unroll
+        for (int t = 0; t < TA; ++t) *(uint2*)&As[buf][t][ar[i]][ac[i]] = make_uint2(lo[t], hi[t]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < AQ; i += 2)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          uint32_t w[TA];
+          nat_split2<TA>(ra[i][c], ra[i + 1][c], w);
+#pragma unroll
+          for (int t = 0; t < TA; ++t) *(uint32_t*)&As[buf][t][ac[i] + c][ar[i]] = w[t];
+        }
+    }
+    if constexpr (B_NC) {
+#pragma unroll
+      for (int j = 0; j < BQ; j += 2) {
+        if (!bok[j]) continue;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          uint32_t w[3];
+          nat_split2<3>(rbv[j][c], rbv[j + 1][c], w);
+#pragma unroll
+          for (int t = 0; t < 3; ++t) *(uint32_t*)&Bs[buf][t][bc[j] + c][br[j]] = w[t];
+          if (DW && do_colsum) cs[j / 2][c] += rbv[j][c] + rbv[j + 1][c];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < BQ; ++j) {
+        uint32_t lo[3], hi[3];
+        nat_split2<3>(rbv[j][0], rbv[j][1], lo);
+        nat_split2<3>(rbv[j][2], rbv[j][3], hi);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) *(uint2*)&Bs[buf][t][br[j]][bc[j]] = make_uint2(lo[t], hi[t]);
+      }
+    }
+  };
+
+  f32x16 acc = {};
+  const int r = lane & 31, h = lane >> 5;
+  auto load_all = [&](int k0, f32x4 (&ra)[AQ], f32x4 (&rbv)[BQ]) {
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) ra[i] = load_a(i, k0);
+#pragma unroll
+    for (int j = 0; j < BQ; ++j) rbv[j] = load_b(j, k0);
+  };
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 af[TA], bv[3];
+#pragma unroll
+      for (int t = 0; t < TA; ++t) af[t] = *(const bf16x8*)&As[buf][t][wm * 32 + r][16 * s + 8 * h];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) bv[t] = *(const bf16x8*)&Bs[buf][t][wn * 32 + r][16 * s + 8 * h];
+      if constexpr (TA == 1) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bv[2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bv[1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bv[0], acc, 0, 0, 0);
+      } else {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bv[2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bv[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bv[1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bv[1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bv[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bv[0], acc, 0, 0, 0);
+      }
+    }
+  };
+  if constexpr (NBUF == 1) {
+    f32x4 ra[AQ], rbv[BQ];
+    load_all(kbeg, ra, rbv);
+    store(0, ra, rbv);
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+      const bool more = k0 + BK < kend;
+      if (more) load_all(k0 + BK, ra, rbv);
+      compute(0);
+      __syncthreads();
+      if (more) {
+        store(0, ra, rbv);
+        __syncthreads();
+      }
+    }
+  } else if constexpr (DW) {
+    f32x4 ra0[AQ], rb0[BQ], ra1[AQ], rb1[BQ];
+    load_all(kbeg, ra0, rb0);
+    store(0, ra0, rb0);
+    if (kbeg + BK < kend) load_all(kbeg + BK, ra1, rb1);
+    if (kbeg + 2 * BK < kend) load_all(kbeg + 2 * BK, ra0, rb0);
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += 2 * BK) {
+      compute(0);
+      if (k0 + BK < kend) {
+        store(NBUF - 1, ra1, rb1);
+        if (k0 + 3 * BK < kend) load_all(k0 + 3 * BK, ra1, rb1);
+      }
+      __syncthreads();
+      if (k0 + BK >= kend) break;
+      compute(NBUF - 1);
+      if (k0 + 2 * BK < kend) {
+        store(0, ra0, rb0);
+        if (k0 + 4 * BK < kend) load_all(k0 + 4 * BK, ra0, rb0);
+      }
+      __syncthreads();
+    }
+  } else {
+    f32x4 ra[AQ], rbv[BQ];
+    load_all(kbeg, ra, rbv);
+    store(0, ra, rbv);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+      const bool more = k0 + BK < kend;
+      if (more) load_all(k0 + BK, ra, rbv);
+      compute(buf);
+      if (more) store(buf ^ (NBUF - 1), ra, rbv);
+      __syncthreads();
+      buf ^= NBUF - 1;
+    }
+  }
+
+  const int col = n0 + wn * 32 + (lane & 31);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int row = m0 + wm * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+    if (row >= a.M || col >= a.N) continue;
+    float v = acc[q];
+    if constexpr (MODE == NG_FWD) {
+      if (split) {
+        a.slab[((int64_t)blockIdx.z * a.M + row) * a.N + col] = v;
+        continue;
+      }
+      a.Y[(int64_t)row * a.N + col] = fmaxf(v + a.bias[col], 0.f);
+    } else if constexpr (MODE == NG_DX) {
+      const int b = row / (NI * NJ), rr = row - b * (NI * NJ), i = rr / NJ, j = rr - (rr / NJ) * NJ;
+      const int64_t o = (((int64_t)b * G::H + py + G::S * i) * G::W + px + G::S * j) * G::C + col;
+      a.Y[o] = a.X[o] > 0.f ? v : 0.f;
+    } else {
+      const int trow = MODE == NG_DW1 ? ((((row >> 3) & 7) * 8 + (row & 7)) * 4 + (row >> 6)) : row;
+      a.slab[((int64_t)blockIdx.z * a.M + trow) * a.N + col] = v;
+    }
+  }
+  if constexpr (DW) {
+    if (do_colsum) {      // (block-uniform) per-pair partials through LDS, summed over the k pairs in order
+      float* red = (float*)&As[0][0][0][0];
+#pragma unroll
+      for (int j = 0; j < BQ; j += 2) {
+        const int pp = tid + 256 * (j >> 1);
+        if (pp < BPAIRS) *(f32x4*)&red[pp * 4] = (f32x4){cs[j / 2][0], cs[j / 2][1], cs[j / 2][2], cs[j / 2][3]};
+      }
+      __syncthreads();
+      if (tid < BN && n0 + tid < a.N) {
+        const int nq = tid >> 2, c = tid & 3;
+        float sum = 0.f;
+        for (int kp = 0; kp < BK / 2; ++kp) sum += red[((((nq >> 2) * (BK / 2) + kp) << 2) | (nq & 3)) * 4 + c];
+        a.colsum[(int64_t)blockIdx.z * a.N + n0 + tid] = sum;
+      }
+    }
+  }
+}
+
+template <int MODE, int LAYER, int BN, int TA>
+static int nat_go_bf(const NatGemm& a, unsigned gz, hipStream_t s, bool one_buf) {
+  constexpr int BM = 4096 / BN;
+  if (a.M <= 0 || a.N <= 0) return 0;
+  const dim3 grid((unsigned)((a.N + BN - 1) / BN), (unsigned)((a.M + BM - 1) / BM), gz);
+  if (one_buf)
+    hipLaunchKernelGGL((k_nat_gemm_bf<MODE, LAYER, BN, TA, 1>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_nat_gemm_bf<MODE, LAYER, BN, TA, 2>), grid, dim3(256), 0, s, a);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
 // conv1 forward on the bf16 matrix cores.  A u8 pixel is exact in bf16, and the fp32 weight is
 // three round-to-nearest bf16 terms (w = hi + mid + lo to ~2^-24 relative, as the NIPS conv1,
 // net_fwd.hip): acc += x hi + x mid + x lo, every product exact in the fp32 accumulator -- three
@@ -534,6 +890,11 @@ static int fc_split(int64_t B) { return a3c_gemm_effective_split(NT_FLAT, a3c_ge
 // conv2 / conv3 forward: few output tiles at the rollout's B = E (324 / 196 of 64 x 64 at 256
 // envs), each a long K chain -- split K in two so twice the workgroups run half the chain
 #define NAT_FWD_SPLIT 2
+// passes on the bf16 matrix cores / with one LDS buffer (bits NAT_*; measured per pass)
+// (tools/r6/nat_bf.sh, r6bf3: the weight gradients of conv2 / conv3 stay on fp32: their row-pair
+// LDS stores and occupancy cost more than the MFMA saves)
+#define NAT_BF_DEFAULT ((1 << NAT_C2F) | (1 << NAT_C3F) | (1 << NAT_C3X) | (1 << NAT_C2X) | (1 << NAT_C1W))
+#define NAT_BF1_DEFAULT ((1 << NAT_C2F) | (1 << NAT_C3X) | (1 << NAT_C2X))
 
 static int64_t nat_fwd_slab_floats(int64_t B) {
   const int sp = fc_split(B);
@@ -542,6 +903,15 @@ static int64_t nat_fwd_slab_floats(int64_t B) {
   return ((fc > cv ? fc : cv) + 63) / 64 * 64;
 }
 int64_t a3c_nat_fwd_ws_floats(int64_t B) { return nat_fwd_slab_floats(B) + A3C_NAT_W1T_BYTES / 4; }
+// which passes run on the bf16 matrix cores (bit NAT_*) and which of those with one LDS buffer
+static bool nat_bf(int pass) {
+  static const long long v = A3C_AB_KNOB("A3C_NAT_BF", NAT_BF_DEFAULT);
+  return (v >> pass) & 1;
+}
+static bool nat_bf1(int pass) {
+  static const long long v = A3C_AB_KNOB("A3C_NAT_BF1", NAT_BF1_DEFAULT);
+  return (v >> pass) & 1;
+}
 static int nat_c1_bf() {
   static const int v = (int)A3C_AB_KNOB("A3C_NAT_C1_BF", 1);   // A/B: 0 = the fp32 MFMA conv1 forward
   return v;
@@ -554,7 +924,9 @@ static int nat_fwd_split(NatGemm a, float* fws, hipStream_t s) {
   a.kchunk = ((a.K + S - 1) / S + 31) / 32 * 32;
   const int ns = (a.K + a.kchunk - 1) / a.kchunk;
   a.slab = fws;
-  int rc = nat_go<NG_FWD, LAYER, 64>(a, (unsigned)ns, s);
+  constexpr int pass = LAYER == 2 ? NAT_C2F : NAT_C3F;
+  int rc = nat_bf(pass) ? nat_go_bf<NG_FWD, LAYER, 64, 3>(a, (unsigned)ns, s, nat_bf1(pass))
+                        : nat_go<NG_FWD, LAYER, 64>(a, (unsigned)ns, s);
   if (rc) return rc;
   GemmArgs g = {};
   g.slab = fws; g.nsplit = ns; g.M = a.M; g.N = a.N; g.C = a.Y; g.ldc = a.N; g.epi = EPI_BIAS_RELU; g.bias = a.bias;
@@ -607,23 +979,28 @@ int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const Stat
     case NAT_C3W:     // dW3 (+ db3) over the (sample, pixel) rows
       a.X = l2; a.dY = bws + p.dl3; a.slab = bws + p.s3; a.colsum = bws + p.c3;
       a.M = NT_K3; a.N = NT3_N; a.K = (int)(B * NT3_P); a.kchunk = p.kc3;
-      return nat_go<NG_DW, 3, 64>(a, (unsigned)p.ns3, s);
+      return nat_bf(NAT_C3W) ? nat_go_bf<NG_DW, 3, 64, 3>(a, (unsigned)p.ns3, s, nat_bf1(NAT_C3W))
+                           : nat_go<NG_DW, 3, 64>(a, (unsigned)p.ns3, s);
     case NAT_C3X:     // dl2 = col2im(dl3 W3^T) * (l2 > 0)
       a.X = l2; a.dY = bws + p.dl3; a.Wt = P + L.off[N_L3W]; a.Y = bws + p.dl2;
       a.M = (int)(B * NT2_P); a.N = NT2_N; a.K = 3 * 3 * NT3_N;
-      return nat_go<NG_DX, 3, 64>(a, 1, s);
+      return nat_bf(NAT_C3X) ? nat_go_bf<NG_DX, 3, 64, 3>(a, 1, s, nat_bf1(NAT_C3X))
+                           : nat_go<NG_DX, 3, 64>(a, 1, s);
     case NAT_C2W:
       a.X = l1; a.dY = bws + p.dl2; a.slab = bws + p.s2; a.colsum = bws + p.c2;
       a.M = NT_K2; a.N = NT2_N; a.K = (int)(B * NT2_P); a.kchunk = p.kc2;
-      return nat_go<NG_DW, 2, 64>(a, (unsigned)p.ns2, s);
+      return nat_bf(NAT_C2W) ? nat_go_bf<NG_DW, 2, 64, 3>(a, (unsigned)p.ns2, s, nat_bf1(NAT_C2W))
+                           : nat_go<NG_DW, 2, 64>(a, (unsigned)p.ns2, s);
     case NAT_C2X:     // dl1 = col2im(dl2 W2^T) * (l1 > 0), per stride-2 parity class
       a.X = l1; a.dY = bws + p.dl2; a.Wt = P + L.off[N_L2W]; a.Y = bws + p.dl1;
       a.M = (int)(B * (NT1_O / 2) * (NT1_O / 2)); a.N = NT1_N; a.K = 2 * 2 * NT2_N;
-      return nat_go<NG_DX, 2, 32>(a, 4, s);
+      return nat_bf(NAT_C2X) ? nat_go_bf<NG_DX, 2, 32, 3>(a, 4, s, nat_bf1(NAT_C2X))
+                           : nat_go<NG_DX, 2, 32>(a, 4, s);
     case NAT_C1W:     // dW1 (+ db1) from the u8 planes (the input needs no gradient)
       a.sa = sa; a.dY = bws + p.dl1; a.slab = bws + p.s1; a.colsum = bws + p.c1;
       a.M = NT_K1; a.N = NT1_N; a.K = (int)(B * NT1_P); a.kchunk = p.kc1;
-      return nat_go<NG_DW1, 1, 32>(a, (unsigned)p.ns1, s);
+      return nat_bf(NAT_C1W) ? nat_go_bf<NG_DW1, 1, 32, 1>(a, (unsigned)p.ns1, s, nat_bf1(NAT_C1W))
+                           : nat_go<NG_DW1, 1, 32>(a, (unsigned)p.ns1, s);
     default:
       return a3c_set_error(A3C_ERR_INVALID, "a3c_nat_pass_launch", "unknown pass");
   }
