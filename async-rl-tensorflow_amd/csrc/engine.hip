@@ -238,11 +238,10 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   e->fc_split = 1;
   e->fc_split = A3C_KNOB("A3C_FC_SPLIT", e->fc_split) != 0;
   e->frame84 = cfg->frame84 ? 1 : 0;
-  // the nature trunk (network.py:30-42) runs its own passes (nature.hip): no NIPS fusions; the
-  // screen is its own launch after each step's head, the exchange one-phase
+  // the nature trunk (network.py:30-42) runs its own passes (nature.hip): of the NIPS fusions only
+  // the head + act + screen kernel (its 512-wide form), the exchange one-phase
   e->nat = L.trunk == A3C_TRUNK_NATURE ? 1 : 0;
   if (e->nat) {
-    e->fused_screen = 0;
     e->fuse_conv = 0;
     e->fc_split = 0;
     if (e->ext) {

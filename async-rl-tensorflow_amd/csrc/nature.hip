@@ -46,7 +46,33 @@ struct NatGemm {
   int kchunk;          // NG_DW*: reduction rows per split (a multiple of the K slice); NG_FWD: > 0 splits K
                        // over grid z into slab partials (the fold applies bias + ReLU)
   float scale;         // NG_FWD1: 1/255
+  int xcd;             // NG_DW*, NG_DX: XCD-grouped tile order (nat_tile_of)
 };
+
+// The dispatcher deals workgroups round-robin over the 8 XCDs (linear id % 8), each with its own
+// L2.  The workgroups that read the same operands -- the m-tiles of one reduction chunk (dW: the
+// same dY rows and overlapping patches), the stride-parity classes of one m-tile (dX: the same dY
+// rows) -- would land on 8 different XCDs and each fetch them from HBM; here a group of them takes
+// consecutive ids of one XCD instead (grid x extent 1: id = y + Y z).
+template <int MODE>
+__device__ inline void nat_tile_of(int xcd, int& by, int& bz) {
+  by = (int)blockIdx.y; bz = (int)blockIdx.z;
+  if (!xcd || gridDim.x != 1 || MODE == NG_FWD1 || MODE == NG_FWD) return;
+  constexpr bool DWM = MODE == NG_DW || MODE == NG_DW1;
+  const int G = DWM ? (int)gridDim.z : (int)gridDim.y;     // groups sharing data
+  const int S = DWM ? (int)gridDim.y : (int)gridDim.z;     // workgroups per group
+  const int L = by + (int)gridDim.y * bz;
+  const int full = G / 8 * 8;
+  int g, m;
+  if (L < full * S) {
+    const int blk = L / (8 * S), rem = L - blk * 8 * S;
+    m = rem / 8; g = blk * 8 + rem % 8;
+  } else {
+    const int cl = G - full, rem = L - full * S;
+    m = rem / cl; g = full + rem % cl;
+  }
+  if (DWM) { bz = g; by = m; } else { by = g; bz = m; }
+}
 
 // the frame-ring planes of sample b = t E + e without 64-bit divisions: slot0 = the ring slot of
 // plane 0 of t = 0, reduced once per launch
@@ -93,11 +119,13 @@ __global__ void __launch_bounds__(256) k_nat_gemm(NatGemm a) {
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + LP];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  int by, bz;
+  nat_tile_of<MODE>(a.xcd, by, bz);
+  const int m0 = by * BM, n0 = blockIdx.x * BN;
   const bool split = DW || (MODE == NG_FWD && a.kchunk > 0);
-  const int kbeg = split ? (int)blockIdx.z * a.kchunk : 0;
+  const int kbeg = split ? bz * a.kchunk : 0;
   const int kend = split ? min(a.K, kbeg + a.kchunk) : a.K;
-  const int py = MODE == NG_DX ? (int)blockIdx.z / G::S : 0, px = MODE == NG_DX ? (int)blockIdx.z % G::S : 0;
+  const int py = MODE == NG_DX ? bz / G::S : 0, px = MODE == NG_DX ? bz % G::S : 0;
   RingRows ring;
   if constexpr (U8) ring.init(a.sa, a.sa.tau_ptr ? *a.sa.tau_ptr : 0);
 
@@ -226,7 +254,7 @@ __global__ void __launch_bounds__(256) k_nat_gemm(NatGemm a) {
 
   f32x16 acc = {};
   float csum = 0.f;
-  const bool do_colsum = DW && a.colsum && blockIdx.y == 0 && tid < BN;
+  const bool do_colsum = DW && a.colsum && by == 0 && tid < BN;
   const int kh = lane >> 5, c = lane & 31;
   auto load_all = [&](int k0, f32x4 (&ra)[AQ], f32x4 (&rbv)[BQ]) {
 #if defined(NAT_ABL) && NAT_ABL == 2      // measurement only: no operand loads
@@ -304,7 +332,7 @@ __global__ void __launch_bounds__(256) k_nat_gemm(NatGemm a) {
     float v = acc[r];
     if constexpr (MODE == NG_FWD1 || MODE == NG_FWD) {
       if (MODE == NG_FWD && split) {            // a K-split partial: the fold adds bias + ReLU
-        a.slab[((int64_t)blockIdx.z * a.M + row) * a.N + col] = v;
+        a.slab[((int64_t)bz * a.M + row) * a.N + col] = v;
         continue;
       }
       v = fmaxf((MODE == NG_FWD1 ? v * a.scale : v) + a.bias[col], 0.f);
@@ -316,16 +344,21 @@ __global__ void __launch_bounds__(256) k_nat_gemm(NatGemm a) {
     } else {
       // conv1's m = (cin, kh, kw) -> the TF row (kh 8 + kw) 4 + cin of dW1 [8][8][4][32]
       const int trow = MODE == NG_DW1 ? ((((row >> 3) & 7) * 8 + (row & 7)) * 4 + (row >> 6)) : row;
-      a.slab[((int64_t)blockIdx.z * a.M + trow) * a.N + col] = v;
+      a.slab[((int64_t)bz * a.M + trow) * a.N + col] = v;
     }
   }
-  if (do_colsum && n0 + tid < a.N) a.colsum[(int64_t)blockIdx.z * a.N + n0 + tid] = csum;
+  if (do_colsum && n0 + tid < a.N) a.colsum[(int64_t)bz * a.N + n0 + tid] = csum;
 }
 
+static int nat_xcd() {
+  static const int v = (int)A3C_AB_KNOB("A3C_NAT_XCD", 1);   // A/B: 0 = the hardware tile order
+  return v;
+}
 template <int MODE, int LAYER, int BN>
-static int nat_go(const NatGemm& a, unsigned gz, hipStream_t s) {
+static int nat_go(NatGemm a, unsigned gz, hipStream_t s) {
   constexpr int BM = 4096 / BN;
   if (a.M <= 0 || a.N <= 0) return 0;
+  a.xcd = nat_xcd();
   const dim3 grid((unsigned)((a.N + BN - 1) / BN), (unsigned)((a.M + BM - 1) / BM), gz);
   hipLaunchKernelGGL((k_nat_gemm<MODE, LAYER, BN>), grid, dim3(256), 0, s, a);
   A3C_CHECK(hipGetLastError());
@@ -386,11 +419,13 @@ __global__ void __launch_bounds__(256) k_nat_gemm_bf(NatGemm a) {
   __shared__ __attribute__((aligned(16))) uint16_t Bs[NBUF][3][BN][LD];    // two barriers per slice
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  int by, bz;
+  nat_tile_of<MODE>(a.xcd, by, bz);
+  const int m0 = by * BM, n0 = blockIdx.x * BN;
   const bool split = DW || (MODE == NG_FWD && a.kchunk > 0);
-  const int kbeg = split ? (int)blockIdx.z * a.kchunk : 0;
+  const int kbeg = split ? bz * a.kchunk : 0;
   const int kend = split ? min(a.K, kbeg + a.kchunk) : a.K;
-  const int py = MODE == NG_DX ? (int)blockIdx.z / G::S : 0, px = MODE == NG_DX ? (int)blockIdx.z % G::S : 0;
+  const int py = MODE == NG_DX ? bz / G::S : 0, px = MODE == NG_DX ? bz % G::S : 0;
   RingRows ring;
   if constexpr (U8) ring.init(a.sa, a.sa.tau_ptr ? *a.sa.tau_ptr : 0);
   // pair p of row quads: 4 lanes along the row's quads (64 contiguous bytes), then 16 k pairs
@@ -498,7 +533,7 @@ __global__ void __launch_bounds__(256) k_nat_gemm_bf(NatGemm a) {
   };
 
   // bias gradient: column sums of dY from the B registers (before the split), one fixed order
-  const bool do_colsum = DW && a.colsum && blockIdx.y == 0;
+  const bool do_colsum = DW && a.colsum && by == 0;
   constexpr int CSN = BQ / 2 > 0 ? BQ / 2 : 1;
   float cs[CSN][4];
 #pragma unroll
@@ -643,7 +678,7 @@ __global__ void __launch_bounds__(256) k_nat_gemm_bf(NatGemm a) {
     float v = acc[q];
     if constexpr (MODE == NG_FWD) {
       if (split) {
-        a.slab[((int64_t)blockIdx.z * a.M + row) * a.N + col] = v;
+        a.slab[((int64_t)bz * a.M + row) * a.N + col] = v;
         continue;
       }
       a.Y[(int64_t)row * a.N + col] = fmaxf(v + a.bias[col], 0.f);
@@ -653,7 +688,7 @@ __global__ void __launch_bounds__(256) k_nat_gemm_bf(NatGemm a) {
       a.Y[o] = a.X[o] > 0.f ? v : 0.f;
     } else {
       const int trow = MODE == NG_DW1 ? ((((row >> 3) & 7) * 8 + (row & 7)) * 4 + (row >> 6)) : row;
-      a.slab[((int64_t)blockIdx.z * a.M + trow) * a.N + col] = v;
+      a.slab[((int64_t)bz * a.M + trow) * a.N + col] = v;
     }
   }
   if constexpr (DW) {
@@ -669,16 +704,17 @@ __global__ void __launch_bounds__(256) k_nat_gemm_bf(NatGemm a) {
         const int nq = tid >> 2, c = tid & 3;
         float sum = 0.f;
         for (int kp = 0; kp < BK / 2; ++kp) sum += red[((((nq >> 2) * (BK / 2) + kp) << 2) | (nq & 3)) * 4 + c];
-        a.colsum[(int64_t)blockIdx.z * a.N + n0 + tid] = sum;
+        a.colsum[(int64_t)bz * a.N + n0 + tid] = sum;
       }
     }
   }
 }
 
 template <int MODE, int LAYER, int BN, int TA>
-static int nat_go_bf(const NatGemm& a, unsigned gz, hipStream_t s, bool one_buf) {
+static int nat_go_bf(NatGemm a, unsigned gz, hipStream_t s, bool one_buf) {
   constexpr int BM = 4096 / BN;
   if (a.M <= 0 || a.N <= 0) return 0;
+  a.xcd = nat_xcd();
   const dim3 grid((unsigned)((a.N + BN - 1) / BN), (unsigned)((a.M + BM - 1) / BM), gz);
   if (one_buf)
     hipLaunchKernelGGL((k_nat_gemm_bf<MODE, LAYER, BN, TA, 1>), grid, dim3(256), 0, s, a);
@@ -1042,6 +1078,9 @@ int a3c_nat_forward_launch(const NetLayout& L, const float* P, const StateAddr& 
     const int rc = a3c_nat_pass_launch(pass, L, P, sa, B, l1, l2, l3, l4, w1t, ws, nullptr, s);
     if (rc) return rc;
   }
+  if (sel.mode >= 0 && sel.env_on && sel.pool)   // the engine's rollout step: head + act + Environment.screen
+    return a3c_head_screen_wide_launch(l4, P + L.off[N_HW], P + L.off[N_HB], P + L.off[N_VW], P + L.off[N_VB], L.A,
+                                       L.zs, B, z, sel, s);
   hipLaunchKernelGGL(k_nat_head, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, l4, B, P + L.off[N_HW],
                      P + L.off[N_HB], P + L.off[N_VW], P + L.off[N_VB], L.A, L.zs, z, sel);
   A3C_CHECK(hipGetLastError());

@@ -498,6 +498,8 @@ __global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ h3, 
 // engine rollout step tail, one workgroup per env: head + action draw (wave 0) while wave 1
 // runs the env act up to the frame (env_act_pre: nothing but the frame depends on the action);
 // returns the post-act frame (pool index) of env b
+// (W: the width of the layer below the heads -- FC, or NT_FC for the nature trunk)
+template <int W = FC>
 __device__ inline int32_t head_act_env(const float* __restrict__ h3, const float* __restrict__ Wp,
                                        const float* __restrict__ bp, const float* __restrict__ Wv,
                                        const float* __restrict__ bv, int A, int zs, float* __restrict__ z,
@@ -513,8 +515,14 @@ __device__ inline int32_t head_act_env(const float* __restrict__ h3, const float
     u32x4 x;
     // the action draw does not depend on the head: computed under its load latency
     // (hrow: the layer-output row, already folded into LDS by the caller)
-    const float myz = hrow ? head_row(hrow, 0, Wp, bp, Wv, bv, A, lane, [&]() { x = action_draw(sel, b, tau); })
-                           : head_row(h3, b, Wp, bp, Wv, bv, A, lane, [&]() { x = action_draw(sel, b, tau); });
+    float myz;
+    if constexpr (W == FC) {
+      myz = hrow ? head_row(hrow, 0, Wp, bp, Wv, bv, A, lane, [&]() { x = action_draw(sel, b, tau); })
+                 : head_row(h3, b, Wp, bp, Wv, bv, A, lane, [&]() { x = action_draw(sel, b, tau); });
+    } else {
+      auto mid = [&]() { x = action_draw(sel, b, tau); };
+      myz = head_row<decltype(mid), W>(h3, b, Wp, bp, Wv, bv, A, lane, mid);
+    }
     if (dbg) {
       if (lane == 0) dbg[1] = __builtin_readcyclecounter() + (uint64_t)(myz * 0.f);
     } else if (lane < zs) {
@@ -565,7 +573,7 @@ __device__ inline int32_t head_act_env(const float* __restrict__ h3, const float
 // head + action draw + env act (head_act_env), then the whole workgroup computes
 // Environment.screen (environment.py:49-53, bit-exact) of the post-act frame straight from the
 // HBM pool into the env's frame-ring slot
-template <int HS_THREADS>
+template <int HS_THREADS, int W = FC>
 __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restrict__ h3,
                                                             const float* __restrict__ Wp,
                                                             const float* __restrict__ bp,
@@ -581,7 +589,7 @@ __global__ void __launch_bounds__(HS_THREADS) k_head_screen(const float* __restr
   dbg = blockIdx.x == HS_TIMES ? (uint64_t*)z : nullptr;
   if (dbg && threadIdx.x == 0) dbg[0] = __builtin_readcyclecounter();
 #endif
-  const int32_t frame = head_act_env(h3, Wp, bp, Wv, bv, A, zs, z, sel, b, tau, dbg);
+  const int32_t frame = head_act_env<W>(h3, Wp, bp, Wv, bv, A, zs, z, sel, b, tau, dbg);
   uint8_t* slot = sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE;
   if (sel.frame84)
     atari::copy_frame84<HS_THREADS>(sel.pool + (int64_t)frame * PLANE, slot);
@@ -768,6 +776,21 @@ int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* 
 
 // skip_conv12: conv1 + conv2 of these states already ran (fused into the previous step's
 // k_head_screen_conv12); next: fuse the next states' conv1 + conv2 into this step's head + screen
+// the same for the nature trunk's 512-wide fc output (nature.hip's rollout steps)
+int a3c_head_screen_wide_launch(const float* l4, const float* Wp, const float* bp, const float* Wv, const float* bv,
+                                int A, int zs, int64_t B, float* z, const HeadSelect& sel, hipStream_t s) {
+  static const int env_t = (int)A3C_AB_KNOB("A3C_HS_THREADS", 0);
+  const int nt = env_t ? env_t : (a3c_shared_gpu() ? 512 : 1024);
+  if (nt == 1024)
+    hipLaunchKernelGGL((k_head_screen<1024, 512>), dim3((unsigned)B), dim3(1024), SCREEN_FRAME_SMEM, s, l4, Wp, bp,
+                       Wv, bv, A, zs, z, sel);
+  else
+    hipLaunchKernelGGL((k_head_screen<512, 512>), dim3((unsigned)B), dim3(512), SCREEN_FRAME_SMEM, s, l4, Wp, bp, Wv,
+                       bv, A, zs, z, sel);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
 int a3c_head_screen_conv12_launch(const NetLayout& L, const float* P, const float* act_l3, int64_t B, float* z,
                                   const HeadSelect& sel, const Conv12Next& nx, hipStream_t s);
 int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* prep, const StateAddr& sa,
@@ -919,6 +942,10 @@ void a3c_conv12_set_smem() {
   (void)hipFuncSetAttribute((const void*)k_head_screen<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             SCREEN_FRAME_SMEM);
   (void)hipFuncSetAttribute((const void*)k_head_screen<1024>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SCREEN_FRAME_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_head_screen<512, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SCREEN_FRAME_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_head_screen<1024, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             SCREEN_FRAME_SMEM);
 }
 

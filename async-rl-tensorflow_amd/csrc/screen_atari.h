@@ -413,7 +413,7 @@ struct NoScreenMid {
 // mid(): work run by every thread while its frame loads are in flight, before the luminance
 // pass writes the scratch (it may use the first 51 KB of smem; it must not wait on vector memory)
 template <int NT, typename Mid = NoScreenMid>
-__device__ inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __restrict__ out, uint8_t* smem,
+__device__ __attribute__((always_inline)) inline void screen_frame(const uint8_t* __restrict__ rgb, uint8_t* __restrict__ out, uint8_t* smem,
                                     uint64_t* dbg = nullptr, uint16_t* lds_bf16 = nullptr, Mid mid = Mid(),
                                     int* kvs_at = nullptr) {
   uint8_t* gray = smem;
