@@ -922,10 +922,20 @@ static NatPlan nat_plan(const NetLayout& L, int64_t B) {
   return p;
 }
 
-static int fc_split(int64_t B) { return a3c_gemm_effective_split(NT_FLAT, a3c_gemm_plan_split((int)B, NT_FC, NT_FLAT, 512)); }
+static int fc_split(int64_t B) {
+  static const int v = (int)A3C_AB_KNOB("A3C_NAT_FC_SPLIT", 0);   // A/B: > 0 overrides the plan
+  return a3c_gemm_effective_split(NT_FLAT, v > 0 ? v : a3c_gemm_plan_split((int)B, NT_FC, NT_FLAT, 512));
+}
 // conv2 / conv3 forward: few output tiles at the rollout's B = E (324 / 196 of 64 x 64 at 256
-// envs), each a long K chain -- split K in two so twice the workgroups run half the chain
-#define NAT_FWD_SPLIT 2
+// envs), each a long K chain -- conv3 splits K in two so twice the workgroups run half the chain
+// (measured, r6sp1: conv2 28.5 us unsplit vs 30.2 split in 2, conv3 25.3 vs 23.2; 4-way loses on both)
+#define NAT_FWD_SPLIT(LAYER) ((LAYER) == 2 ? 1 : 2)
+#define NAT_FWD_SPLIT_MAX 4
+static int nat_fwd_split_n(int layer) {
+  static const int v = (int)A3C_AB_KNOB("A3C_NAT_FWD_SPLIT", 0);   // A/B: 1..4 for both layers
+  const int n = v > 0 ? v : NAT_FWD_SPLIT(layer);
+  return n > NAT_FWD_SPLIT_MAX ? NAT_FWD_SPLIT_MAX : n;
+}
 // passes on the bf16 matrix cores / with one LDS buffer (bits NAT_*; measured per pass)
 // (tools/r6/nat_bf.sh, r6bf3: the weight gradients of conv2 / conv3 stay on fp32: their row-pair
 // LDS stores and occupancy cost more than the MFMA saves)
@@ -935,7 +945,7 @@ static int fc_split(int64_t B) { return a3c_gemm_effective_split(NT_FLAT, a3c_ge
 static int64_t nat_fwd_slab_floats(int64_t B) {
   const int sp = fc_split(B);
   const int64_t fc = sp > 1 ? (int64_t)sp * B * NT_FC : 0;
-  const int64_t cv = (int64_t)NAT_FWD_SPLIT * B * (NT2_P * NT2_N > NT3_P * NT3_N ? NT2_P * NT2_N : NT3_P * NT3_N);
+  const int64_t cv = (int64_t)NAT_FWD_SPLIT_MAX * B * (NT2_P * NT2_N > NT3_P * NT3_N ? NT2_P * NT2_N : NT3_P * NT3_N);
   return ((fc > cv ? fc : cv) + 63) / 64 * 64;
 }
 int64_t a3c_nat_fwd_ws_floats(int64_t B) { return nat_fwd_slab_floats(B) + A3C_NAT_W1T_BYTES / 4; }
@@ -956,11 +966,15 @@ static int nat_c1_bf() {
 // a split conv forward: partials into fws, then the fold with bias + ReLU into Y (gemm.hip)
 template <int LAYER>
 static int nat_fwd_split(NatGemm a, float* fws, hipStream_t s) {
-  constexpr int S = NAT_FWD_SPLIT;
+  constexpr int pass = LAYER == 2 ? NAT_C2F : NAT_C3F;
+  const int S = nat_fwd_split_n(LAYER);
+  if (S == 1) {    // one K chain per tile: bias + ReLU in the tile's epilogue
+    a.kchunk = 0;
+    return nat_bf(pass) ? nat_go_bf<NG_FWD, LAYER, 64, 3>(a, 1, s, nat_bf1(pass)) : nat_go<NG_FWD, LAYER, 64>(a, 1, s);
+  }
   a.kchunk = ((a.K + S - 1) / S + 31) / 32 * 32;
   const int ns = (a.K + a.kchunk - 1) / a.kchunk;
   a.slab = fws;
-  constexpr int pass = LAYER == 2 ? NAT_C2F : NAT_C3F;
   int rc = nat_bf(pass) ? nat_go_bf<NG_FWD, LAYER, 64, 3>(a, (unsigned)ns, s, nat_bf1(pass))
                         : nat_go<NG_FWD, LAYER, 64>(a, (unsigned)ns, s);
   if (rc) return rc;
