@@ -394,7 +394,7 @@ __device__ inline void nat_split2(float x0, float x1, uint32_t (&o)[NT]) {
   }
 }
 
-template <int MODE, int LAYER, int BN, int TA, int NBUF>
+template <int MODE, int LAYER, int BN, int TA, int NBUF, int PF>
 __global__ void __launch_bounds__(256) k_nat_gemm_bf(NatGemm a) {
   using G = NG<LAYER>;
   constexpr int BM = 4096 / BN, BK = 32, LD = 40;
@@ -617,7 +617,32 @@ __global__ void __launch_bounds__(256) k_nat_gemm_bf(NatGemm a) {
       }
     }
   };
-  if constexpr (NBUF == 1) {
+  if constexpr (PF == 2) {
+    // two register sets: slice s + 2 loads while slice s computes (s + 1 waits in registers)
+    f32x4 ra0[AQ], rb0[BQ], ra1[AQ], rb1[BQ];
+    load_all(kbeg, ra0, rb0);
+    store(0, ra0, rb0);
+    if (kbeg + BK < kend) load_all(kbeg + BK, ra1, rb1);
+    if (kbeg + 2 * BK < kend) load_all(kbeg + 2 * BK, ra0, rb0);
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += 2 * BK) {
+      compute(0);
+      if constexpr (NBUF == 1) __syncthreads();
+      if (k0 + BK < kend) {
+        store(NBUF - 1, ra1, rb1);
+        if (k0 + 3 * BK < kend) load_all(k0 + 3 * BK, ra1, rb1);
+      }
+      __syncthreads();
+      if (k0 + BK >= kend) break;
+      compute(NBUF - 1);
+      if constexpr (NBUF == 1) __syncthreads();
+      if (k0 + 2 * BK < kend) {
+        store(0, ra0, rb0);
+        if (k0 + 4 * BK < kend) load_all(k0 + 4 * BK, ra0, rb0);
+      }
+      __syncthreads();
+    }
+  } else if constexpr (NBUF == 1) {
     f32x4 ra[AQ], rbv[BQ];
     load_all(kbeg, ra, rbv);
     store(0, ra, rbv);
@@ -632,28 +657,6 @@ __global__ void __launch_bounds__(256) k_nat_gemm_bf(NatGemm a) {
         __syncthreads();
       }
     }
-  } else if constexpr (DW) {
-    f32x4 ra0[AQ], rb0[BQ], ra1[AQ], rb1[BQ];
-    load_all(kbeg, ra0, rb0);
-    store(0, ra0, rb0);
-    if (kbeg + BK < kend) load_all(kbeg + BK, ra1, rb1);
-    if (kbeg + 2 * BK < kend) load_all(kbeg + 2 * BK, ra0, rb0);
-    __syncthreads();
-    for (int k0 = kbeg; k0 < kend; k0 += 2 * BK) {
-      compute(0);
-      if (k0 + BK < kend) {
-        store(NBUF - 1, ra1, rb1);
-        if (k0 + 3 * BK < kend) load_all(k0 + 3 * BK, ra1, rb1);
-      }
-      __syncthreads();
-      if (k0 + BK >= kend) break;
-      compute(NBUF - 1);
-      if (k0 + 2 * BK < kend) {
-        store(0, ra0, rb0);
-        if (k0 + 4 * BK < kend) load_all(k0 + 4 * BK, ra0, rb0);
-      }
-      __syncthreads();
-    }
   } else {
     f32x4 ra[AQ], rbv[BQ];
     load_all(kbeg, ra, rbv);
@@ -664,9 +667,9 @@ __global__ void __launch_bounds__(256) k_nat_gemm_bf(NatGemm a) {
       const bool more = k0 + BK < kend;
       if (more) load_all(k0 + BK, ra, rbv);
       compute(buf);
-      if (more) store(buf ^ (NBUF - 1), ra, rbv);
+      if (more) store(buf ^ 1, ra, rbv);
       __syncthreads();
-      buf ^= NBUF - 1;
+      buf ^= 1;
     }
   }
 
@@ -711,15 +714,19 @@ __global__ void __launch_bounds__(256) k_nat_gemm_bf(NatGemm a) {
 }
 
 template <int MODE, int LAYER, int BN, int TA>
-static int nat_go_bf(NatGemm a, unsigned gz, hipStream_t s, bool one_buf) {
+static int nat_go_bf(NatGemm a, unsigned gz, hipStream_t s, bool one_buf, bool pf2) {
   constexpr int BM = 4096 / BN;
   if (a.M <= 0 || a.N <= 0) return 0;
   a.xcd = nat_xcd();
   const dim3 grid((unsigned)((a.N + BN - 1) / BN), (unsigned)((a.M + BM - 1) / BM), gz);
-  if (one_buf)
-    hipLaunchKernelGGL((k_nat_gemm_bf<MODE, LAYER, BN, TA, 1>), grid, dim3(256), 0, s, a);
+  if (one_buf && pf2)
+    hipLaunchKernelGGL((k_nat_gemm_bf<MODE, LAYER, BN, TA, 1, 2>), grid, dim3(256), 0, s, a);
+  else if (one_buf)
+    hipLaunchKernelGGL((k_nat_gemm_bf<MODE, LAYER, BN, TA, 1, 1>), grid, dim3(256), 0, s, a);
+  else if (pf2)
+    hipLaunchKernelGGL((k_nat_gemm_bf<MODE, LAYER, BN, TA, 2, 2>), grid, dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((k_nat_gemm_bf<MODE, LAYER, BN, TA, 2>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_nat_gemm_bf<MODE, LAYER, BN, TA, 2, 1>), grid, dim3(256), 0, s, a);
   A3C_CHECK(hipGetLastError());
   return 0;
 }
@@ -937,10 +944,14 @@ static int nat_fwd_split_n(int layer) {
   return n > NAT_FWD_SPLIT_MAX ? NAT_FWD_SPLIT_MAX : n;
 }
 // passes on the bf16 matrix cores / with one LDS buffer (bits NAT_*; measured per pass)
-// (tools/r6/nat_bf.sh, r6bf3: the weight gradients of conv2 / conv3 stay on fp32: their row-pair
-// LDS stores and occupancy cost more than the MFMA saves)
-#define NAT_BF_DEFAULT ((1 << NAT_C2F) | (1 << NAT_C3F) | (1 << NAT_C3X) | (1 << NAT_C2X) | (1 << NAT_C1W))
-#define NAT_BF1_DEFAULT ((1 << NAT_C2F) | (1 << NAT_C3X) | (1 << NAT_C2X))
+// (every pass on bf16 terms; one LDS buffer (30 KB instead of 61: room for the other stream's
+// workgroups) for all but conv3 fwd; two slices in registers for conv1 dW.  Chosen by whole-bench
+// A/B, tools/r6/nat_ab_bench.sh r6pf3: 1.20M with two buffers on the dW passes although they time
+// faster alone, 1.28M with one)
+#define NAT_BF_DEFAULT ((1 << NAT_C2F) | (1 << NAT_C3F) | (1 << NAT_C3W) | (1 << NAT_C3X) | (1 << NAT_C2W) | \
+                        (1 << NAT_C2X) | (1 << NAT_C1W))
+#define NAT_BF1_DEFAULT ((1 << NAT_C2F) | (1 << NAT_C3W) | (1 << NAT_C3X) | (1 << NAT_C2W) | (1 << NAT_C2X))
+#define NAT_PF2_DEFAULT (1 << NAT_C1W)
 
 static int64_t nat_fwd_slab_floats(int64_t B) {
   const int sp = fc_split(B);
@@ -958,6 +969,10 @@ static bool nat_bf1(int pass) {
   static const long long v = A3C_AB_KNOB("A3C_NAT_BF1", NAT_BF1_DEFAULT);
   return (v >> pass) & 1;
 }
+static bool nat_pf2(int pass) {     // two slices in flight in registers
+  static const long long v = A3C_AB_KNOB("A3C_NAT_PF2", NAT_PF2_DEFAULT);
+  return (v >> pass) & 1;
+}
 static int nat_c1_bf() {
   static const int v = (int)A3C_AB_KNOB("A3C_NAT_C1_BF", 1);   // A/B: 0 = the fp32 MFMA conv1 forward
   return v;
@@ -970,12 +985,12 @@ static int nat_fwd_split(NatGemm a, float* fws, hipStream_t s) {
   const int S = nat_fwd_split_n(LAYER);
   if (S == 1) {    // one K chain per tile: bias + ReLU in the tile's epilogue
     a.kchunk = 0;
-    return nat_bf(pass) ? nat_go_bf<NG_FWD, LAYER, 64, 3>(a, 1, s, nat_bf1(pass)) : nat_go<NG_FWD, LAYER, 64>(a, 1, s);
+    return nat_bf(pass) ? nat_go_bf<NG_FWD, LAYER, 64, 3>(a, 1, s, nat_bf1(pass), nat_pf2(pass)) : nat_go<NG_FWD, LAYER, 64>(a, 1, s);
   }
   a.kchunk = ((a.K + S - 1) / S + 31) / 32 * 32;
   const int ns = (a.K + a.kchunk - 1) / a.kchunk;
   a.slab = fws;
-  int rc = nat_bf(pass) ? nat_go_bf<NG_FWD, LAYER, 64, 3>(a, (unsigned)ns, s, nat_bf1(pass))
+  int rc = nat_bf(pass) ? nat_go_bf<NG_FWD, LAYER, 64, 3>(a, (unsigned)ns, s, nat_bf1(pass), nat_pf2(pass))
                         : nat_go<NG_FWD, LAYER, 64>(a, (unsigned)ns, s);
   if (rc) return rc;
   GemmArgs g = {};
@@ -1029,27 +1044,27 @@ int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const Stat
     case NAT_C3W:     // dW3 (+ db3) over the (sample, pixel) rows
       a.X = l2; a.dY = bws + p.dl3; a.slab = bws + p.s3; a.colsum = bws + p.c3;
       a.M = NT_K3; a.N = NT3_N; a.K = (int)(B * NT3_P); a.kchunk = p.kc3;
-      return nat_bf(NAT_C3W) ? nat_go_bf<NG_DW, 3, 64, 3>(a, (unsigned)p.ns3, s, nat_bf1(NAT_C3W))
+      return nat_bf(NAT_C3W) ? nat_go_bf<NG_DW, 3, 64, 3>(a, (unsigned)p.ns3, s, nat_bf1(NAT_C3W), nat_pf2(NAT_C3W))
                            : nat_go<NG_DW, 3, 64>(a, (unsigned)p.ns3, s);
     case NAT_C3X:     // dl2 = col2im(dl3 W3^T) * (l2 > 0)
       a.X = l2; a.dY = bws + p.dl3; a.Wt = P + L.off[N_L3W]; a.Y = bws + p.dl2;
       a.M = (int)(B * NT2_P); a.N = NT2_N; a.K = 3 * 3 * NT3_N;
-      return nat_bf(NAT_C3X) ? nat_go_bf<NG_DX, 3, 64, 3>(a, 1, s, nat_bf1(NAT_C3X))
+      return nat_bf(NAT_C3X) ? nat_go_bf<NG_DX, 3, 64, 3>(a, 1, s, nat_bf1(NAT_C3X), nat_pf2(NAT_C3X))
                            : nat_go<NG_DX, 3, 64>(a, 1, s);
     case NAT_C2W:
       a.X = l1; a.dY = bws + p.dl2; a.slab = bws + p.s2; a.colsum = bws + p.c2;
       a.M = NT_K2; a.N = NT2_N; a.K = (int)(B * NT2_P); a.kchunk = p.kc2;
-      return nat_bf(NAT_C2W) ? nat_go_bf<NG_DW, 2, 64, 3>(a, (unsigned)p.ns2, s, nat_bf1(NAT_C2W))
+      return nat_bf(NAT_C2W) ? nat_go_bf<NG_DW, 2, 64, 3>(a, (unsigned)p.ns2, s, nat_bf1(NAT_C2W), nat_pf2(NAT_C2W))
                            : nat_go<NG_DW, 2, 64>(a, (unsigned)p.ns2, s);
     case NAT_C2X:     // dl1 = col2im(dl2 W2^T) * (l1 > 0), per stride-2 parity class
       a.X = l1; a.dY = bws + p.dl2; a.Wt = P + L.off[N_L2W]; a.Y = bws + p.dl1;
       a.M = (int)(B * (NT1_O / 2) * (NT1_O / 2)); a.N = NT1_N; a.K = 2 * 2 * NT2_N;
-      return nat_bf(NAT_C2X) ? nat_go_bf<NG_DX, 2, 32, 3>(a, 4, s, nat_bf1(NAT_C2X))
+      return nat_bf(NAT_C2X) ? nat_go_bf<NG_DX, 2, 32, 3>(a, 4, s, nat_bf1(NAT_C2X), nat_pf2(NAT_C2X))
                            : nat_go<NG_DX, 2, 32>(a, 4, s);
     case NAT_C1W:     // dW1 (+ db1) from the u8 planes (the input needs no gradient)
       a.sa = sa; a.dY = bws + p.dl1; a.slab = bws + p.s1; a.colsum = bws + p.c1;
       a.M = NT_K1; a.N = NT1_N; a.K = (int)(B * NT1_P); a.kchunk = p.kc1;
-      return nat_bf(NAT_C1W) ? nat_go_bf<NG_DW1, 1, 32, 1>(a, (unsigned)p.ns1, s, nat_bf1(NAT_C1W))
+      return nat_bf(NAT_C1W) ? nat_go_bf<NG_DW1, 1, 32, 1>(a, (unsigned)p.ns1, s, nat_bf1(NAT_C1W), nat_pf2(NAT_C1W))
                            : nat_go<NG_DW1, 1, 32>(a, (unsigned)p.ns1, s);
     default:
       return a3c_set_error(A3C_ERR_INVALID, "a3c_nat_pass_launch", "unknown pass");
