@@ -772,12 +772,13 @@ __device__ inline uint2 nat_u8x4_bf16(uint32_t d) {   // 4 pixels -> 4 bf16 (exa
 
 // tile: 128 rows (sample, pixel) x 32 channels, 4 waves of 32 rows; K = 256 in 8 slices of 32 (k' =
 // (cin, kh, kw): a row's 32 k' of a slice are 4 kernel rows of 8 pixels of one plane), LDS double-buffered
+template <int NBUF>
 __global__ void __launch_bounds__(256) k_nat_conv1_bf(StateAddr sa, const uint16_t* __restrict__ w1t,
                                                       const float* __restrict__ bias, float* __restrict__ Y, int M,
                                                       float scale) {
   constexpr int BM = 128, BK = 32, P = NT1_P, OW = NT1_O;
-  __shared__ __attribute__((aligned(16))) uint16_t As[2][BM][C1B_LD];
-  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][3][NT1_N][C1B_LD];
+  __shared__ __attribute__((aligned(16))) uint16_t As[NBUF][BM][C1B_LD];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[NBUF][3][NT1_N][C1B_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int m0 = blockIdx.x * BM;
   RingRows ring;
@@ -851,9 +852,14 @@ __global__ void __launch_bounds__(256) k_nat_conv1_bf(StateAddr sa, const uint16
     const bool more = k0 + BK < NT_K1;
     if (more) load_all(k0 + BK);
     compute(buf);
-    if (more) store(buf ^ 1);
+    if constexpr (NBUF == 1) {   // one buffer: the slice is stored after every wave has read it
+      __syncthreads();
+      if (more) store(0);
+    } else {
+      if (more) store(buf ^ 1);
+    }
     __syncthreads();
-    buf ^= 1;
+    buf ^= NBUF - 1;
   }
   const int col = lane & 31;
   const float bc = bias[col];
@@ -944,13 +950,14 @@ static int nat_fwd_split_n(int layer) {
   return n > NAT_FWD_SPLIT_MAX ? NAT_FWD_SPLIT_MAX : n;
 }
 // passes on the bf16 matrix cores / with one LDS buffer (bits NAT_*; measured per pass)
-// (every pass on bf16 terms; one LDS buffer (30 KB instead of 61: room for the other stream's
-// workgroups) for all but conv3 fwd; two slices in registers for conv1 dW.  Chosen by whole-bench
-// A/B, tools/r6/nat_ab_bench.sh r6pf3: 1.20M with two buffers on the dW passes although they time
-// faster alone, 1.28M with one)
+// (every pass on bf16 terms, with one LDS buffer (30 KB instead of 61: room for the other stream's
+// workgroups); two slices in registers for conv1 dW.  Chosen by whole-bench A/B,
+// tools/r6/nat_ab_bench.sh r6pf3 / r6pf4: 1.20M with two buffers on the dW passes although they time
+// faster alone, 1.28M with one, 1.33M with conv3 fwd's one as well)
 #define NAT_BF_DEFAULT ((1 << NAT_C2F) | (1 << NAT_C3F) | (1 << NAT_C3W) | (1 << NAT_C3X) | (1 << NAT_C2W) | \
                         (1 << NAT_C2X) | (1 << NAT_C1W))
-#define NAT_BF1_DEFAULT ((1 << NAT_C2F) | (1 << NAT_C3W) | (1 << NAT_C3X) | (1 << NAT_C2W) | (1 << NAT_C2X))
+#define NAT_BF1_DEFAULT ((1 << NAT_C2F) | (1 << NAT_C3F) | (1 << NAT_C3W) | (1 << NAT_C3X) | (1 << NAT_C2W) | \
+                         (1 << NAT_C2X))
 #define NAT_PF2_DEFAULT (1 << NAT_C1W)
 
 static int64_t nat_fwd_slab_floats(int64_t B) {
@@ -1008,8 +1015,12 @@ int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const Stat
     case NAT_C1F:
       if (w1t && nat_c1_bf()) {
         const int M = (int)(B * NT1_P);
-        hipLaunchKernelGGL(k_nat_conv1_bf, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, sa, w1t,
-                           P + L.off[N_L1B], (float*)l1, M, 1.0f / 255.0f);
+        if (nat_bf1(NAT_C1F))
+          hipLaunchKernelGGL(k_nat_conv1_bf<1>, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, sa, w1t,
+                             P + L.off[N_L1B], (float*)l1, M, 1.0f / 255.0f);
+        else
+          hipLaunchKernelGGL(k_nat_conv1_bf<2>, dim3((unsigned)((M + 127) / 128)), dim3(256), 0, s, sa, w1t,
+                             P + L.off[N_L1B], (float*)l1, M, 1.0f / 255.0f);
         A3C_CHECK(hipGetLastError());
         return 0;
       }
