@@ -54,6 +54,7 @@ int a3c_nat_fused_tab(const NetLayout& L, TensorTab* tt);
 // (fws: the fc's split-K slabs), backward passes over B samples on the plan's buffers in bws
 // (valid after a backward of the same B has filled them)
 enum { NAT_C1F = 0, NAT_C2F, NAT_C3F, NAT_FCF, NAT_C3W, NAT_C3X, NAT_C2W, NAT_C2X, NAT_C1W };
+enum { NAT_FCW = NAT_C1W + 1, NAT_FCX };   // (variant-selection bits of the fc backward GEMMs, nature.hip)
 int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* l1,
                         const float* l2, const float* l3, const float* l4, const uint16_t* w1t, float* fws,
                         float* bws, hipStream_t s);

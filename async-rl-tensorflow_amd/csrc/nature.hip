@@ -32,6 +32,9 @@ template <int LAYER> struct NG;
 template <> struct NG<1> { static constexpr int H = IMG, W = IMG, C = HIST, KH = 8, KW = 8, S = 4, OH = NT1_O, OW = NT1_O, OC = NT1_N; };
 template <> struct NG<2> { static constexpr int H = NT1_O, W = NT1_O, C = NT1_N, KH = 4, KW = 4, S = 2, OH = NT2_O, OW = NT2_O, OC = NT2_N; };
 template <> struct NG<3> { static constexpr int H = NT2_O, W = NT2_O, C = NT2_N, KH = 3, KW = 3, S = 1, OH = NT3_O, OW = NT3_O, OC = NT3_N; };
+// the fc 3136 -> 512 (network.py:41-42) as a 1x1 convolution of a 1x1 "image": the same tile
+// kernels then run its forward, weight gradient (NG_DW) and input gradient with the l3 ReLU mask (NG_DX)
+template <> struct NG<4> { static constexpr int H = 1, W = 1, C = NT_FLAT, KH = 1, KW = 1, S = 1, OH = 1, OW = 1, OC = NT_FC; };
 
 struct NatGemm {
   StateAddr sa;        // NG_FWD1 / NG_DW1: the u8 state planes of sample b (b = t E + e)
@@ -953,7 +956,9 @@ static int nat_fwd_split_n(int layer) {
 // (every pass on bf16 terms, with one LDS buffer (30 KB instead of 61: room for the other stream's
 // workgroups); two slices in registers for conv1 dW.  Chosen by whole-bench A/B,
 // tools/r6/nat_ab_bench.sh r6pf3 / r6pf4: 1.20M with two buffers on the dW passes although they time
-// faster alone, 1.28M with one, 1.33M with conv3 fwd's one as well)
+// faster alone, 1.28M with one, 1.33M with conv3 fwd's one as well).  Bits NAT_FCF / NAT_FCW /
+// NAT_FCX put the fc's forward and backward GEMMs on the same kernels: measured-and-rejected
+// (r6fc1: 1.27M / 1.30M / 1.32M against 1.33M on gemm.hip), so they stay A/B-only)
 #define NAT_BF_DEFAULT ((1 << NAT_C2F) | (1 << NAT_C3F) | (1 << NAT_C3W) | (1 << NAT_C3X) | (1 << NAT_C2W) | \
                         (1 << NAT_C2X) | (1 << NAT_C1W))
 #define NAT_BF1_DEFAULT ((1 << NAT_C2F) | (1 << NAT_C3F) | (1 << NAT_C3W) | (1 << NAT_C3X) | (1 << NAT_C2W) | \
@@ -1037,6 +1042,20 @@ int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const Stat
       a.M = (int)(B * NT3_P); a.N = NT3_N; a.K = NT_K3;
       return nat_fwd_split<3>(a, fws, s);
     case NAT_FCF: {
+      if (nat_bf(NAT_FCF)) {   // bf16 terms: K split over grid z into fws slabs, fold with bias + ReLU
+        a.X = l3; a.Wt = P + L.off[N_FCW]; a.bias = P + L.off[N_FCB]; a.Y = (float*)l4;
+        a.M = (int)B; a.N = NT_FC; a.K = NT_FLAT;
+        const int ns = fc_split(B);
+        if (ns <= 1) return nat_go_bf<NG_FWD, 4, 64, 3>(a, 1, s, nat_bf1(NAT_FCF), nat_pf2(NAT_FCF));
+        a.kchunk = ((a.K + ns - 1) / ns + 31) / 32 * 32;
+        const int nz = (a.K + a.kchunk - 1) / a.kchunk;
+        a.slab = fws;
+        int rc = nat_go_bf<NG_FWD, 4, 64, 3>(a, (unsigned)nz, s, nat_bf1(NAT_FCF), nat_pf2(NAT_FCF));
+        if (rc) return rc;
+        GemmArgs g = {};
+        g.slab = fws; g.nsplit = nz; g.M = a.M; g.N = a.N; g.C = a.Y; g.ldc = a.N; g.epi = EPI_BIAS_RELU; g.bias = a.bias;
+        return a3c_gemm_reduce(g, s);
+      }
       // l4 = relu(l3 W + b) (network.py:41-42, ops.py:41-44): split-K slabs, the fold applies the epilogue
       GemmArgs gf = {};
       gf.A = l3; gf.lda = NT_FLAT;
@@ -1177,6 +1196,12 @@ int a3c_nat_backward_launch(const NetLayout& L, const float* P, const StateAddr&
   rc = a3c_gemm(false, true, gh, s);
   if (rc) return rc;
   // fc weights: dW[3136][512] = l3^T dl4 straight into grads (split-K inside the workgroups), db = colsum
+  if (nat_bf(NAT_FCW)) {   // bf16 terms, one reduction chain per tile straight into grads (+ db)
+    NatGemm a = {};
+    a.X = l3; a.dY = dl4; a.slab = grads + L.off[N_FCW]; a.colsum = ws + p.fccol;
+    a.M = NT_FLAT; a.N = NT_FC; a.K = (int)B; a.kchunk = (int)B;
+    rc = nat_go_bf<NG_DW, 4, 64, 3>(a, 1, s, nat_bf1(NAT_FCW), nat_pf2(NAT_FCW));
+  } else {
   GemmArgs gf = {};
   gf.A = l3; gf.lda = NT_FLAT;
   gf.B = dl4; gf.ldb = NT_FC;
@@ -1184,8 +1209,15 @@ int a3c_nat_backward_launch(const NetLayout& L, const float* P, const StateAddr&
   gf.M = NT_FLAT; gf.N = NT_FC; gf.K = (int)B;
   gf.epi = EPI_STORE; gf.colsum = ws + p.fccol; gf.wg_split = 4; gf.xcd = 1;
   rc = a3c_gemm(false, true, gf, s);
+  }
   if (rc) return rc;
   // dl3 = (dl4 W^T) * (l3 > 0)
+  if (nat_bf(NAT_FCX)) {
+    NatGemm a = {};
+    a.X = l3; a.dY = dl4; a.Wt = P + L.off[N_FCW]; a.Y = ws + p.dl3;
+    a.M = (int)B; a.N = NT_FLAT; a.K = NT_FC;
+    rc = nat_go_bf<NG_DX, 4, 64, 3>(a, 1, s, nat_bf1(NAT_FCX), nat_pf2(NAT_FCX));
+  } else {
   GemmArgs gd = {};
   gd.A = dl4; gd.lda = NT_FC;
   gd.B = P + L.off[N_FCW]; gd.ldb = NT_FC;
@@ -1193,6 +1225,7 @@ int a3c_nat_backward_launch(const NetLayout& L, const float* P, const StateAddr&
   gd.M = (int)B; gd.N = NT_FLAT; gd.K = NT_FC;
   gd.epi = EPI_MASK; gd.mask = l3; gd.ldm = NT_FLAT; gd.nsplit = 1;
   rc = a3c_gemm(true, false, gd, s);
+  }
   if (rc) return rc;
   for (int pass = NAT_C3W; pass <= NAT_C1W; ++pass) {
     rc = a3c_nat_pass_launch(pass, L, P, sa, B, l1, l2, l3, l4, nullptr, nullptr, ws, s);
