@@ -985,6 +985,13 @@ static bool nat_pf2(int pass) {     // two slices in flight in registers
   static const long long v = A3C_AB_KNOB("A3C_NAT_PF2", NAT_PF2_DEFAULT);
   return (v >> pass) & 1;
 }
+// A/B: 1 = the fc's split-K fold inside the head + screen kernel (one launch per step fewer);
+// measured-and-rejected: 1.29M vs 1.33M (r6fh1) -- 256 workgroups each folding 16 slabs of one
+// row are slower than the wide fold kernel
+static int nat_fold_head() {
+  static const int v = (int)A3C_AB_KNOB("A3C_NAT_FOLD_HEAD", 0);
+  return v;
+}
 static int nat_c1_bf() {
   static const int v = (int)A3C_AB_KNOB("A3C_NAT_C1_BF", 1);   // A/B: 0 = the fp32 MFMA conv1 forward
   return v;
@@ -1042,6 +1049,7 @@ int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const Stat
       a.M = (int)(B * NT3_P); a.N = NT3_N; a.K = NT_K3;
       return nat_fwd_split<3>(a, fws, s);
     case NAT_FCF: {
+      if (fws == nullptr) return a3c_set_error(A3C_ERR_INVALID, "a3c_nat_pass_launch", "fc: no slab workspace");
       if (nat_bf(NAT_FCF)) {   // bf16 terms: K split over grid z into fws slabs, fold with bias + ReLU
         a.X = l3; a.Wt = P + L.off[N_FCW]; a.bias = P + L.off[N_FCB]; a.Y = (float*)l4;
         a.M = (int)B; a.N = NT_FC; a.K = NT_FLAT;
@@ -1133,11 +1141,26 @@ int a3c_nat_forward_launch(const NetLayout& L, const float* P, const StateAddr& 
     if (int rc = nat_w1_terms_launch(L, P, t, s)) return rc;
     w1t = t;
   }
-  for (int pass = NAT_C1F; pass <= NAT_FCF; ++pass) {
+  const bool step_tail = sel.mode >= 0 && sel.env_on && sel.pool;   // the engine's rollout step
+  const int fcs = fc_split(B);
+  const bool fold_in_head = step_tail && fcs > 1 && !nat_bf(NAT_FCF) && nat_fold_head();
+  for (int pass = NAT_C1F; pass <= (fold_in_head ? NAT_C3F : NAT_FCF); ++pass) {
     const int rc = a3c_nat_pass_launch(pass, L, P, sa, B, l1, l2, l3, l4, w1t, ws, nullptr, s);
     if (rc) return rc;
   }
-  if (sel.mode >= 0 && sel.env_on && sel.pool)   // the engine's rollout step: head + act + Environment.screen
+  if (fold_in_head) {   // the fc's K-slice partials, folded by the head + act + screen kernel
+    GemmArgs gf = {};
+    gf.A = l3; gf.lda = NT_FLAT;
+    gf.B = P + L.off[N_FCW]; gf.ldb = NT_FC;
+    gf.C = l4; gf.ldc = NT_FC;
+    gf.M = (int)B; gf.N = NT_FC; gf.K = NT_FLAT;
+    gf.epi = EPI_BIAS_RELU; gf.bias = P + L.off[N_FCB];
+    gf.nsplit = fcs; gf.slab = ws; gf.defer_reduce = 1;
+    if (int rc = a3c_gemm(true, true, gf, s)) return rc;
+    return a3c_head_screen_fold_launch(ws, fcs, P + L.off[N_FCB], l4, P + L.off[N_HW], P + L.off[N_HB],
+                                       P + L.off[N_VW], P + L.off[N_VB], L.A, L.zs, B, z, sel, s);
+  }
+  if (step_tail)   // head + act + Environment.screen
     return a3c_head_screen_wide_launch(l4, P + L.off[N_HW], P + L.off[N_HB], P + L.off[N_VW], P + L.off[N_VB], L.A,
                                        L.zs, B, z, sel, s);
   hipLaunchKernelGGL(k_nat_head, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, l4, B, P + L.off[N_HW],

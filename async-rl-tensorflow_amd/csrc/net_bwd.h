@@ -102,6 +102,9 @@ int a3c_td_target_launch(const float* rewards, const uint8_t* terms, const float
 int a3c_select_launch(const float* z, int64_t B, int zs, int A, const HeadSelect& sel, hipStream_t s);
 void a3c_conv12_set_smem();
 void a3c_conv_bwd_set_smem();
+int a3c_head_screen_fold_launch(const float* part, int nsplit, const float* fbias, float* l4, const float* Wp,
+                                const float* bp, const float* Wv, const float* bv, int A, int zs, int64_t B, float* z,
+                                const HeadSelect& sel, hipStream_t s);
 int a3c_head_screen_wide_launch(const float* l4, const float* Wp, const float* bp, const float* Wv, const float* bv,
                                 int A, int zs, int64_t B, float* z, const HeadSelect& sel, hipStream_t s);
 int a3c_head_screen_launch(const NetLayout& L, const float* P, const float* act_l3, int64_t B, float* z,

@@ -521,7 +521,8 @@ __device__ inline int32_t head_act_env(const float* __restrict__ h3, const float
                  : head_row(h3, b, Wp, bp, Wv, bv, A, lane, [&]() { x = action_draw(sel, b, tau); });
     } else {
       auto mid = [&]() { x = action_draw(sel, b, tau); };
-      myz = head_row<decltype(mid), W>(h3, b, Wp, bp, Wv, bv, A, lane, mid);
+      myz = hrow ? head_row<decltype(mid), W>(hrow, 0, Wp, bp, Wv, bv, A, lane, mid)
+                 : head_row<decltype(mid), W>(h3, b, Wp, bp, Wv, bv, A, lane, mid);
     }
     if (dbg) {
       if (lane == 0) dbg[1] = __builtin_readcyclecounter() + (uint64_t)(myz * 0.f);
@@ -776,6 +777,53 @@ int a3c_fc_fwd_launch(const float* A, const float* W, const float* bias, float* 
 
 // skip_conv12: conv1 + conv2 of these states already ran (fused into the previous step's
 // k_head_screen_conv12); next: fuse the next states' conv1 + conv2 into this step's head + screen
+// the nature trunk's rollout step tail with the fc's split-K fold in front: the workgroup folds
+// env b's row of the nsplit K-slice partials (slice order, + bias, ReLU: k_reduce_slabs' order, so
+// the row is bit-identical to the separate fold), keeps it in LDS for the head and writes it out for
+// the backward -- one launch per step fewer
+template <int HS_THREADS, int W>
+__global__ void __launch_bounds__(HS_THREADS) k_head_screen_fold(const float* __restrict__ part, int nsplit,
+                                                                 int64_t pstride, const float* __restrict__ fbias,
+                                                                 float* __restrict__ hout,
+                                                                 const float* __restrict__ Wp,
+                                                                 const float* __restrict__ bp,
+                                                                 const float* __restrict__ Wv,
+                                                                 const float* __restrict__ bv, int A, int zs,
+                                                                 float* __restrict__ z, HeadSelect sel) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ __attribute__((aligned(16))) float hrow[W];
+  const int64_t b = blockIdx.x;
+  const int64_t tau = *sel.tau_ptr + sel.tau_add;
+  for (int i = threadIdx.x; i < W; i += HS_THREADS) {
+    const float v = fmaxf(sum_strided(part + b * W + i, nsplit, pstride) + fbias[i], 0.f);
+    hrow[i] = v;
+    hout[b * W + i] = v;
+  }
+  __syncthreads();
+  const int32_t frame = head_act_env<W>(nullptr, Wp, bp, Wv, bv, A, zs, z, sel, b, tau, nullptr, hrow);
+  uint8_t* slot = sel.ring + b * sel.R * PLANE + ((tau + 1) % sel.R) * PLANE;
+  if (sel.frame84)
+    atari::copy_frame84<HS_THREADS>(sel.pool + (int64_t)frame * PLANE, slot);
+  else
+    atari::screen_frame<HS_THREADS>(sel.pool + (int64_t)frame * (atari::IH * atari::IW * 3), slot, smem, nullptr);
+}
+
+int a3c_head_screen_fold_launch(const float* part, int nsplit, const float* fbias, float* l4, const float* Wp,
+                                const float* bp, const float* Wv, const float* bv, int A, int zs, int64_t B, float* z,
+                                const HeadSelect& sel, hipStream_t s) {
+  static const int env_t = (int)A3C_AB_KNOB("A3C_HS_THREADS", 0);
+  const int nt = env_t ? env_t : (a3c_shared_gpu() ? 512 : 1024);
+  const int64_t ps = B * 512;
+  if (nt == 1024)
+    hipLaunchKernelGGL((k_head_screen_fold<1024, 512>), dim3((unsigned)B), dim3(1024), SCREEN_FRAME_SMEM, s, part,
+                       nsplit, ps, fbias, l4, Wp, bp, Wv, bv, A, zs, z, sel);
+  else
+    hipLaunchKernelGGL((k_head_screen_fold<512, 512>), dim3((unsigned)B), dim3(512), SCREEN_FRAME_SMEM, s, part,
+                       nsplit, ps, fbias, l4, Wp, bp, Wv, bv, A, zs, z, sel);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
+
 // the same for the nature trunk's 512-wide fc output (nature.hip's rollout steps)
 int a3c_head_screen_wide_launch(const float* l4, const float* Wp, const float* bp, const float* Wv, const float* bv,
                                 int A, int zs, int64_t B, float* z, const HeadSelect& sel, hipStream_t s) {
@@ -946,6 +994,10 @@ void a3c_conv12_set_smem() {
   (void)hipFuncSetAttribute((const void*)k_head_screen<512, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             SCREEN_FRAME_SMEM);
   (void)hipFuncSetAttribute((const void*)k_head_screen<1024, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SCREEN_FRAME_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_head_screen_fold<512, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SCREEN_FRAME_SMEM);
+  (void)hipFuncSetAttribute((const void*)k_head_screen_fold<1024, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             SCREEN_FRAME_SMEM);
 }
 
