@@ -445,6 +445,11 @@ __global__ void __launch_bounds__(256) k_nat_gemm_bf(NatGemm a) {
     if constexpr (A_KC) {
       const int q = tid + 256 * i;
       ar[i] = q >> 3; ac[i] = (q & 7) * 4;
+    } else if constexpr (U8) {
+      // conv1 dW: quads i = (half h = i >> 1, row i & 1) of one 8-pixel patch row: a lane loads
+      // kw 0..7 of (cin, kh) as one 8-byte load per row; lanes run along the k pairs
+      static_assert(AQ == 4 && BM == 128, "u8 octets: 16 octets x 16 k pairs");
+      ar[i] = 2 * (tid % (BK / 2)) + (i & 1); ac[i] = ((tid / (BK / 2)) * 2 + (i >> 1)) * 4;
     } else {
       const int pp = tid + 256 * (i >> 1);
       ar[i] = pair_k(pp) + (i & 1); ac[i] = pair_q(pp, BM / 4) * 4;
@@ -592,9 +597,29 @@ __global__ void __launch_bounds__(256) k_nat_gemm_bf(NatGemm a) {
 
   f32x16 acc = {};
   const int r = lane & 31, h = lane >> 5;
+  // conv1 dW: the 8 pixels kw 0..7 of quad i's (cin, kh) row -> quads i (kw 0..3) and i + 2 (kw 4..7)
+  auto load_a8 = [&](int i, int k0, f32x4& lo, f32x4& hi) {
+    const int r = k0 + ar[i];
+    uint2 d = make_uint2(0u, 0u);
+    if (aval[i] && r < kend) {
+      const int b = r / P, pos = r - b * P, oy = pos / G::OW, ox = pos - oy * G::OW;
+      const int y = oy * G::S + mk[i][0], x = ox * G::S;
+      const int t = ring.step_of(b);
+      const uint32_t* q = (const uint32_t*)(ring.plane(b - t * ring.E, t, mk[i][2]) + y * IMG + x);
+      d.x = q[0];
+      d.y = q[1];
+    }
+    lo = (f32x4){(float)(d.x & 255u), (float)((d.x >> 8) & 255u), (float)((d.x >> 16) & 255u), (float)(d.x >> 24)};
+    hi = (f32x4){(float)(d.y & 255u), (float)((d.y >> 8) & 255u), (float)((d.y >> 16) & 255u), (float)(d.y >> 24)};
+  };
   auto load_all = [&](int k0, f32x4 (&ra)[AQ], f32x4 (&rbv)[BQ]) {
+    if constexpr (U8) {
+      load_a8(0, k0, ra[0], ra[2]);
+      load_a8(1, k0, ra[1], ra[3]);
+    } else {
 #pragma unroll
-    for (int i = 0; i < AQ; ++i) ra[i] = load_a(i, k0);
+      for (int i = 0; i < AQ; ++i) ra[i] = load_a(i, k0);
+    }
 #pragma unroll
     for (int j = 0; j < BQ; ++j) rbv[j] = load_b(j, k0);
   };
