@@ -1631,6 +1631,9 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
   if (e->nat) {   // one pass of the nature trunk: forward over E states, backward passes over n*E samples
     const int pass = kernel - A3C_KER_NAT_C1F;
     const bool fwd = pass <= NAT_FCF;
+    if (pass == NAT_C3F && a3c_nat_conv23_fused())
+      return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_time_kernel",
+                           "conv3 forward runs inside the conv2 forward launch (k_nat_conv23): time A3C_KER_NAT_C2F");
     if (!fwd && !e->grad_ready)
       return a3c_set_error(A3C_ERR_STATE, "a3c_engine_time_kernel", "backward passes: run an iteration first");
     const Slot& bs = e->slot[e->nslot == 2 ? (int)((e->iter - 2) & 1) : 0];   // the last back-propagated rollout

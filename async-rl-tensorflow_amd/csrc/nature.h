@@ -54,12 +54,19 @@ int a3c_nat_fused_tab(const NetLayout& L, TensorTab* tt);
 // (fws: the fc's split-K slabs), backward passes over B samples on the plan's buffers in bws
 // (valid after a backward of the same B has filled them)
 enum { NAT_C1F = 0, NAT_C2F, NAT_C3F, NAT_FCF, NAT_C3W, NAT_C3X, NAT_C2W, NAT_C2X, NAT_C1W };
-enum { NAT_FCW = NAT_C1W + 1, NAT_FCX };   // (variant-selection bits of the fc backward GEMMs, nature.hip)
+enum { NAT_FCW = NAT_C1W + 1, NAT_FCX };
+// conv2 + conv3 forward run as one launch (k_nat_conv23, under NAT_C2F; NAT_C3F launches nothing)
+bool a3c_nat_conv23_fused();   // (variant-selection bits of the fc backward GEMMs, nature.hip)
 int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* l1,
                         const float* l2, const float* l3, const float* l4, const uint16_t* w1t, float* fws,
                         float* bws, hipStream_t s);
-// the rollout start on the nature trunk: conv1's bf16 weight terms of P into w1t (A3C_NAT_W1T_BYTES),
-// tau snapshot (overlap) and the backward's go
+// the rollout start on the nature trunk: the bf16 weight terms of P into w1t (the prepared block,
+// A3C_NAT_PREP_BYTES: conv1's [3][32][256] in (cin, kh, kw) order, then conv2's [3][64][512] and
+// conv3's [3][64][576], each [term][cout][k] in TF k order), tau snapshot (overlap) and the
+// backward's go
 #define A3C_NAT_W1T_BYTES (3 * NT1_N * NT_K1 * 2)
+#define A3C_NAT_W2T_OFF A3C_NAT_W1T_BYTES
+#define A3C_NAT_W3T_OFF (A3C_NAT_W2T_OFF + 3 * NT2_N * NT_K2 * 2)
+#define A3C_NAT_PREP_BYTES (A3C_NAT_W3T_OFF + 3 * NT3_N * NT_K3 * 2)
 int a3c_nat_prep_launch(const NetLayout& L, const float* P, uint16_t* w1t, const int64_t* tau_src, int64_t* tau_dst,
                         uint32_t* sig, hipStream_t s);

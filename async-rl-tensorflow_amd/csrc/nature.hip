@@ -774,21 +774,42 @@ __device__ inline uint32_t nat_bf16_rn(float f) {
   return u >> 16;
 }
 
-__global__ void __launch_bounds__(256) k_nat_w1_terms(const float* __restrict__ W1, uint16_t* __restrict__ w1t) {
+__device__ inline void nat_terms3(float w, uint16_t* dst, int64_t tstride) {
 #pragma clang fp contract(off)
-  const int i = blockIdx.x * 256 + threadIdx.x;     // (cout, k')
-  if (i >= NT1_N * NT_K1) return;
-  const int n = i / NT_K1, k = i - n * NT_K1;
-  const int c = k >> 6, kh = (k >> 3) & 7, kw = k & 7;
-  const float w = W1[((kh * 8 + kw) * HIST + c) * NT1_N + n];
   const uint32_t h = nat_bf16_rn(w);
   const float r1 = w - __uint_as_float(h << 16);
   const uint32_t m = nat_bf16_rn(r1);
   const float r2 = r1 - __uint_as_float(m << 16);
   const uint32_t l = nat_bf16_rn(r2);
-  w1t[(0 * NT1_N + n) * NT_K1 + k] = (uint16_t)h;
-  w1t[(1 * NT1_N + n) * NT_K1 + k] = (uint16_t)m;
-  w1t[(2 * NT1_N + n) * NT_K1 + k] = (uint16_t)l;
+  dst[0] = (uint16_t)h;
+  dst[tstride] = (uint16_t)m;
+  dst[2 * tstride] = (uint16_t)l;
+}
+
+// the prepared block: conv1 [3][32][256] with k' = (cin, kh, kw); conv2 [3][64][512] and conv3
+// [3][64][576] with k in TF order (kh, kw, cin) -- one thread per (cout, k)
+__global__ void __launch_bounds__(256) k_nat_w_terms(const float* __restrict__ W1, const float* __restrict__ W2,
+                                                     const float* __restrict__ W3, uint16_t* __restrict__ wt,
+                                                     int all) {
+  int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < NT1_N * NT_K1) {
+    const int n = i / NT_K1, k = i - n * NT_K1;
+    const int c = k >> 6, kh = (k >> 3) & 7, kw = k & 7;
+    nat_terms3(W1[((kh * 8 + kw) * HIST + c) * NT1_N + n], wt + n * NT_K1 + k, NT1_N * NT_K1);
+    return;
+  }
+  if (!all) return;
+  i -= NT1_N * NT_K1;
+  if (i < NT2_N * NT_K2) {
+    const int n = i / NT_K2, k = i - n * NT_K2;
+    nat_terms3(W2[k * NT2_N + n], wt + A3C_NAT_W2T_OFF / 2 + n * NT_K2 + k, NT2_N * NT_K2);
+    return;
+  }
+  i -= NT2_N * NT_K2;
+  if (i < NT3_N * NT_K3) {
+    const int n = i / NT_K3, k = i - n * NT_K3;
+    nat_terms3(W3[k * NT3_N + n], wt + A3C_NAT_W3T_OFF / 2 + n * NT_K3 + k, NT3_N * NT_K3);
+  }
 }
 
 __device__ inline uint2 nat_u8x4_bf16(uint32_t d) {   // 4 pixels -> 4 bf16 (exact: the upper halves of their f32)
@@ -811,13 +832,14 @@ __global__ void __launch_bounds__(256) k_nat_conv1_bf(StateAddr sa, const uint16
   const int m0 = blockIdx.x * BM;
   RingRows ring;
   ring.init(sa, sa.tau_ptr ? *sa.tau_ptr : 0);
-  int ar[4], ac[4], ai[4], aj[4];
-  bool aval[4];
-  const uint8_t* apl[4][4];
+  // A: 2 octets per thread, an octet = kw 0..7 of one (cin, kh) patch row = one 8-byte load
+  int ar[2], ac[2], ai[2], aj[2];
+  bool aval[2];
+  const uint8_t* apl[2][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 2; ++i) {
     const int q = tid + 256 * i;
-    ar[i] = q >> 3; ac[i] = (q & 7) * 4;
+    ar[i] = q >> 2; ac[i] = (q & 3) * 8;
     const int m = m0 + ar[i];
     aval[i] = m < M;
     const int mm = aval[i] ? m : 0;
@@ -827,29 +849,33 @@ __global__ void __launch_bounds__(256) k_nat_conv1_bf(StateAddr sa, const uint16
     for (int c = 0; c < 4; ++c) apl[i][c] = ring.plane(e, t, c);
     ai[i] = oy * 4; aj[i] = ox * 4;
   }
-  auto load_a = [&](int i, int k0) -> uint32_t {
+  auto load_a = [&](int i, int k0) -> uint2 {
     const int k = k0 + ac[i];
-    if (!aval[i]) return 0u;
-    const int c = k >> 6, kh = (k >> 3) & 7, kw = k & 7;
-    return *(const uint32_t*)(apl[i][c] + (ai[i] + kh) * IMG + aj[i] + kw);
+    if (!aval[i]) return make_uint2(0u, 0u);
+    const int c = k >> 6, kh = (k >> 3) & 7;
+    const uint32_t* q = (const uint32_t*)(apl[i][c] + (ai[i] + kh) * IMG + aj[i]);
+    return make_uint2(q[0], q[1]);
   };
   // B: 3 terms x 32 couts x 32 k' per slice = 384 chunks of 8 bf16
   auto load_b = [&](int q, int k0) -> uint4 {
     const int term = q >> 7, n = (q >> 2) & 31, kc = (q & 3) * 8;
     return *(const uint4*)(w1t + (term * NT1_N + n) * NT_K1 + k0 + kc);
   };
-  uint32_t ra[4];
+  uint2 ra[2];
   uint4 rb0, rb1;
   const bool b2 = tid < 128;
   auto load_all = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ra[i] = load_a(i, k0);
+    for (int i = 0; i < 2; ++i) ra[i] = load_a(i, k0);
     rb0 = load_b(tid, k0);
     if (b2) rb1 = load_b(256 + tid, k0);
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *(uint2*)&As[buf][ar[i]][ac[i]] = nat_u8x4_bf16(ra[i]);
+    for (int i = 0; i < 2; ++i) {
+      const uint2 lo = nat_u8x4_bf16(ra[i].x), hi = nat_u8x4_bf16(ra[i].y);
+      *(uint4*)&As[buf][ar[i]][ac[i]] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    }
     {
       const int q = tid, term = q >> 7, n = (q >> 2) & 31, kc = (q & 3) * 8;
       *(uint4*)&Bs[buf][term][n][kc] = rb0;
@@ -896,6 +922,161 @@ __global__ void __launch_bounds__(256) k_nat_conv1_bf(StateAddr sa, const uint16
     const int row = m0 + wid * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
     if (row < M) Y[(int64_t)row * NT1_N + col] = fmaxf(acc[q] * scale + bc, 0.f);
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// conv2 + conv3 forward fused, one workgroup per sample (the rollout's B = E states): the sample's
+// l1 (20x20x32) is split into three bf16 terms into LDS once; conv2 (M = 81 pixels, N = 64,
+// K = 16 taps x 32) and then conv3 (M = 49, N = 64, K = 9 taps x 64) run on
+// v_mfma_f32_16x16x32_bf16 with the six products of the term split (as k_nat_gemm_bf); l2 goes
+// out (the backward's operand) and, as terms, into the LDS the l1 terms held, for conv3.  Wave w
+// owns output channels 16w..16w+15 of both layers, its weight fragments (the prepared terms,
+// [term][cout][k]) streamed from L2 with a 3-tap register ring.  Replaces two K-chain-bound passes
+// of 324 / 392 tiles and a fold with one 256-workgroup launch and no l2 re-read from HBM.
+// ---------------------------------------------------------------------------------------
+// l1 terms: [term][y 20][x parity 2][x / 2 10][40 bf16]: a 16-lane fragment read walks consecutive
+// output pixels, which sit at x = 2 ox + kw -- parity-split rows of 80 B put them 80 B apart, the
+// 16 lanes on distinct banks.  l2 terms: [term][81][72 bf16] over the same LDS after conv2.
+#define C23_R1 40
+#define C23_T1 (NT1_O * 2 * (NT1_O / 2) * C23_R1)   // bf16 per l1 term: 16000
+#define C23_R2 72
+#define C23_T2 (NT2_P * C23_R2)                     // 5832
+static_assert(3 * C23_T2 <= 3 * C23_T1, "l2 terms overlay the l1 terms");
+
+__device__ inline f32x4 c23_mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
+
+__global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1, const uint16_t* __restrict__ w2t,
+                                                    const float* __restrict__ b2, const uint16_t* __restrict__ w3t,
+                                                    const float* __restrict__ b3, float* __restrict__ l2,
+                                                    float* __restrict__ l3) {
+  __shared__ __attribute__((aligned(16))) uint16_t sm[3 * C23_T1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i16 = lane & 15, g = lane >> 4;
+  const int64_t b = blockIdx.x;
+  // ---- stage l1 of sample b as three bf16 terms (3200 float4 chunks, 12.5 per thread) ----
+  {
+    const f32x4* src = (const f32x4*)(l1 + b * NT_A1);
+    constexpr int NCH = NT_A1 / 4;
+#pragma unroll 4
+    for (int c = tid; c < NCH; c += 256) {
+      const f32x4 v = src[c];
+      const int px = c >> 3, c4 = (c & 7) * 4;          // pixel (y 20 x 20), channel quad
+      const int y = px / NT1_O, x = px - y * NT1_O;
+      const int slot = (y * 2 + (x & 1)) * (NT1_O / 2) + (x >> 1);
+      uint32_t lo[3], hi[3];
+      nat_split2<3>(v[0], v[1], lo);
+      nat_split2<3>(v[2], v[3], hi);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) *(uint2*)&sm[t * C23_T1 + slot * C23_R1 + c4] = make_uint2(lo[t], hi[t]);
+    }
+  }
+  __syncthreads();
+  // ---- conv2: 6 m-tiles of 16 pixels (81 valid) x this wave's 16 channels, 16 taps ----
+  const int n = 16 * w + i16;
+  int base2[6];
+#pragma unroll
+  for (int mt = 0; mt < 6; ++mt) {
+    const int m = min(16 * mt + i16, NT2_P - 1);
+    const int oy = m / NT2_O, ox = m - oy * NT2_O;
+    base2[mt] = (oy * 2 * 2) * (NT1_O / 2) + ox;           // slot of (y = 2 oy, parity 0, x/2 = ox)
+  }
+  f32x4 acc2[6];
+#pragma unroll
+  for (int mt = 0; mt < 6; ++mt) acc2[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const uint16_t* wb2 = w2t + (int64_t)n * NT_K2 + 8 * g;
+  bf16x8 bq[3][3];
+  auto ldb2 = [&](int tap, bf16x8 (&dst)[3]) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t) dst[t] = *(const bf16x8*)(wb2 + (int64_t)t * NT2_N * NT_K2 + tap * 32);
+  };
+  ldb2(0, bq[0]);
+  ldb2(1, bq[1]);
+#pragma unroll
+  for (int tap = 0; tap < 16; ++tap) {
+    if (tap + 2 < 16) ldb2(tap + 2, bq[(tap + 2) % 3]);
+    const int kh = tap >> 2, kw = tap & 3;
+    const int toff = (kh * 2 + (kw & 1)) * (NT1_O / 2) + (kw >> 1);
+#pragma unroll
+    for (int mt = 0; mt < 6; ++mt) {
+      bf16x8 a[3];
+      const uint16_t* ap = sm + (base2[mt] + toff) * C23_R1 + 8 * g;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) a[t] = *(const bf16x8*)(ap + t * C23_T1);
+      acc2[mt] = c23_mfma6(a, bq[tap % 3], acc2[mt]);
+    }
+  }
+  __syncthreads();   // every wave is done reading the l1 terms
+  // ---- conv2 epilogue: bias + ReLU, l2 out, l2 terms into LDS ----
+  {
+    const float bn = b2[n];
+#pragma unroll
+    for (int mt = 0; mt < 6; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * mt + 4 * g + r;
+        if (m < NT2_P) {
+          const float v = fmaxf(acc2[mt][r] + bn, 0.f);
+          l2[(b * NT2_P + m) * NT2_N + n] = v;
+          const float hf = __uint_as_float(nat_bf16_rn(v) << 16);
+          const float r1 = v - hf;
+          const float mf = __uint_as_float(nat_bf16_rn(r1) << 16);
+          const float r2 = r1 - mf;
+          sm[0 * C23_T2 + m * C23_R2 + n] = (uint16_t)(__float_as_uint(hf) >> 16);
+          sm[1 * C23_T2 + m * C23_R2 + n] = (uint16_t)(__float_as_uint(mf) >> 16);
+          sm[2 * C23_T2 + m * C23_R2 + n] = (uint16_t)nat_bf16_rn(r2);
+        }
+      }
+  }
+  // weight ring of conv3 starts under the barrier
+  const uint16_t* wb3 = w3t + (int64_t)n * NT_K3 + 8 * g;
+  auto ldb3 = [&](int st, bf16x8 (&dst)[3]) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t) dst[t] = *(const bf16x8*)(wb3 + (int64_t)t * NT3_N * NT_K3 + st * 32);
+  };
+  ldb3(0, bq[0]);
+  ldb3(1, bq[1]);
+  __syncthreads();
+  // ---- conv3: 4 m-tiles of 16 pixels (49 valid), 18 K steps (9 taps x 2 channel halves) ----
+  int base3[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const int m = min(16 * mt + i16, NT3_P - 1);
+    const int oy = m / NT3_O, ox = m - oy * NT3_O;
+    base3[mt] = oy * NT2_O + ox;
+  }
+  f32x4 acc3[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) acc3[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < 18; ++st) {
+    if (st + 2 < 18) ldb3(st + 2, bq[(st + 2) % 3]);
+    const int tap = st >> 1, kh = tap / 3, kw = tap - kh * 3;
+    const int off = (kh * NT2_O + kw) * C23_R2 + 32 * (st & 1) + 8 * g;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      bf16x8 a[3];
+      const uint16_t* ap = sm + base3[mt] * C23_R2 + off;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) a[t] = *(const bf16x8*)(ap + t * C23_T2);
+      acc3[mt] = c23_mfma6(a, bq[st % 3], acc3[mt]);
+    }
+  }
+  const float b3n = b3[n];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 16 * mt + 4 * g + r;
+      if (m < NT3_P) l3[(b * NT3_P + m) * NT3_N + n] = fmaxf(acc3[mt][r] + b3n, 0.f);
+    }
 }
 
 // the policy / value head of B states (one wave each) on the 512-wide fc output, + the action
@@ -996,7 +1177,7 @@ static int64_t nat_fwd_slab_floats(int64_t B) {
   const int64_t cv = (int64_t)NAT_FWD_SPLIT_MAX * B * (NT2_P * NT2_N > NT3_P * NT3_N ? NT2_P * NT2_N : NT3_P * NT3_N);
   return ((fc > cv ? fc : cv) + 63) / 64 * 64;
 }
-int64_t a3c_nat_fwd_ws_floats(int64_t B) { return nat_fwd_slab_floats(B) + A3C_NAT_W1T_BYTES / 4; }
+int64_t a3c_nat_fwd_ws_floats(int64_t B) { return nat_fwd_slab_floats(B) + A3C_NAT_PREP_BYTES / 4; }
 // which passes run on the bf16 matrix cores (bit NAT_*) and which of those with one LDS buffer
 static bool nat_bf(int pass) {
   static const long long v = A3C_AB_KNOB("A3C_NAT_BF", NAT_BF_DEFAULT);
@@ -1017,6 +1198,11 @@ static int nat_fold_head() {
   static const int v = (int)A3C_AB_KNOB("A3C_NAT_FOLD_HEAD", 0);
   return v;
 }
+static int nat_fuse23() {
+  static const int v = (int)A3C_AB_KNOB("A3C_NAT_FUSE23", 1);   // A/B: 0 = separate conv2 / conv3 passes
+  return v;
+}
+bool a3c_nat_conv23_fused() { return nat_fuse23() != 0; }
 static int nat_c1_bf() {
   static const int v = (int)A3C_AB_KNOB("A3C_NAT_C1_BF", 1);   // A/B: 0 = the fp32 MFMA conv1 forward
   return v;
@@ -1066,10 +1252,17 @@ int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const Stat
       a.M = (int)(B * NT1_P); a.N = NT1_N; a.K = NT_K1; a.scale = 1.0f / 255.0f;
       return nat_go<NG_FWD1, 1, 32>(a, 1, s);
     case NAT_C2F:
+      if (w1t && nat_fuse23()) {   // conv2 + conv3 in one launch (k_nat_conv23); NAT_C3F is then empty
+        hipLaunchKernelGGL(k_nat_conv23, dim3((unsigned)B), dim3(256), 0, s, l1, w1t + A3C_NAT_W2T_OFF / 2,
+                           P + L.off[N_L2B], w1t + A3C_NAT_W3T_OFF / 2, P + L.off[N_L3B], (float*)l2, (float*)l3);
+        A3C_CHECK(hipGetLastError());
+        return 0;
+      }
       a.X = l1; a.Wt = P + L.off[N_L2W]; a.bias = P + L.off[N_L2B]; a.Y = (float*)l2;
       a.M = (int)(B * NT2_P); a.N = NT2_N; a.K = NT_K2;
       return nat_fwd_split<2>(a, fws, s);
     case NAT_C3F:
+      if (w1t && nat_fuse23()) return 0;
       a.X = l2; a.Wt = P + L.off[N_L3W]; a.bias = P + L.off[N_L3B]; a.Y = (float*)l3;
       a.M = (int)(B * NT3_P); a.N = NT3_N; a.K = NT_K3;
       return nat_fwd_split<3>(a, fws, s);
@@ -1141,7 +1334,10 @@ __global__ void k_nat_prep(const int64_t* __restrict__ tau_src, int64_t* __restr
   if (sig) (void)__hip_atomic_fetch_add(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 static int nat_w1_terms_launch(const NetLayout& L, const float* P, uint16_t* w1t, hipStream_t s) {
-  hipLaunchKernelGGL(k_nat_w1_terms, dim3((NT1_N * NT_K1 + 255) / 256), dim3(256), 0, s, P + L.off[N_L1W], w1t);
+  const int all = nat_fuse23() ? 1 : 0;
+  const int n = NT1_N * NT_K1 + (all ? NT2_N * NT_K2 + NT3_N * NT_K3 : 0);
+  hipLaunchKernelGGL(k_nat_w_terms, dim3((n + 255) / 256), dim3(256), 0, s, P + L.off[N_L1W], P + L.off[N_L2W],
+                     P + L.off[N_L3W], w1t, all);
   A3C_CHECK(hipGetLastError());
   return 0;
 }

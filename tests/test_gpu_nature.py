@@ -74,7 +74,14 @@ def test_nature_pass_timing_hook():
     eng.iterate()
     torch.cuda.synchronize()
     for name, k in _lib.KER_NAT.items():
-        ms = eng.time_kernel(k, 3)
+        if name == 'conv3_fwd':   # with the fused conv2 + conv3 launch it has no launch of its own
+            try:
+                ms = eng.time_kernel(k, 3)
+            except _lib.A3CError as e:
+                assert 'k_nat_conv23' in str(e)
+                continue
+        else:
+            ms = eng.time_kernel(k, 3)
         assert 0.0 < ms < 100.0, (name, ms)
     with pytest.raises(RuntimeError):
         eng.time_kernel(_lib.KER_CONV12_FWD, 1)                            # a NIPS kernel id
