@@ -988,7 +988,8 @@ static int enqueue_grad_impl(a3c_engine* e, const Slot& sl, hipStream_t s) {
   }
   if (e->nat)
     rc = a3c_nat_backward_launch(L, sl.P, bsa, e->nE, sl.act_l1, sl.act_l2, sl.act_l3, sl.act_l4, sl.z, sl.actions,
-                                 sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra, &sf);
+                                 sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra, &sf,
+                                 (const uint16_t*)sl.prep);
   else
   rc = a3c_backward_launch(L, sl.P, bsa, e->nE, sl.act_l1, sl.act_l2, sl.act_l3, sl.z,
                            sl.actions, sl.R_buf, c.beta, c.literal_adv, e->grads, e->loss, e->ws, s, &ra,
@@ -1631,9 +1632,10 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
   if (e->nat) {   // one pass of the nature trunk: forward over E states, backward passes over n*E samples
     const int pass = kernel - A3C_KER_NAT_C1F;
     const bool fwd = pass <= NAT_FCF;
-    if (pass == NAT_C3F && a3c_nat_conv23_fused())
+    if ((pass == NAT_C3F && a3c_nat_conv23_fused()) || (pass == NAT_C1F && a3c_nat_conv123_fused()) ||
+        (pass == NAT_C2X && a3c_nat_dx_fused()))
       return a3c_set_error(A3C_ERR_INVALID, "a3c_engine_time_kernel",
-                           "conv3 forward runs inside the conv2 forward launch (k_nat_conv23): time A3C_KER_NAT_C2F");
+                           "this pass runs inside another pass's launch (k_nat_conv23 under A3C_KER_NAT_C2F, k_nat_dx32 under A3C_KER_NAT_C3X)");
     if (!fwd && !e->grad_ready)
       return a3c_set_error(A3C_ERR_STATE, "a3c_engine_time_kernel", "backward passes: run an iteration first");
     const Slot& bs = e->slot[e->nslot == 2 ? (int)((e->iter - 2) & 1) : 0];   // the last back-propagated rollout
@@ -1641,8 +1643,8 @@ extern "C" int a3c_engine_time_kernel(a3c_engine* e, int kernel, int iters, void
     auto go = [&]() -> int {
       return fwd ? a3c_nat_pass_launch(pass, L, e->params, sa, E, sl.act_l1, sl.act_l2, sl.act_l3, sl.act_l4,
                                        (const uint16_t*)sl.prep, e->nat_fws, nullptr, s)
-                 : a3c_nat_pass_launch(pass, L, bs.P, sa, e->nE, bs.act_l1, bs.act_l2, bs.act_l3, bs.act_l4, nullptr,
-                                       nullptr, e->ws, s);
+                 : a3c_nat_pass_launch(pass, L, bs.P, sa, e->nE, bs.act_l1, bs.act_l2, bs.act_l3, bs.act_l4,
+                                       (const uint16_t*)bs.prep, nullptr, e->ws, s);
     };
     int rc = go();
     if (rc) return rc;

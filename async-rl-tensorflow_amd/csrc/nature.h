@@ -45,10 +45,12 @@ struct SumsqFused;
 // gradients of every tensor into grads (TF order), loss terms summed into loss_out[4]; with sf, the
 // per-tensor squared-norm partials (layout a3c_nat_fused_tab) and the lr schedule as well.
 int64_t a3c_nat_bwd_ws_floats(const NetLayout& L, int64_t B);
+// wt: the prepared weight terms of P (a3c_nat_prep_launch), or null: prepared into ws first
 int a3c_nat_backward_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* l1,
                             const float* l2, const float* l3, const float* l4, const float* z,
                             const int32_t* actions, const float* target, float beta, int literal, float* grads,
-                            float* loss_out, float* ws, hipStream_t s, const ReturnsArgs* ra, const SumsqFused* sf);
+                            float* loss_out, float* ws, hipStream_t s, const ReturnsArgs* ra, const SumsqFused* sf,
+                            const uint16_t* wt);
 int a3c_nat_fused_tab(const NetLayout& L, TensorTab* tt);
 // the single launches behind both (a3c_engine_time_kernel): forward passes over B states
 // (fws: the fc's split-K slabs), backward passes over B samples on the plan's buffers in bws
@@ -56,7 +58,9 @@ int a3c_nat_fused_tab(const NetLayout& L, TensorTab* tt);
 enum { NAT_C1F = 0, NAT_C2F, NAT_C3F, NAT_FCF, NAT_C3W, NAT_C3X, NAT_C2W, NAT_C2X, NAT_C1W };
 enum { NAT_FCW = NAT_C1W + 1, NAT_FCX };
 // conv2 + conv3 forward run as one launch (k_nat_conv23, under NAT_C2F; NAT_C3F launches nothing)
-bool a3c_nat_conv23_fused();   // (variant-selection bits of the fc backward GEMMs, nature.hip)
+bool a3c_nat_conv23_fused();
+bool a3c_nat_conv123_fused();   // conv1 as well (NAT_C1F launches nothing)
+bool a3c_nat_dx_fused();        // conv3 dX + conv2 dX as one launch under NAT_C3X (NAT_C2X launches nothing)   // (variant-selection bits of the fc backward GEMMs, nature.hip)
 int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* l1,
                         const float* l2, const float* l3, const float* l4, const uint16_t* w1t, float* fws,
                         float* bws, hipStream_t s);
@@ -67,6 +71,10 @@ int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const Stat
 #define A3C_NAT_W1T_BYTES (3 * NT1_N * NT_K1 * 2)
 #define A3C_NAT_W2T_OFF A3C_NAT_W1T_BYTES
 #define A3C_NAT_W3T_OFF (A3C_NAT_W2T_OFF + 3 * NT2_N * NT_K2 * 2)
-#define A3C_NAT_PREP_BYTES (A3C_NAT_W3T_OFF + 3 * NT3_N * NT_K3 * 2)
+#define A3C_NAT_W2X_OFF (A3C_NAT_W3T_OFF + 3 * NT3_N * NT_K3 * 2)
+#define NT_X2 (4 * 4 * NT2_N)     // conv2's dX form: a cin row of 16 taps x 64 cout (1024)
+#define A3C_NAT_W3X_OFF (A3C_NAT_W2X_OFF + 3 * NT1_N * NT_X2 * 2)
+// (+ the dX forms: conv2's [3][32 cin][16 taps x 64 cout], conv3's [3][64 cin][9 taps x 64 cout])
+#define A3C_NAT_PREP_BYTES (A3C_NAT_W3X_OFF + 3 * NT2_N * NT_K3 * 2)
 int a3c_nat_prep_launch(const NetLayout& L, const float* P, uint16_t* w1t, const int64_t* tau_src, int64_t* tau_dst,
                         uint32_t* sig, hipStream_t s);

@@ -809,6 +809,19 @@ __global__ void __launch_bounds__(256) k_nat_w_terms(const float* __restrict__ W
   if (i < NT3_N * NT_K3) {
     const int n = i / NT_K3, k = i - n * NT_K3;
     nat_terms3(W3[k * NT3_N + n], wt + A3C_NAT_W3T_OFF / 2 + n * NT_K3 + k, NT3_N * NT_K3);
+    return;
+  }
+  i -= NT3_N * NT_K3;
+  // dX forms: [term][cin][tap][cout] = W[tap][cin][cout] (TF [kh][kw][cin][cout]): a copy per term
+  if (i < NT1_N * NT_X2) {
+    const int c = i / NT_X2, r = i - c * NT_X2, tap = r >> 6, oc = r & 63;
+    nat_terms3(W2[(tap * NT1_N + c) * NT2_N + oc], wt + A3C_NAT_W2X_OFF / 2 + i, NT1_N * NT_X2);
+    return;
+  }
+  i -= NT1_N * NT_X2;
+  if (i < NT2_N * NT_K3) {
+    const int c = i / NT_K3, r = i - c * NT_K3, tap = r >> 6, oc = r & 63;
+    nat_terms3(W3[(tap * NT2_N + c) * NT3_N + oc], wt + A3C_NAT_W3X_OFF / 2 + i, NT2_N * NT_K3);
   }
 }
 
@@ -953,17 +966,94 @@ __device__ inline f32x4 c23_mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f3
   return acc;
 }
 
-__global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1, const uint16_t* __restrict__ w2t,
+// C1: conv1 as well (k_nat_conv123): the sample's 4 u8 planes staged as bf16 rows, conv1 (M = 400
+// pixels, N = 32, K = 256 in (cin, kh, kw) order, the u8 pixel exact: three products) on the same
+// MFMA, its output (x/255 + bias, ReLU) written out for the backward and, as terms, into LDS.
+#define C123_PR 88                                   // bf16 per staged plane row (84 + 4)
+static_assert(HIST * IMG * C123_PR <= 3 * C23_T1, "planes fit the term LDS");
+template <bool C1>
+__global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1c, const uint16_t* __restrict__ w2t,
                                                     const float* __restrict__ b2, const uint16_t* __restrict__ w3t,
                                                     const float* __restrict__ b3, float* __restrict__ l2,
-                                                    float* __restrict__ l3) {
+                                                    float* __restrict__ l3, StateAddr sa, const uint16_t* __restrict__ w1t,
+                                                    const float* __restrict__ b1, float* __restrict__ l1, float scale) {
   __shared__ __attribute__((aligned(16))) uint16_t sm[3 * C23_T1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i16 = lane & 15, g = lane >> 4;
   const int64_t b = blockIdx.x;
-  // ---- stage l1 of sample b as three bf16 terms (3200 float4 chunks, 12.5 per thread) ----
-  {
-    const f32x4* src = (const f32x4*)(l1 + b * NT_A1);
+  if constexpr (C1) {
+    // ---- the 4 history planes of state b as bf16 [cin][84][88] ----
+    RingRows ring;
+    ring.init(sa, sa.tau_ptr ? *sa.tau_ptr : 0);
+    const int st = ring.step_of((int)b), e = (int)b - st * ring.E;
+#pragma unroll
+    for (int c = 0; c < HIST; ++c) {
+      const uint32_t* src = (const uint32_t*)ring.plane(e, st, c);
+      for (int q = tid; q < PLANE / 4; q += 256) {
+        const int y = q / (IMG / 4), x4 = (q - y * (IMG / 4)) * 4;
+        *(uint2*)&sm[(c * IMG + y) * C123_PR + x4] = nat_u8x4_bf16(src[q]);
+      }
+    }
+    __syncthreads();
+    // ---- conv1: 25 m-tiles x 2 n-tiles of 16; wave w: n-tile w & 1, m-tiles (w >> 1) + 2 i ----
+    const int n1 = 16 * (w & 1) + i16;
+    const int mh = w >> 1;
+    int base1[13];
+    f32x4 acc1[13];
+#pragma unroll
+    for (int i = 0; i < 13; ++i) {
+      const int m = min(16 * (mh + 2 * i) + i16, NT1_P - 1);
+      const int oy = m / NT1_O, ox = m - oy * NT1_O;
+      base1[i] = 4 * oy * C123_PR + 4 * ox;
+      acc1[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    const uint16_t* wb1 = w1t + n1 * NT_K1 + 8 * g;
+    bf16x8 q1[3][3];
+    auto ldb1 = [&](int ks, bf16x8 (&dst)[3]) {
+#pragma unroll
+      for (int t = 0; t < 3; ++t) dst[t] = *(const bf16x8*)(wb1 + t * NT1_N * NT_K1 + ks * 32);
+    };
+    ldb1(0, q1[0]);
+    ldb1(1, q1[1]);
+#pragma unroll
+    for (int ks = 0; ks < NT_K1 / 32; ++ks) {
+      if (ks + 2 < NT_K1 / 32) ldb1(ks + 2, q1[(ks + 2) % 3]);
+      const int cin = ks >> 1, kh = 4 * (ks & 1) + g;
+      const uint16_t* rp = sm + (cin * IMG + kh) * C123_PR;
+#pragma unroll
+      for (int i = 0; i < 13; ++i) {
+        if (mh + 2 * i >= NT1_P / 16) continue;          // (wave-uniform) the 25 tiles
+        const uint2 u0 = *(const uint2*)(rp + base1[i]), u1 = *(const uint2*)(rp + base1[i] + 4);
+        const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(u0.x, u0.y, u1.x, u1.y));
+        const bf16x8* bb = q1[ks % 3];
+        acc1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb[2], acc1[i], 0, 0, 0);
+        acc1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb[1], acc1[i], 0, 0, 0);
+        acc1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb[0], acc1[i], 0, 0, 0);
+      }
+    }
+    __syncthreads();   // the planes are no longer read: their LDS takes the l1 terms
+    const float bn1 = b1[n1];
+#pragma unroll
+    for (int i = 0; i < 13; ++i) {
+      if (mh + 2 * i >= NT1_P / 16) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * (mh + 2 * i) + 4 * g + r;
+        const float v = fmaxf(acc1[i][r] * scale + bn1, 0.f);
+        l1[(b * NT1_P + m) * NT1_N + n1] = v;
+        const int y = m / NT1_O, x = m - y * NT1_O;
+        const int slot = (y * 2 + (x & 1)) * (NT1_O / 2) + (x >> 1);
+        const float hf = __uint_as_float(nat_bf16_rn(v) << 16);
+        const float r1 = v - hf;
+        const float mf = __uint_as_float(nat_bf16_rn(r1) << 16);
+        sm[0 * C23_T1 + slot * C23_R1 + n1] = (uint16_t)(__float_as_uint(hf) >> 16);
+        sm[1 * C23_T1 + slot * C23_R1 + n1] = (uint16_t)(__float_as_uint(mf) >> 16);
+        sm[2 * C23_T1 + slot * C23_R1 + n1] = (uint16_t)nat_bf16_rn(r1 - mf);
+      }
+    }
+  } else {
+    // ---- stage l1 of sample b as three bf16 terms (3200 float4 chunks, 12.5 per thread) ----
+    const f32x4* src = (const f32x4*)(l1c + b * NT_A1);
     constexpr int NCH = NT_A1 / 4;
 #pragma unroll 4
     for (int c = tid; c < NCH; c += 256) {
@@ -1079,6 +1169,160 @@ __global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// conv3 dX and conv2 dX fused, one workgroup per sample (network.py's conv2 / conv3 backward):
+//   dl2 = col2im(dl3 W3^T) * (l2 > 0)   M = 81 pixels, N = 64, K = 9 taps x 64 cout
+//   dl1 = col2im(dl2 W2^T) * (l1 > 0)   per stride-2 parity class: M = 100, N = 32, K = 4 real taps x 64
+// dl3 (already masked by l3 > 0) is staged as three bf16 terms on a zero-bordered 11 x 11 grid,
+// so every tap reads a plain fragment (out-of-range sources are the zeros); dl2 goes out (conv2
+// dW's operand) and, as terms on a 1-bordered 11 x 11 grid, into the same LDS for conv2 dX.
+// The weights' dX forms ([term][cin][tap][cout], prepared per rollout) stream from L2.
+// ---------------------------------------------------------------------------------------
+#define DX_R 72                                   // bf16 per grid cell (64 + 8)
+#define DX_G (11 * 11)
+#define DX_T (DX_G * DX_R)                        // bf16 per term
+__global__ void __launch_bounds__(256) k_nat_dx32(const float* __restrict__ dl3, const float* __restrict__ l2,
+                                                  const float* __restrict__ l1, const uint16_t* __restrict__ w3x,
+                                                  const uint16_t* __restrict__ w2x, float* __restrict__ dl2,
+                                                  float* __restrict__ dl1) {
+  __shared__ __attribute__((aligned(16))) uint16_t sm[3 * DX_T];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i16 = lane & 15, g = lane >> 4;
+  const int64_t b = blockIdx.x;
+  auto zero_all = [&]() {
+    for (int q = tid; q < 3 * DX_T / 8; q += 256) ((uint4*)sm)[q] = make_uint4(0u, 0u, 0u, 0u);
+  };
+  zero_all();
+  __syncthreads();
+  {   // dl3 [49][64] -> cells (y + 2, x + 2)
+    const f32x4* src = (const f32x4*)(dl3 + b * NT_FLAT);
+    for (int q = tid; q < NT_FLAT / 4; q += 256) {
+      const f32x4 v = src[q];
+      const int px = q >> 4, c4 = (q & 15) * 4, y = px / NT3_O, x = px - y * NT3_O;
+      const int cell = (y + 2) * 11 + x + 2;
+      uint32_t lo[3], hi[3];
+      nat_split2<3>(v[0], v[1], lo);
+      nat_split2<3>(v[2], v[3], hi);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) *(uint2*)&sm[t * DX_T + cell * DX_R + c4] = make_uint2(lo[t], hi[t]);
+    }
+  }
+  __syncthreads();
+  // ---- conv3 dX: 6 m-tiles of the 81 l2 pixels x this wave's 16 cin, 18 K steps ----
+  const int n3 = 16 * w + i16;
+  int cell3[6];
+#pragma unroll
+  for (int mt = 0; mt < 6; ++mt) {
+    const int m = min(16 * mt + i16, NT2_P - 1);
+    const int y = m / NT2_O, x = m - y * NT2_O;
+    cell3[mt] = (y + 2) * 11 + x + 2;
+  }
+  f32x4 acc3[6];
+#pragma unroll
+  for (int mt = 0; mt < 6; ++mt) acc3[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const uint16_t* wb3 = w3x + (int64_t)n3 * NT_K3 + 8 * g;
+  bf16x8 bq[3][3];
+  auto ldb3 = [&](int st, bf16x8 (&dst)[3]) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t) dst[t] = *(const bf16x8*)(wb3 + (int64_t)t * NT2_N * NT_K3 + st * 32);
+  };
+  ldb3(0, bq[0]);
+  ldb3(1, bq[1]);
+#pragma unroll
+  for (int st = 0; st < 18; ++st) {
+    if (st + 2 < 18) ldb3(st + 2, bq[(st + 2) % 3]);
+    const int tap = st >> 1, kh = tap / 3, kw = tap - kh * 3;
+    const int off = -(kh * 11 + kw) * DX_R + 32 * (st & 1) + 8 * g;   // source dl3 pixel (y - kh, x - kw)
+#pragma unroll
+    for (int mt = 0; mt < 6; ++mt) {
+      bf16x8 a[3];
+      const uint16_t* ap = sm + cell3[mt] * DX_R + off;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) a[t] = *(const bf16x8*)(ap + t * DX_T);
+      acc3[mt] = c23_mfma6(a, bq[st % 3], acc3[mt]);
+    }
+  }
+  __syncthreads();   // dl3 terms no longer read
+  zero_all();
+  __syncthreads();
+  // dl2 = acc * (l2 > 0): out, and as terms into cells (y + 1, x + 1)
+#pragma unroll
+  for (int mt = 0; mt < 6; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 16 * mt + 4 * g + r;
+      if (m < NT2_P) {
+        const int64_t o = (b * NT2_P + m) * NT2_N + n3;
+        const float v = l2[o] > 0.f ? acc3[mt][r] : 0.f;
+        dl2[o] = v;
+        const int y = m / NT2_O, x = m - y * NT2_O, cell = (y + 1) * 11 + x + 1;
+        const float hf = __uint_as_float(nat_bf16_rn(v) << 16);
+        const float r1 = v - hf;
+        const float mf = __uint_as_float(nat_bf16_rn(r1) << 16);
+        sm[0 * DX_T + cell * DX_R + n3] = (uint16_t)(__float_as_uint(hf) >> 16);
+        sm[1 * DX_T + cell * DX_R + n3] = (uint16_t)(__float_as_uint(mf) >> 16);
+        sm[2 * DX_T + cell * DX_R + n3] = (uint16_t)nat_bf16_rn(r1 - mf);
+      }
+    }
+  __syncthreads();
+  // ---- conv2 dX: 4 parity classes x 7 m-tiles (100 pixels of the 10 x 10 class grid) x 2
+  // n-tiles of 16 cin; wave w: n-tile w & 1, m-tiles (w >> 1) + 2 j of every class ----
+  const int n2 = 16 * (w & 1) + i16;
+  const int mh = w >> 1;
+  const uint16_t* wb2 = w2x + (int64_t)n2 * NT_X2 + 8 * g;
+#pragma unroll
+  for (int cl = 0; cl < 4; ++cl) {
+    const int py = cl >> 1, px = cl & 1;
+    int cell2[4];
+    f32x4 acc2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = min(16 * (mh + 2 * j) + i16, 99);
+      const int ci = m / 10, cj = m - ci * 10;
+      cell2[j] = (ci + 1) * 11 + cj + 1;
+      acc2[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    // K step ks: real tap (th, tw) = ((ks >> 1) >> 1, (ks >> 1) & 1), kernel tap (py + 2 th, px + 2 tw)
+    auto ldb2 = [&](int ks, bf16x8 (&dst)[3]) {
+      const int tp = ks >> 1, th = tp >> 1, tw = tp & 1;
+      const int tap = (py + 2 * th) * 4 + px + 2 * tw;
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+        dst[t] = *(const bf16x8*)(wb2 + (int64_t)t * NT1_N * NT_X2 + tap * 64 + 32 * (ks & 1));
+    };
+    ldb2(0, bq[0]);
+    ldb2(1, bq[1]);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      if (ks + 2 < 8) ldb2(ks + 2, bq[(ks + 2) % 3]);
+      const int tp = ks >> 1, th = tp >> 1, tw = tp & 1;
+      const int off = -(th * 11 + tw) * DX_R + 32 * (ks & 1) + 8 * g;   // dl2 pixel (i - th, j - tw)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (mh + 2 * j >= 7) continue;                  // (wave-uniform) the class's 7 tiles
+        bf16x8 a[3];
+        const uint16_t* ap = sm + cell2[j] * DX_R + off;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) a[t] = *(const bf16x8*)(ap + t * DX_T);
+        acc2[j] = c23_mfma6(a, bq[ks % 3], acc2[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (mh + 2 * j >= 7) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * (mh + 2 * j) + 4 * g + r;
+        if (m < 100) {
+          const int ci = m / 10, cj = m - ci * 10;
+          const int64_t o = (b * NT1_P + (2 * ci + py) * NT1_O + 2 * cj + px) * NT1_N + n2;
+          dl1[o] = l1[o] > 0.f ? acc2[j][r] : 0.f;
+        }
+      }
+    }
+  }
+}
+
 // the policy / value head of B states (one wave each) on the 512-wide fc output, + the action
 // draw and fused env act when sel.mode >= 0 (agent.py:59-62, network.py:72)
 __global__ void __launch_bounds__(256) k_nat_head(const float* __restrict__ l4, int64_t B, const float* __restrict__ Wp,
@@ -1101,7 +1345,7 @@ __global__ void __launch_bounds__(256) k_nat_head(const float* __restrict__ l4, 
 #define NAT_GROUPS 8
 struct NatPlan {
   int head_split, ns1, ns2, ns3, kc1, kc2, kc3;
-  int64_t dz, dl4, dl3, dl2, dl1, terms, hgrad, hcol, hslab, fccol, s1, s2, s3, c1, c2, c3, g1, g2, g3, total;
+  int64_t dz, dl4, dl3, dl2, dl1, terms, hgrad, hcol, hslab, fccol, s1, s2, s3, c1, c2, c3, g1, g2, g3, wprep, total;
 };
 // the reduction split of a weight-gradient pass: ~target workgroups over its m tiles
 static void dw_split(int64_t R, int mtiles, int target, int& ns, int& kc) {
@@ -1140,6 +1384,7 @@ static NatPlan nat_plan(const NetLayout& L, int64_t B) {
   p.g1 = take((int64_t)NAT_GROUPS * NT_K1 * NT1_N);
   p.g2 = take((int64_t)NAT_GROUPS * NT_K2 * NT2_N);
   p.g3 = take((int64_t)NAT_GROUPS * NT_K3 * NT3_N);
+  p.wprep = take(A3C_NAT_PREP_BYTES / 4);   // the per-op path's weight terms (the engine's are in the slot)
   p.total = o;
   return p;
 }
@@ -1202,7 +1447,20 @@ static int nat_fuse23() {
   static const int v = (int)A3C_AB_KNOB("A3C_NAT_FUSE23", 1);   // A/B: 0 = separate conv2 / conv3 passes
   return v;
 }
+static int nat_fuse123() {
+  static const int v = (int)A3C_AB_KNOB("A3C_NAT_FUSE123", 1);   // A/B: 0 = conv1 its own launch
+  return v;
+}
+// A/B: 1 = conv3 dX + conv2 dX as one per-sample launch (k_nat_dx32): 153 us alone against 85 + 107
+// for the two passes, but the whole bench loses (r6fu: 1.51M vs 1.60M) -- its 52 KB of LDS per
+// workgroup keeps the rollout's 96 KB conv workgroups off the CUs it holds; so it stays off
+static int nat_fuse_dx() {
+  static const int v = (int)A3C_AB_KNOB("A3C_NAT_FUSE_DX", 0);
+  return v;
+}
+bool a3c_nat_dx_fused() { return nat_fuse_dx() != 0; }
 bool a3c_nat_conv23_fused() { return nat_fuse23() != 0; }
+bool a3c_nat_conv123_fused() { return nat_fuse23() && nat_fuse123(); }
 static int nat_c1_bf() {
   static const int v = (int)A3C_AB_KNOB("A3C_NAT_C1_BF", 1);   // A/B: 0 = the fp32 MFMA conv1 forward
   return v;
@@ -1236,6 +1494,7 @@ int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const Stat
   NatGemm a = {};
   switch (pass) {
     case NAT_C1F:
+      if (w1t && nat_fuse23() && nat_fuse123()) return 0;   // inside NAT_C2F's launch
       if (w1t && nat_c1_bf()) {
         const int M = (int)(B * NT1_P);
         if (nat_bf1(NAT_C1F))
@@ -1252,9 +1511,16 @@ int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const Stat
       a.M = (int)(B * NT1_P); a.N = NT1_N; a.K = NT_K1; a.scale = 1.0f / 255.0f;
       return nat_go<NG_FWD1, 1, 32>(a, 1, s);
     case NAT_C2F:
-      if (w1t && nat_fuse23()) {   // conv2 + conv3 in one launch (k_nat_conv23); NAT_C3F is then empty
-        hipLaunchKernelGGL(k_nat_conv23, dim3((unsigned)B), dim3(256), 0, s, l1, w1t + A3C_NAT_W2T_OFF / 2,
-                           P + L.off[N_L2B], w1t + A3C_NAT_W3T_OFF / 2, P + L.off[N_L3B], (float*)l2, (float*)l3);
+      if (w1t && nat_fuse23()) {   // conv2 + conv3 (+ conv1) in one launch; NAT_C3F (NAT_C1F) then empty
+        if (nat_fuse123())
+          hipLaunchKernelGGL(k_nat_conv23<true>, dim3((unsigned)B), dim3(256), 0, s, (const float*)nullptr,
+                             w1t + A3C_NAT_W2T_OFF / 2, P + L.off[N_L2B], w1t + A3C_NAT_W3T_OFF / 2,
+                             P + L.off[N_L3B], (float*)l2, (float*)l3, sa, w1t, P + L.off[N_L1B], (float*)l1,
+                             1.0f / 255.0f);
+        else
+          hipLaunchKernelGGL(k_nat_conv23<false>, dim3((unsigned)B), dim3(256), 0, s, l1, w1t + A3C_NAT_W2T_OFF / 2,
+                             P + L.off[N_L2B], w1t + A3C_NAT_W3T_OFF / 2, P + L.off[N_L3B], (float*)l2, (float*)l3,
+                             sa, (const uint16_t*)nullptr, (const float*)nullptr, (float*)nullptr, 0.f);
         A3C_CHECK(hipGetLastError());
         return 0;
       }
@@ -1303,6 +1569,12 @@ int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const Stat
       return nat_bf(NAT_C3W) ? nat_go_bf<NG_DW, 3, 64, 3>(a, (unsigned)p.ns3, s, nat_bf1(NAT_C3W), nat_pf2(NAT_C3W))
                            : nat_go<NG_DW, 3, 64>(a, (unsigned)p.ns3, s);
     case NAT_C3X:     // dl2 = col2im(dl3 W3^T) * (l2 > 0)
+      if (w1t && nat_fuse_dx()) {   // and dl1 in the same launch (k_nat_dx32); NAT_C2X then empty
+        hipLaunchKernelGGL(k_nat_dx32, dim3((unsigned)B), dim3(256), 0, s, bws + p.dl3, l2, l1,
+                           w1t + A3C_NAT_W3X_OFF / 2, w1t + A3C_NAT_W2X_OFF / 2, bws + p.dl2, bws + p.dl1);
+        A3C_CHECK(hipGetLastError());
+        return 0;
+      }
       a.X = l2; a.dY = bws + p.dl3; a.Wt = P + L.off[N_L3W]; a.Y = bws + p.dl2;
       a.M = (int)(B * NT2_P); a.N = NT2_N; a.K = 3 * 3 * NT3_N;
       return nat_bf(NAT_C3X) ? nat_go_bf<NG_DX, 3, 64, 3>(a, 1, s, nat_bf1(NAT_C3X), nat_pf2(NAT_C3X))
@@ -1313,6 +1585,7 @@ int a3c_nat_pass_launch(int pass, const NetLayout& L, const float* P, const Stat
       return nat_bf(NAT_C2W) ? nat_go_bf<NG_DW, 2, 64, 3>(a, (unsigned)p.ns2, s, nat_bf1(NAT_C2W), nat_pf2(NAT_C2W))
                            : nat_go<NG_DW, 2, 64>(a, (unsigned)p.ns2, s);
     case NAT_C2X:     // dl1 = col2im(dl2 W2^T) * (l1 > 0), per stride-2 parity class
+      if (w1t && nat_fuse_dx()) return 0;
       a.X = l1; a.dY = bws + p.dl2; a.Wt = P + L.off[N_L2W]; a.Y = bws + p.dl1;
       a.M = (int)(B * (NT1_O / 2) * (NT1_O / 2)); a.N = NT1_N; a.K = 2 * 2 * NT2_N;
       return nat_bf(NAT_C2X) ? nat_go_bf<NG_DX, 2, 32, 3>(a, 4, s, nat_bf1(NAT_C2X), nat_pf2(NAT_C2X))
@@ -1334,8 +1607,8 @@ __global__ void k_nat_prep(const int64_t* __restrict__ tau_src, int64_t* __restr
   if (sig) (void)__hip_atomic_fetch_add(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 static int nat_w1_terms_launch(const NetLayout& L, const float* P, uint16_t* w1t, hipStream_t s) {
-  const int all = nat_fuse23() ? 1 : 0;
-  const int n = NT1_N * NT_K1 + (all ? NT2_N * NT_K2 + NT3_N * NT_K3 : 0);
+  const int all = nat_fuse23() || nat_fuse_dx() ? 1 : 0;
+  const int n = NT1_N * NT_K1 + (all ? NT2_N * NT_K2 + NT3_N * NT_K3 + NT1_N * NT_X2 + NT2_N * NT_K3 : 0);
   hipLaunchKernelGGL(k_nat_w_terms, dim3((n + 255) / 256), dim3(256), 0, s, P + L.off[N_L1W], P + L.off[N_L2W],
                      P + L.off[N_L3W], w1t, all);
   A3C_CHECK(hipGetLastError());
@@ -1416,12 +1689,18 @@ int a3c_nat_fused_tab(const NetLayout& L, TensorTab* tt) {
 int a3c_nat_backward_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, const float* l1,
                             const float* l2, const float* l3, const float* l4, const float* z,
                             const int32_t* actions, const float* target, float beta, int literal, float* grads,
-                            float* loss_out, float* ws, hipStream_t s, const ReturnsArgs* ra_in, const SumsqFused* sf) {
+                            float* loss_out, float* ws, hipStream_t s, const ReturnsArgs* ra_in, const SumsqFused* sf,
+                            const uint16_t* wt) {
   if (L.trunk != A3C_TRUNK_NATURE || B <= 0 || B * NT1_P > 0x7fffffffLL)
     return a3c_set_error(A3C_ERR_INVALID, "a3c_nat_backward", "nature trunk, 0 < B, B * 400 < 2^31");
   ReturnsArgs ra = {};
   if (ra_in) ra = *ra_in;
   const NatPlan p = nat_plan(L, B);
+  if (!wt) {   // one-off backward: the weight terms into the workspace first
+    uint16_t* t = (uint16_t*)(ws + p.wprep);
+    if (int rc = nat_w1_terms_launch(L, P, t, s)) return rc;
+    wt = t;
+  }
   float* dz = ws + p.dz;
   float* dl4 = ws + p.dl4;
   float* terms = ws + p.terms;
@@ -1472,7 +1751,7 @@ int a3c_nat_backward_launch(const NetLayout& L, const float* P, const StateAddr&
   }
   if (rc) return rc;
   for (int pass = NAT_C3W; pass <= NAT_C1W; ++pass) {
-    rc = a3c_nat_pass_launch(pass, L, P, sa, B, l1, l2, l3, l4, nullptr, nullptr, ws, s);
+    rc = a3c_nat_pass_launch(pass, L, P, sa, B, l1, l2, l3, l4, wt, nullptr, ws, s);
     if (rc) return rc;
   }
   // the weight slabs in NAT_GROUPS fixed-order groups, then k_finalize: every segment, the loss
@@ -1573,5 +1852,5 @@ extern "C" int a3c_nature_loss_backward(const a3c_net_desc* net, const float* pa
     return a3c_set_error(A3C_ERR_INVALID, "a3c_nature_loss_backward", "bad argument");
   return a3c_nat_backward_launch(L, params, nat_states(states, B), B, l1, l2, l3, l4, z, actions, target, beta,
                                  literal_adv, grads, loss_out, nat_align(workspace), (hipStream_t)stream, nullptr,
-                                 nullptr);
+                                 nullptr, nullptr);
 }

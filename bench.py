@@ -246,13 +246,13 @@ def nature_roofline(eng, _lib, E, n, iter_ms):
     last rollout's n E samples); the dominant one by time share of the iteration names the roofline
     (MFMA-bound: algorithmic FLOP per launch / its average launch duration, against the FP32 matrix peak)."""
     kernels = {}
-    fused23 = False
+    inside = []                        # passes that run inside conv2's launch (k_nat_conv23)
     for name, kid in _lib.KER_NAT.items():
-        if name == 'conv3_fwd':
+        if name in ('conv1_fwd', 'conv3_fwd', 'conv2_dx'):
             try:
                 ms = eng.time_kernel(kid, 10)
-            except _lib.A3CError:      # conv3 runs inside conv2's launch (k_nat_conv23)
-                fused23 = True
+            except _lib.A3CError:
+                inside.append(name)
                 continue
         else:
             ms = eng.time_kernel(kid, 10)
@@ -263,10 +263,16 @@ def nature_roofline(eng, _lib, E, n, iter_ms):
         kernels['nat_' + name] = dict(avg_ms=round(ms, 4), per_iter=per_iter, share=round(ms * per_iter / iter_ms, 3),
                                       bound='mfma', achieved=round(flop / (ms * 1e-3) / 1e12, 2), unit='TFLOP/s',
                                       flop_per_launch=flop)
-    if fused23:                        # the conv2 launch is conv2 + conv3 forward
+    fin = [p for p in inside if p.endswith('_fwd')]
+    if fin:                            # the conv2 launch is conv2 + conv3 (+ conv1) forward (k_nat_conv23)
         k = kernels.pop('nat_conv2_fwd')
-        flop = (NAT_FLOP['conv2_fwd'] + NAT_FLOP['conv3_fwd']) * E
-        kernels['nat_conv23_fwd'] = dict(k, achieved=round(flop / (k['avg_ms'] * 1e-3) / 1e12, 2), flop_per_launch=flop)
+        flop = sum(NAT_FLOP[p] for p in ['conv2_fwd'] + fin) * E
+        key = 'nat_conv123_fwd' if 'conv1_fwd' in fin else 'nat_conv23_fwd'
+        kernels[key] = dict(k, achieved=round(flop / (k['avg_ms'] * 1e-3) / 1e12, 2), flop_per_launch=flop)
+    if 'conv2_dx' in inside:           # the conv3 dX launch is conv3 + conv2 dX (k_nat_dx32)
+        k = kernels.pop('nat_conv3_dx')
+        flop = (NAT_FLOP['conv3_dx'] + NAT_FLOP['conv2_dx']) * n * E
+        kernels['nat_conv32_dx'] = dict(k, achieved=round(flop / (k['avg_ms'] * 1e-3) / 1e12, 2), flop_per_launch=flop)
     dom = max(kernels, key=lambda k: kernels[k]['avg_ms'] * kernels[k]['per_iter'])
     d = kernels[dom]
     traffic = None

@@ -74,11 +74,11 @@ def test_nature_pass_timing_hook():
     eng.iterate()
     torch.cuda.synchronize()
     for name, k in _lib.KER_NAT.items():
-        if name == 'conv3_fwd':   # with the fused conv2 + conv3 launch it has no launch of its own
+        if name in ('conv1_fwd', 'conv3_fwd', 'conv2_dx'):   # inside a fused launch: none of their own
             try:
                 ms = eng.time_kernel(k, 3)
             except _lib.A3CError as e:
-                assert 'k_nat_conv23' in str(e)
+                assert 'k_nat_' in str(e)
                 continue
         else:
             ms = eng.time_kernel(k, 3)

@@ -18,8 +18,12 @@ def main(path):
         n = name.replace(' ', '')
         if n.startswith('k_nat_conv1_bf'):
             key = 'conv1_fwd'
+        elif n.startswith('k_nat_conv23<true>'):
+            key = 'conv123_fwd'
         elif n.startswith('k_nat_conv23'):
             key = 'conv23_fwd'
+        elif n.startswith('k_nat_dx32'):
+            key = 'conv32_dx'
         else:
             m = re.match(r'k_nat_gemm(?:_bf)?<(\d+),(\d+),', n)
             if not m:
