@@ -1607,8 +1607,10 @@ __global__ void k_nat_prep(const int64_t* __restrict__ tau_src, int64_t* __restr
   if (sig) (void)__hip_atomic_fetch_add(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 static int nat_w1_terms_launch(const NetLayout& L, const float* P, uint16_t* w1t, hipStream_t s) {
+  // (the forward forms for k_nat_conv23, the dX forms only for k_nat_dx32)
   const int all = nat_fuse23() || nat_fuse_dx() ? 1 : 0;
-  const int n = NT1_N * NT_K1 + (all ? NT2_N * NT_K2 + NT3_N * NT_K3 + NT1_N * NT_X2 + NT2_N * NT_K3 : 0);
+  const int n = NT1_N * NT_K1 + (all ? NT2_N * NT_K2 + NT3_N * NT_K3 : 0) +
+                (nat_fuse_dx() ? NT1_N * NT_X2 + NT2_N * NT_K3 : 0);
   hipLaunchKernelGGL(k_nat_w_terms, dim3((n + 255) / 256), dim3(256), 0, s, P + L.off[N_L1W], P + L.off[N_L2W],
                      P + L.off[N_L3W], w1t, all);
   A3C_CHECK(hipGetLastError());
