@@ -947,10 +947,12 @@ __global__ void __launch_bounds__(256) k_nat_conv1_bf(StateAddr sa, const uint16
 // [term][cout][k]) streamed from L2 with a 3-tap register ring.  Replaces two K-chain-bound passes
 // of 324 / 392 tiles and a fold with one 256-workgroup launch and no l2 re-read from HBM.
 // ---------------------------------------------------------------------------------------
-// l1 terms: [term][y 20][x parity 2][x / 2 10][40 bf16]: a 16-lane fragment read walks consecutive
-// output pixels, which sit at x = 2 ox + kw -- parity-split rows of 80 B put them 80 B apart, the
-// 16 lanes on distinct banks.  l2 terms: [term][81][72 bf16] over the same LDS after conv2.
-#define C23_R1 40
+// l1 terms: [term][y 20][x parity 2][x / 2 10][32 bf16]: a 16-lane fragment read walks consecutive
+// output pixels, which sit at x = 2 ox + kw -- parity-split rows put them one row apart.
+// l2 terms: [term][81][72 bf16] over the same LDS after conv2.
+#ifndef C23_R1          // (A/B builds: -DC23_R1=40, rows padded for the fragment reads' banks: 96 KB)
+#define C23_R1 32          // unpadded: 77 KB, same time alone, room beside the backward (r6r32: 1.64M vs 1.59M)
+#endif
 #define C23_T1 (NT1_O * 2 * (NT1_O / 2) * C23_R1)   // bf16 per l1 term: 16000
 #define C23_R2 72
 #define C23_T2 (NT2_P * C23_R2)                     // 5832
