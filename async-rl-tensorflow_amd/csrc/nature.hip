@@ -1454,8 +1454,9 @@ static int nat_fuse123() {
   return v;
 }
 // A/B: 1 = conv3 dX + conv2 dX as one per-sample launch (k_nat_dx32): 153 us alone against 85 + 107
-// for the two passes, but the whole bench loses (r6fu: 1.51M vs 1.60M) -- its 52 KB of LDS per
-// workgroup keeps the rollout's 96 KB conv workgroups off the CUs it holds; so it stays off
+// for the two passes, but the whole bench loses (r6fu: 1.51M vs 1.60M; r6dxp: 1.58M vs 1.64M) --
+// two of its 52 KB workgroups on a CU keep the rollout's conv workgroup off it, and reserving LDS
+// so that only one fits (1.37M) starves the pass itself; so it stays off
 static int nat_fuse_dx() {
   static const int v = (int)A3C_AB_KNOB("A3C_NAT_FUSE_DX", 0);
   return v;
