@@ -361,9 +361,9 @@ def main():
     if args.lstm and args.algo != 'a3c':
         raise SystemExit('--lstm is an a3c head')
     nature = args.dqn_type == 'nature'
-    if nature and (args.algo != 'a3c' or args.lstm or args.env != 'device' or args.frames84):
+    if nature and (args.algo != 'a3c' or args.lstm or args.env != 'device'):
         raise SystemExit('--dqn-type nature: the A3C Network trunk (network.py:30-42) -- a3c, feed-forward head, '
-                         'device envs, raw RGB frames')
+                         'device envs')
     host = args.env == 'host'
     if host and args.update != 'sync':
         args.update = 'sync'              # host-stepped envs drive a synchronous engine

@@ -32,6 +32,18 @@ def test_nature_overlap_matches_oracle():
     check_overlap_vs_oracle(6, 16, 5, 3, rollouts=4, seed=520, frames=48, scale=2.0, learning_rate=2e-3, **NAT)
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('overlap', [False, True])
+def test_nature_frame84_mode_matches_oracle(overlap):
+    """Mode M2 (pre-sized 84x84 frames, copied by the fused head + screen kernel) on the nature trunk."""
+    if overlap:
+        check_overlap_vs_oracle(6, 16, 5, 0, rollouts=4, seed=540, frames=48, scale=2.0, learning_rate=2e-3,
+                                frame84=1, **NAT)
+    else:
+        check_sync_vs_oracle('a3c', 6, 8, 4, 0, iters=3, seed=541, frames=48, scale=2.0, learning_rate=2e-3,
+                             frame84=1, **NAT)
+
+
 @pytest.mark.timeout(900)
 def test_nature_bench_shape_sync_matches_oracle():
     """bench.py --dqn-type nature --update sync: Pong, 256 envs, n = 5, reference init."""
