@@ -973,6 +973,12 @@ __device__ inline f32x4 c23_mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f3
 // MFMA, its output (x/255 + bias, ReLU) written out for the backward and, as terms, into LDS.
 #define C123_PR 88                                   // bf16 per staged plane row (84 + 4)
 static_assert(HIST * IMG * C123_PR <= 3 * C23_T1, "planes fit the term LDS");
+#ifndef C23_PD     // weight-fragment prefetch distance in K steps (the ring holds C23_PD + 1 steps)
+#define C23_PD 2
+#endif
+#ifndef C23_BATCH  // 1: the plane staging issues all its loads before the first conversion
+#define C23_BATCH 1
+#endif
 template <bool C1>
 __global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1c, const uint16_t* __restrict__ w2t,
                                                     const float* __restrict__ b2, const uint16_t* __restrict__ w3t,
@@ -988,6 +994,27 @@ __global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1
     RingRows ring;
     ring.init(sa, sa.tau_ptr ? *sa.tau_ptr : 0);
     const int st = ring.step_of((int)b), e = (int)b - st * ring.E;
+#if C23_BATCH
+    // every dword of the 4 planes in flight at once (28 per thread), then converted and stored
+    constexpr int NQ = HIST * PLANE / 4, PQ = PLANE / 4, PER = (NQ + 255) / 256;
+    const uint32_t* pl4[HIST];
+#pragma unroll
+    for (int c = 0; c < HIST; ++c) pl4[c] = (const uint32_t*)ring.plane(e, st, c);
+    uint32_t pv[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int q = tid + 256 * i, c = q / PQ;
+      pv[i] = q < NQ ? pl4[c < HIST ? c : 0][q - c * PQ] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int q = tid + 256 * i;
+      if (q < NQ) {
+        const int c = q / PQ, r = q - c * PQ, y = r / (IMG / 4), x4 = (r - y * (IMG / 4)) * 4;
+        *(uint2*)&sm[(c * IMG + y) * C123_PR + x4] = nat_u8x4_bf16(pv[i]);
+      }
+    }
+#else
 #pragma unroll
     for (int c = 0; c < HIST; ++c) {
       const uint32_t* src = (const uint32_t*)ring.plane(e, st, c);
@@ -996,6 +1023,7 @@ __global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1
         *(uint2*)&sm[(c * IMG + y) * C123_PR + x4] = nat_u8x4_bf16(src[q]);
       }
     }
+#endif
     __syncthreads();
     // ---- conv1: 25 m-tiles x 2 n-tiles of 16; wave w: n-tile w & 1, m-tiles (w >> 1) + 2 i ----
     const int n1 = 16 * (w & 1) + i16;
@@ -1010,16 +1038,16 @@ __global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1
       acc1[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
     }
     const uint16_t* wb1 = w1t + n1 * NT_K1 + 8 * g;
-    bf16x8 q1[3][3];
+    bf16x8 q1[C23_PD + 1][3];
     auto ldb1 = [&](int ks, bf16x8 (&dst)[3]) {
 #pragma unroll
       for (int t = 0; t < 3; ++t) dst[t] = *(const bf16x8*)(wb1 + t * NT1_N * NT_K1 + ks * 32);
     };
-    ldb1(0, q1[0]);
-    ldb1(1, q1[1]);
+#pragma unroll
+    for (int q = 0; q < C23_PD; ++q) ldb1(q, q1[q]);
 #pragma unroll
     for (int ks = 0; ks < NT_K1 / 32; ++ks) {
-      if (ks + 2 < NT_K1 / 32) ldb1(ks + 2, q1[(ks + 2) % 3]);
+      if (ks + C23_PD < NT_K1 / 32) ldb1(ks + C23_PD, q1[(ks + C23_PD) % (C23_PD + 1)]);
       const int cin = ks >> 1, kh = 4 * (ks & 1) + g;
       const uint16_t* rp = sm + (cin * IMG + kh) * C123_PR;
 #pragma unroll
@@ -1027,7 +1055,7 @@ __global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1
         if (mh + 2 * i >= NT1_P / 16) continue;          // (wave-uniform) the 25 tiles
         const uint2 u0 = *(const uint2*)(rp + base1[i]), u1 = *(const uint2*)(rp + base1[i] + 4);
         const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(u0.x, u0.y, u1.x, u1.y));
-        const bf16x8* bb = q1[ks % 3];
+        const bf16x8* bb = q1[ks % (C23_PD + 1)];
         acc1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb[2], acc1[i], 0, 0, 0);
         acc1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb[1], acc1[i], 0, 0, 0);
         acc1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb[0], acc1[i], 0, 0, 0);
@@ -1084,16 +1112,16 @@ __global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1
 #pragma unroll
   for (int mt = 0; mt < 6; ++mt) acc2[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const uint16_t* wb2 = w2t + (int64_t)n * NT_K2 + 8 * g;
-  bf16x8 bq[3][3];
+  bf16x8 bq[C23_PD + 1][3];
   auto ldb2 = [&](int tap, bf16x8 (&dst)[3]) {
 #pragma unroll
     for (int t = 0; t < 3; ++t) dst[t] = *(const bf16x8*)(wb2 + (int64_t)t * NT2_N * NT_K2 + tap * 32);
   };
-  ldb2(0, bq[0]);
-  ldb2(1, bq[1]);
+#pragma unroll
+  for (int q = 0; q < C23_PD; ++q) ldb2(q, bq[q]);
 #pragma unroll
   for (int tap = 0; tap < 16; ++tap) {
-    if (tap + 2 < 16) ldb2(tap + 2, bq[(tap + 2) % 3]);
+    if (tap + C23_PD < 16) ldb2(tap + C23_PD, bq[(tap + C23_PD) % (C23_PD + 1)]);
     const int kh = tap >> 2, kw = tap & 3;
     const int toff = (kh * 2 + (kw & 1)) * (NT1_O / 2) + (kw >> 1);
 #pragma unroll
@@ -1102,7 +1130,7 @@ __global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1
       const uint16_t* ap = sm + (base2[mt] + toff) * C23_R1 + 8 * g;
 #pragma unroll
       for (int t = 0; t < 3; ++t) a[t] = *(const bf16x8*)(ap + t * C23_T1);
-      acc2[mt] = c23_mfma6(a, bq[tap % 3], acc2[mt]);
+      acc2[mt] = c23_mfma6(a, bq[tap % (C23_PD + 1)], acc2[mt]);
     }
   }
   __syncthreads();   // every wave is done reading the l1 terms
@@ -1133,8 +1161,8 @@ __global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1
 #pragma unroll
     for (int t = 0; t < 3; ++t) dst[t] = *(const bf16x8*)(wb3 + (int64_t)t * NT3_N * NT_K3 + st * 32);
   };
-  ldb3(0, bq[0]);
-  ldb3(1, bq[1]);
+#pragma unroll
+  for (int q = 0; q < C23_PD; ++q) ldb3(q, bq[q]);
   __syncthreads();
   // ---- conv3: 4 m-tiles of 16 pixels (49 valid), 18 K steps (9 taps x 2 channel halves) ----
   int base3[4];
@@ -1149,7 +1177,7 @@ __global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1
   for (int mt = 0; mt < 4; ++mt) acc3[mt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int st = 0; st < 18; ++st) {
-    if (st + 2 < 18) ldb3(st + 2, bq[(st + 2) % 3]);
+    if (st + C23_PD < 18) ldb3(st + C23_PD, bq[(st + C23_PD) % (C23_PD + 1)]);
     const int tap = st >> 1, kh = tap / 3, kw = tap - kh * 3;
     const int off = (kh * NT2_O + kw) * C23_R2 + 32 * (st & 1) + 8 * g;
 #pragma unroll
@@ -1158,7 +1186,7 @@ __global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1
       const uint16_t* ap = sm + base3[mt] * C23_R2 + off;
 #pragma unroll
       for (int t = 0; t < 3; ++t) a[t] = *(const bf16x8*)(ap + t * C23_T2);
-      acc3[mt] = c23_mfma6(a, bq[st % 3], acc3[mt]);
+      acc3[mt] = c23_mfma6(a, bq[st % (C23_PD + 1)], acc3[mt]);
     }
   }
   const float b3n = b3[n];
