@@ -1392,9 +1392,12 @@ static NatPlan nat_plan(const NetLayout& L, int64_t B) {
   int64_t o = 0;
   auto take = [&](int64_t floats) { int64_t r = o; o += (floats + 63) & ~(int64_t)63; return r; };
   p.head_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(NT_FC, L.zs, (int)B, 128));
-  dw_split(B * NT1_P, 2, 512, p.ns1, p.kc1);      // M = 256 in 128-row tiles
-  dw_split(B * NT2_P, 8, 512, p.ns2, p.kc2);      // M = 512 in 64-row tiles
-  dw_split(B * NT3_P, 9, 512, p.ns3, p.kc3);      // M = 576
+  // workgroups per dW pass: 1536 (r6dwg: conv3 / conv2 / conv1 dW 62 / 89 / 97 -> 51 / 74 / 81 us
+  // alone against 512, the bench 1.651M -> 1.661M; 256 / 128 lose 16 / 42 %)
+  static const int wgs = (int)A3C_AB_KNOB("A3C_NAT_DW_WGS", 1536);
+  dw_split(B * NT1_P, 2, wgs, p.ns1, p.kc1);      // M = 256 in 128-row tiles
+  dw_split(B * NT2_P, 8, wgs, p.ns2, p.kc2);      // M = 512 in 64-row tiles
+  dw_split(B * NT3_P, 9, wgs, p.ns3, p.kc3);      // M = 576
   p.dz = take(B * L.zs);
   p.dl4 = take(B * NT_FC);
   p.dl3 = take(B * NT_FLAT);
