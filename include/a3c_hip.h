@@ -502,8 +502,12 @@ int a3c_engine_slot_buffers(a3c_engine* eng, int slot, a3c_engine_buffers* out);
 #define A3C_KER_FC_PART 6      /* fc as K-slice partials (overlap mode; the head folds them)  */
 /* nature trunk engines (nature.hip k_nat_gemm passes): forward over E states of the live
  * parameters, backward passes over the n*E samples of the last back-propagated rollout */
+/* The release build runs the three forward convolutions of a state as ONE launch (the per-state
+ * kernel k_nat_conv23, nature.hip) under A3C_KER_NAT_C2F; A3C_KER_NAT_C1F and _C3F then have no
+ * launch of their own and a3c_engine_time_kernel returns A3C_ERR_INVALID for them (likewise
+ * _C2X in builds that fuse the two dX passes under _C3X). */
 #define A3C_KER_NAT_C1F 7      /* conv1 8x8/4 4->32 forward (u8 ring -> l1), B = E         */
-#define A3C_KER_NAT_C2F 8      /* conv2 4x4/2 32->64 forward                               */
+#define A3C_KER_NAT_C2F 8      /* conv2 4x4/2 32->64 forward (release: conv1+conv2+conv3)  */
 #define A3C_KER_NAT_C3F 9      /* conv3 3x3/1 64->64 forward                               */
 #define A3C_KER_NAT_FCF 10     /* fc 3136->512 forward (split-K GEMM + bias/ReLU fold)      */
 #define A3C_KER_NAT_C3W 11     /* conv3 weight gradient (slabs), B = n*E                  */
