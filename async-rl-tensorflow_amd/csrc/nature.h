@@ -32,8 +32,9 @@ inline int64_t nat_act_floats() { return (int64_t)NT_A1 + NT_A2 + NT_FLAT + NT_F
 // forward of B states s_{tau0 + b / E} (sa) with parameters P.  Activations [B][...] NHWC:
 // l1 [B][12800], l2 [B][5184], l3 [B][3136] (the (h,w,c) flatten of network.py's linear), l4 [B][512];
 // z [B][zs] (logits, value); sel.mode >= 0: action draw + fused env act (as the NIPS head kernels).
-// ws: a3c_nat_fwd_ws_floats(B) floats (split-K slabs; with w1t null, also conv1's bf16 weight terms,
-// prepared there first).  w1t: the terms a3c_nat_prep_launch made from P (the engine's rollouts).
+// ws: a3c_nat_fwd_ws_floats(B) floats (split-K slabs; with w1t null, also the prepared weight
+// terms, made there first).  w1t: the prepared block a3c_nat_prep_launch made from P (the engine's
+// rollouts: conv1's terms at its start, then the conv2 / conv3 forms, A3C_NAT_*_OFF).
 int64_t a3c_nat_fwd_ws_floats(int64_t B);
 int a3c_nat_forward_launch(const NetLayout& L, const float* P, const StateAddr& sa, int64_t B, float* l1, float* l2,
                            float* l3, float* l4, float* z, const HeadSelect& sel, const uint16_t* w1t, float* ws,
@@ -54,7 +55,8 @@ int a3c_nat_backward_launch(const NetLayout& L, const float* P, const StateAddr&
 int a3c_nat_fused_tab(const NetLayout& L, TensorTab* tt);
 // the single launches behind both (a3c_engine_time_kernel): forward passes over B states
 // (fws: the fc's split-K slabs), backward passes over B samples on the plan's buffers in bws
-// (valid after a backward of the same B has filled them)
+// (valid after a backward of the same B has filled them); w1t: the prepared block (null: the
+// per-layer forms of the passes that need none)
 enum { NAT_C1F = 0, NAT_C2F, NAT_C3F, NAT_FCF, NAT_C3W, NAT_C3X, NAT_C2W, NAT_C2X, NAT_C1W };
 enum { NAT_FCW = NAT_C1W + 1, NAT_FCX };
 // conv2 + conv3 forward run as one launch (k_nat_conv23, under NAT_C2F; NAT_C3F launches nothing)
