@@ -392,10 +392,12 @@ def _hog_worker(rank, world, port, out, lockstep, cfg):
 @pytest.mark.parametrize('world,lockstep,cfg', [(2, True, {}), (2, False, {}), (4, True, {}), (4, False, {}),
                                                 (2, True, dict(algo='q', tq=300)), (4, True, dict(algo='q', A=4, lives=5, tq=300)),
                                                 (2, True, dict(ov=True)), (4, False, dict(ov=True)),
-                                                (2, True, dict(algo='q', tq=300, ov=True))],
+                                                (2, True, dict(algo='q', tq=300, ov=True)),
+                                                (2, True, dict(dqn='nature', split=0)),
+                                                (2, True, dict(dqn='nature', split=0, ov=True))],
                          ids=['w2-lockstep', 'w2-free', 'w4-lockstep', 'w4-free', 'w2-q-lockstep',
                               'w4-q-breakout-lockstep', 'w2-overlap-lockstep', 'w4-overlap-free',
-                              'w2-q-overlap-lockstep'])
+                              'w2-q-overlap-lockstep', 'w2-nature-lockstep', 'w2-nature-overlap-lockstep'])
 def test_hogwild_sharded_ps(world, lockstep, cfg):
     """`world` ranks on one GPU push into each other's IPC-mapped shards.  Lock-step: each rank runs
     the production Engine.iterate_hogwild in its turn (rollout, push, pull, commit), which must
