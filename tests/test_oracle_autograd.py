@@ -141,3 +141,42 @@ def test_lstm_oracle_matches_torch_autograd():
                                    atol=1e-12, err_msg=k)
     carry = fwd['lstm']['carry']
     np.testing.assert_allclose(carry[0], hp.detach().numpy(), rtol=1e-12, atol=1e-14)
+
+
+def test_nature_oracle_matches_torch_autograd():
+    """The nature trunk (network.py:30-42: conv 8x8/4 32, conv 4x4/2 64, conv 3x3/1 64, fc 3136 -> 512)
+    in the oracle's hand-written forward / backward against torch autograd in float64, under the
+    A3C losses -- what pins the engine's nature kernels (tests/test_gpu_nature.py compare them with
+    this oracle)."""
+    rng = np.random.default_rng(17)
+    A, B, beta = 6, 3, 0.01
+    shapes = R.param_shapes(A, 'a3c', dqn_type='nature')
+    p = R.init_params(shapes, seed=5, stddev=0.05)
+    for k in p:
+        if k.endswith('_b'):
+            p[k] = (rng.standard_normal(p[k].shape) * 0.05).astype(np.float32)
+    states = rng.integers(0, 256, (B, 84, 84, 4), dtype=np.uint8)
+    actions = rng.integers(0, A, B)
+    target = rng.standard_normal(B)
+    fwd = R.forward(p, states, 'a3c', dqn_type='nature')
+    x = torch.as_tensor(states, dtype=torch.float64).permute(0, 3, 1, 2) / 255.0
+    T = {k: torch.as_tensor(v, dtype=torch.float64).requires_grad_(True) for k, v in p.items()}
+    h = x
+    for name, s in (('l1', 4), ('l2', 2), ('l3', 1)):
+        h = F.relu(F.conv2d(h, T[name + '_w'].permute(3, 2, 0, 1), T[name + '_b'], stride=s))
+    flat = h.permute(0, 2, 3, 1).reshape(B, -1)               # (h, w, c) order: 7 x 7 x 64
+    h4 = F.relu(flat @ T['l4_w'] + T['l4_b'])
+    z = torch.cat([h4 @ T['p_w'] + T['p_b'], h4 @ T['q_w'] + T['q_b']], dim=1)
+    np.testing.assert_allclose(z.detach().numpy(), fwd['z'], rtol=1e-10, atol=1e-12)
+    losses, dz = R.a3c_loss_and_dz(fwd['z'], actions, target, beta, False)
+    logpi = F.log_softmax(z[:, :A], dim=1)
+    H = -(logpi.exp() * logpi).sum(1)
+    adv = torch.as_tensor(target) - z[:, A]
+    lp_a = logpi[torch.arange(B), torch.as_tensor(actions)]
+    loss = (-(lp_a * adv.detach()) - beta * H + 0.5 * adv * adv).sum()
+    assert np.isclose(loss.item(), losses['total'], rtol=1e-12)
+    loss.backward()
+    g = R.backward(p, fwd, dz, 'a3c', dqn_type='nature')
+    for k in p:
+        np.testing.assert_allclose(g[k].reshape(p[k].shape), T[k].grad.numpy(), rtol=1e-9, atol=1e-12,
+                                   err_msg=k)
