@@ -518,6 +518,13 @@ static bool spans_on() {
   static const bool on = A3C_KNOB("A3C_SPANS", 1) != 0;
   return on;
 }
+// the nature trunk's rollout states s_{tau + t}: its per-state conv kernel records its live launch
+// span in spans[1] (the nips engine's k_head_screen_conv12 slot, unused on this trunk)
+static StateAddr nat_step_addr(const a3c_engine* e, int t) {
+  StateAddr sa = ring_addr(e, t, e->counters);
+  sa.span = spans_on() ? e->spans + (size_t)SPAN_RECS * SPAN_WGS * 2 : nullptr;
+  return sa;
+}
 // conv fusion (k_head_screen_conv12) runs with the device envs and the fused screen
 static bool conv_fused(const a3c_engine* e) { return e->fuse_conv && !e->ext && e->fused_screen; }
 // the fused rollout's fc as K-slice partials folded by the head (feed-forward head only)
@@ -677,7 +684,7 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
   }
   int rc;
   if (e->nat)
-    rc = a3c_nat_forward_launch(L, sl.P, ring_addr(e, t, e->counters), E, sl.act_l1 + o * NT_A1,
+    rc = a3c_nat_forward_launch(L, sl.P, nat_step_addr(e, t), E, sl.act_l1 + o * NT_A1,
                                 sl.act_l2 + o * NT_A2, sl.act_l3 + o * NT_FLAT, sl.act_l4 + o * NT_FC, sl.z + o * zs, sel,
                                 (const uint16_t*)sl.prep, e->nat_fws, s);
   else
@@ -716,6 +723,7 @@ static int enqueue_rollout_end(a3c_engine* e, const Slot& sl, hipStream_t s) {
     }
     if (e->nat) {
       float* x = sl.nscr;
+      // (no span record: s_n is the next rollout's s_0, whose step-0 launch keys the same record)
       return a3c_nat_forward_launch(L, sl.P, ring_addr(e, n, e->counters), E, x, x + E * NT_A1,
                                     x + E * (NT_A1 + NT_A2), x + E * (NT_A1 + NT_A2 + NT_FLAT), sl.z + e->nE * L.zs,
                                     none, (const uint16_t*)sl.prep, e->nat_fws, s);

@@ -989,6 +989,9 @@ __global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i16 = lane & 15, g = lane >> 4;
   const int64_t b = blockIdx.x;
+  // the engine's live launch span (a3c_engine_span_stats 1, bench.py's roofline)
+  unsigned long long* srec = C1 ? span_rec(sa, sa.tau_ptr ? *sa.tau_ptr : 0) : nullptr;
+  span_begin(srec);
   if constexpr (C1) {
     // ---- the 4 history planes of state b as bf16 [cin][84][88] ----
     RingRows ring;
@@ -1197,6 +1200,7 @@ __global__ void __launch_bounds__(256) k_nat_conv23(const float* __restrict__ l1
       const int m = 16 * mt + 4 * g + r;
       if (m < NT3_P) l3[(b * NT3_P + m) * NT3_N + n] = fmaxf(acc3[mt][r] + b3n, 0.f);
     }
+  span_end(srec);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -58,3 +58,16 @@ def test_unfused_passes_keep_their_own_entries():
     bench, (roof, k) = _roof(set())
     assert set(k) == {'nat_' + n for n in TIMES}
     assert k['nat_conv2_fwd']['flop_per_launch'] == bench.NAT_FLOP['conv2_fwd'] * 256
+
+
+def test_live_span_names_the_roofline_time():
+    """With the per-state conv kernel's live spans (bench.py's timed region), the roofline takes the
+    live average (what the rocprof trace sees beside the backward) and keeps the isolated time."""
+    import bench
+    from src import _lib
+    eng = FakeEngine(_lib, TIMES, {'conv1_fwd', 'conv3_fwd'})
+    roof, k = bench.nature_roofline(eng, _lib, 256, 5, 0.776, {'nat_conv123_fwd': (42.1, 60.0, 1200)})
+    assert roof['kernel'] == 'nat_conv123_fwd' and roof['timing'].startswith('live')
+    assert roof['avg_us'] == 42.1 and roof['isolated_us'] == pytest.approx(36.9)
+    assert roof['frac'] == pytest.approx(3961520128 / 42.1e-6 / 1e12 / bench.PEAK_FP32_TFLOPS, rel=1e-3)
+    assert k['nat_conv123_fwd']['live_launches'] == 1200
