@@ -19,7 +19,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 extern "C" int a3c_set_error(int code, const char* what, const char* detail);
 
 // Environment switches.  A release build reads only the documented, tested ones (A3C_KNOB:
-// A3C_WAIT_VALUE, A3C_L2BITS, A3C_FC_SPLIT, A3C_FUSE_CONV, A3C_FUSED_SCREEN, A3C_SPANS; bench.py
+// A3C_WAIT_VALUE, A3C_L2BITS, A3C_FC_SPLIT, A3C_FUSE_CONV, A3C_FUSED_SCREEN, A3C_SPANS, A3C_LSTM_FCFOLD; bench.py
 // records every A3C_* variable that is set).  The A/B knobs of measured-and-rejected variants
 // (A3C_AB_KNOB) compile to their defaults unless the library is built with -DA3C_KNOBS
 // (tools/build_variant.sh), so a stray variable cannot change a release run's summation order.

@@ -81,6 +81,8 @@ struct a3c_engine {
   float* ep_end;           // q: per env final epsilon
   float* ws;               // backward workspace
   float* fcpart;           // fused overlap rollout: the fc as FC_NS K-slice partials [FC_NS][E][FC]
+  unsigned* fctick;        // C5 with lstm_fcfold: k_fc_part_fold's ticket word per 32 x 64 fc tile (zeroed)
+  int lstm_fcfold;         // C5: the fc launch folds its partials (k_fc_part_fold), not every cell workgroup
   int fc_split;            // 1: the fused rollout's fc runs as k_fc_part + the head's fold
   int nat;                 // the nature trunk (cfg.net.trunk = A3C_TRUNK_NATURE, nature.hip)
   float* nat_fws;          // nature trunk: the rollout forward's fc split-K slabs
@@ -126,6 +128,9 @@ struct a3c_engine {
   bool grad_applied;       // ... and a3c_engine_iterate already applied it (apply is then a no-op)
   bool reset_done;
 };
+
+// k_fc_part_fold's ticket words: one per 32-row x 64-column tile of the E-row fc
+static size_t fctick_bytes(int64_t E) { return (size_t)((E + 31) / 32) * (FC / 64) * sizeof(unsigned); }
 
 static int dalloc(a3c_engine* e, void** p, size_t bytes) {
   bytes = (bytes + 255) & ~(size_t)255;
@@ -238,6 +243,8 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   e->fc_split = 1;
   e->fc_split = A3C_KNOB("A3C_FC_SPLIT", e->fc_split) != 0;
   e->frame84 = cfg->frame84 ? 1 : 0;
+  e->lstm_fcfold = 0;
+  e->lstm_fcfold = A3C_KNOB("A3C_LSTM_FCFOLD", e->lstm_fcfold) != 0;
   // the nature trunk (network.py:30-42) runs its own passes (nature.hip): of the NIPS fusions only
   // the head + act + screen kernel (its 512-wide form), the exchange one-phase
   e->nat = L.trunk == A3C_TRUNK_NATURE ? 1 : 0;
@@ -347,6 +354,11 @@ extern "C" int a3c_engine_create(const a3c_engine_config* cfg, a3c_engine** out)
   ALLOC(e->ep_acc, E * 8);
   // last: the other buffers keep the placement they had before the ReLU bits existed
   for (int k = 0; k < e->nslot; ++k) ALLOC(e->slot[k].l2m, nE * C2_Q * 4);
+  ALLOC(e->fctick, fctick_bytes(E));
+  if (hipError_t st = hipMemset(e->fctick, 0, fctick_bytes(E))) {
+    a3c_engine_destroy(e);
+    return a3c_set_error((int)st, "a3c_engine_create", "hipMemset failed");
+  }
 #undef ALLOC
   if (a3c_make_tab(L.nt, L.off, L.size, L.total, &e->tt) ||
       (e->nat ? a3c_nat_fused_tab(L, &e->tt_f) : a3c_fused_tab(L, &e->tt_f))) {
@@ -662,6 +674,7 @@ static int enqueue_step(a3c_engine* e, const Slot& sl, int t, hipStream_t s) {
     ls.h_src = src.lh + so * LSTM_U; ls.c_src = src.lc + so * LSTM_U; ls.prev_terms = src.terms + so;
     ls.hp = sl.lhp + o * LSTM_U; ls.cp = sl.lcp + o * LSTM_U; ls.gates = sl.lg + o * LSTM_G;
     ls.h = sl.lh + o * LSTM_U; ls.c = sl.lc + o * LSTM_U;
+    if (e->lstm_fcfold) ls.fc_tick = e->fctick;
   }
   // conv fusion: step t > 0's conv1 + conv2 ran inside step t-1's head + screen kernel, and this
   // step's head + screen runs step t+1's (the bootstrap state's after the last step, a3c)
@@ -720,6 +733,7 @@ static int enqueue_rollout_end(a3c_engine* e, const Slot& sl, hipStream_t s) {
       ls.wt = sl.lwt;
       ls.h_src = sl.lh + lastE * LSTM_U; ls.c_src = sl.lc + lastE * LSTM_U; ls.prev_terms = sl.terms + lastE;
       ls.h = sl.lhb; ls.c = sl.lcb;
+      if (e->lstm_fcfold) ls.fc_tick = e->fctick;
     }
     if (e->nat) {
       float* x = sl.nscr;

@@ -18,6 +18,9 @@ struct LstmStep {
   const float* fc_part = nullptr;
   const float* fc_bias = nullptr;
   float* l3_out = nullptr;
+  // with fc_part set by the caller: the fc launch folds its own partials (k_fc_part_fold, one
+  // ticket word per fc tile) and the cell reads the finished rows
+  unsigned* fc_tick = nullptr;
 };
 
 int a3c_lstm_fwd_launch(const float* bias, const float* x, const LstmStep& st, int64_t B, hipStream_t s);

@@ -192,6 +192,11 @@ int a3c_fc_part_launch(const float* A, const float* Wp, float* part, int64_t M, 
                        int64_t* adv_ptr = nullptr, int adv_n = 0);
 // the policy / value head of B states from the fc's K-slice partials (fold + bias + ReLU + head,
 // k_head_fwd): z rows, no action draw
+// the same with the fold in the launch (C5): each tile's last K-slice workgroup folds the FC_NS
+// partials in slice order + fbias + ReLU into fout[M][FC]; tick: one zeroed word per 32 x 64 tile,
+// (ceil(M / 32) * 4), left zeroed by the launch
+int a3c_fc_part_fold_launch(const float* A, const float* Wp, float* part, int64_t M, unsigned* tick,
+                            const float* fbias, float* fout, hipStream_t s);
 int a3c_head_fold_launch(const NetLayout& L, const float* P, const float* fc_part, int64_t B, float* z,
                          hipStream_t s);
 int a3c_fcp_split();

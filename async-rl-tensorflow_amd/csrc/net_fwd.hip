@@ -858,14 +858,18 @@ int a3c_forward_launch(const NetLayout& L, const float* params, const uint8_t* p
   // C5: the LSTM cell folds the partials itself (k_lstm_fwd), on every step of a fused rollout
   const bool part_lstm = fc_part && ls != nullptr;
   const bool part = fc_part && (part_lstm || (next ? sel.mode >= 0 && sel.env_on && sel.ring : sel.mode < 0));
-  int rc = part ? a3c_fc_part_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), fc_part, B, s)
+  // (with ls->fc_tick the fc's last K-slice workgroup per tile folds them instead: k_fc_part_fold)
+  const bool fold_fc = part_lstm && ls->fc_tick;
+  int rc = fold_fc ? a3c_fc_part_fold_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), fc_part, B, ls->fc_tick,
+                                             P + L.off[T_FCB], act_l3, s)
+         : part ? a3c_fc_part_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), fc_part, B, s)
                 : a3c_fc_fwd_launch(act_l2, (const float*)(prep + PREP_W1S_BYTES), P + L.off[T_FCB], act_l3, B, s,
                                     P + L.off[T_FCW]);
   if (rc) return rc;
   const float* head_in = act_l3;
   if (ls) {   // C5: LSTM cell on the fc output, heads on its h
     LstmStep st = *ls;
-    if (part_lstm) {
+    if (part_lstm && !fold_fc) {
       st.fc_part = fc_part;
       st.fc_bias = P + L.off[T_FCB];
       st.l3_out = act_l3;
@@ -1161,11 +1165,19 @@ __device__ inline int fcp_c0(int x) { return (FC_CH * x) / FC_NS; }
 // their sums to range 0's wave through LDS, which adds them in range order and stores.  KS = 2:
 // two waves per SIMD at 75 VGPRs, KS = 4: four at <= 64 VGPRs -- beside a compact conv backward
 // workgroup either way.  Measured (M1 / M2 env-steps/s): KS 1 4.67M / 5.82M, KS 2 4.78M / 6.07M.
-template <int KS>
-__global__ void __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(KS == 4 ? 8 : 1)))
-k_fc_part(const float* __restrict__ A, const float* __restrict__ Wp, float* __restrict__ part, int M,
-          int64_t* adv_ptr, int adv_n) {
-  WGLOG(2);
+//
+// FOLD (C5, the LSTM cell's input): the tile's K-slice workgroups hand their partials to the one
+// whose ticket comes last, which folds the FC_NS slices in slice order (+ bias, ReLU: the cell
+// kernel's fold, bit for bit) and writes the fc output rows -- once per tile instead of once per
+// LSTM unit tile.  Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the
+// sc1 table): every partial is stored sc1 (write-through), every storing wave drains vmcnt before
+// the workgroup barrier, lane 0 draws an agent-scope ticket, and the last arriver reads the
+// partials with sc1 loads only.  tick[tile] is zeroed at engine creation and reset by the last
+// arriver (every launch completes all FC_NS tickets of every tile).
+template <int KS, bool FOLD>
+__device__ __forceinline__ void fc_part_body(const float* __restrict__ A, const float* __restrict__ Wp,
+                                             float* __restrict__ part, int M, int64_t* adv_ptr, int adv_n,
+                                             unsigned* tick, const float* fbias, float* fout) {
   if (adv_ptr && blockIdx.x == 0 && threadIdx.x == 0) *adv_ptr += adv_n;   // (reads no tau)
   __shared__ __attribute__((aligned(16))) float as[FCP_RB * FCP_LD];
   constexpr int NT = 256 * KS;
@@ -1240,21 +1252,81 @@ k_fc_part(const float* __restrict__ A, const float* __restrict__ Wp, float* __re
       xs[(((kr - 1) * 4 + (wid & 3)) * 2 + 1) * 64 + lane] = acc1;
     }
     __syncthreads();
-    if (kr) return;
+    if constexpr (!FOLD) {
+      if (kr) return;
+    }
+    if (!kr) {
 #pragma unroll
-    for (int q = 0; q < KS - 1; ++q) {
-      acc0 += xs[((q * 4 + (wid & 3)) * 2 + 0) * 64 + lane];
-      acc1 += xs[((q * 4 + (wid & 3)) * 2 + 1) * 64 + lane];
+      for (int q = 0; q < KS - 1; ++q) {
+        acc0 += xs[((q * 4 + (wid & 3)) * 2 + 0) * 64 + lane];
+        acc1 += xs[((q * 4 + (wid & 3)) * 2 + 1) * 64 + lane];
+      }
     }
   }
   // partial tile rows m0 + 16 rt + 4 j4 + r, column 16 ct + i16
   float* out = part + ((int64_t)x * M) * FC + 16 * ct + i16;
+  if constexpr (!FOLD) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row0 = m0 + 4 * j4 + r, row1 = row0 + 16;
-    if (row0 < M) out[(int64_t)row0 * FC] = acc0[r];
-    if (row1 < M) out[(int64_t)row1 * FC] = acc1[r];
+    for (int r = 0; r < 4; ++r) {
+      const int row0 = m0 + 4 * j4 + r, row1 = row0 + 16;
+      if (row0 < M) out[(int64_t)row0 * FC] = acc0[r];
+      if (row1 < M) out[(int64_t)row1 * FC] = acc1[r];
+    }
+  } else {
+    if (kr == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row0 = m0 + 4 * j4 + r, row1 = row0 + 16;
+        if (row0 < M) __hip_atomic_store(out + (int64_t)row0 * FC, acc0[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (row1 < M) __hip_atomic_store(out + (int64_t)row1 * FC, acc1[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every storing wave drains its sc1 stores
+    __syncthreads();
+    unsigned* flag = (unsigned*)as + (FCP_RB * FCP_LD - 1);   // a pad word of the A tile's last row
+    if (threadIdx.x == 0) {
+      const unsigned t = __hip_atomic_fetch_add(tick + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == FC_NS - 1) __hip_atomic_store(tick + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = t;
+    }
+    __syncthreads();
+    if (*flag != FC_NS - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // (no instruction: keeps the loads below)
+    // fold of the tile: 32 rows x 64 columns as 512 groups of 4, slices in order, + bias, ReLU
+    for (int i = threadIdx.x; i < FCP_RB * FCP_CB / 4; i += 256 * KS) {
+      const int row = m0 + i / (FCP_CB / 4), col = cb * FCP_CB + 4 * (i % (FCP_CB / 4));
+      if (row >= M) continue;
+      const float* pp = part + (int64_t)row * FC + col;
+      f32x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = __hip_atomic_load(pp + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int xs2 = 1; xs2 < FC_NS; ++xs2) {
+        const float* q = pp + (int64_t)xs2 * M * FC;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += __hip_atomic_load(q + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const f32x4 fb = *(const f32x4*)(fbias + col);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + fb[r], 0.f);
+      *(f32x4*)(fout + (int64_t)row * FC + col) = v;
+    }
   }
+}
+
+template <int KS>
+__global__ void __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(KS == 4 ? 8 : 1)))
+k_fc_part(const float* __restrict__ A, const float* __restrict__ Wp, float* __restrict__ part, int M,
+          int64_t* adv_ptr, int adv_n) {
+  WGLOG(2);
+  fc_part_body<KS, false>(A, Wp, part, M, adv_ptr, adv_n, nullptr, nullptr, nullptr);
+}
+
+template <int KS>
+__global__ void __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(KS == 4 ? 8 : 1)))
+k_fc_part_fold(const float* __restrict__ A, const float* __restrict__ Wp, float* part, int M,
+               unsigned* tick, const float* __restrict__ fbias, float* __restrict__ fout) {
+  fc_part_body<KS, true>(A, Wp, part, M, nullptr, 0, tick, fbias, fout);
 }
 
 // K splits of the partial fc, set by the engine per frame mode (a3c_set_fcp_split; A3C_FCP_KS
@@ -1262,6 +1334,22 @@ k_fc_part(const float* __restrict__ A, const float* __restrict__ Wp, float* __re
 static thread_local int t_fcp_split = 2;
 int a3c_fcp_split() { return t_fcp_split; }
 void a3c_set_fcp_split(int ks) { t_fcp_split = ks; }
+
+int a3c_fc_part_fold_launch(const float* A, const float* Wp, float* part, int64_t M, unsigned* tick,
+                            const float* fbias, float* fout, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (!tick || !fbias || !fout || (((uintptr_t)fbias | (uintptr_t)fout) & 15))
+    return a3c_set_error(A3C_ERR_INVALID, "a3c_fc_part_fold", "bad argument");
+  const int nrb = (int)((M + FCP_RB - 1) / FCP_RB);
+  static const int env_ks = (int)A3C_AB_KNOB("A3C_FCP_KS", 0);
+  const int ks = env_ks ? env_ks : a3c_fcp_split();
+  const dim3 grid((unsigned)(FC_NS * nrb * (FC / FCP_CB)));
+  if (ks == 4) hipLaunchKernelGGL(k_fc_part_fold<4>, grid, dim3(1024), 0, s, A, Wp, part, (int)M, tick, fbias, fout);
+  else if (ks == 2) hipLaunchKernelGGL(k_fc_part_fold<2>, grid, dim3(512), 0, s, A, Wp, part, (int)M, tick, fbias, fout);
+  else hipLaunchKernelGGL(k_fc_part_fold<1>, grid, dim3(256), 0, s, A, Wp, part, (int)M, tick, fbias, fout);
+  A3C_CHECK(hipGetLastError());
+  return 0;
+}
 
 int a3c_fc_part_launch(const float* A, const float* Wp, float* part, int64_t M, hipStream_t s, int64_t* adv_ptr,
                        int adv_n) {

@@ -194,6 +194,30 @@ def test_engine_lstm_bench_shape_runs():
     assert torch.equal(a.params, b.params)
 
 
+@pytest.mark.parametrize('E', [40, 256])
+def test_engine_lstm_fc_fold_forms_identical(E, monkeypatch):
+    """C5's fc fold in either place -- by every cell workgroup (k_lstm_fwd) or once per fc tile by
+    the tile's last K-slice workgroup (k_fc_part_fold, an in-launch hand-off through sc1 stores and
+    an agent-scope ticket) -- sums the same partials in the same order: bit-identical rollouts and
+    updates, overlapped with the backward (uneven load), E = 40 a ragged last tile of both kernels."""
+    runs = {}
+    for fold in ('0', '1'):
+        monkeypatch.setenv('A3C_LSTM_FCFOLD', fold)
+        runs[fold], _, _ = build(6, E, 5, 3, seed=77, frames=256, scale=2.0, learning_rate=2e-3, overlap=True,
+                                 use_graph=True)
+    a, b = runs['0'], runs['1']
+    for k in range(6):
+        a.iterate()
+        b.iterate()
+        torch.cuda.synchronize()
+        sa, sb = a.slot(k & 1), b.slot(k & 1)
+        for key in ('actions', 'z', 'lstm_h', 'lstm_c', 'lstm_gates', 'act_l3'):
+            if key in sa:
+                assert torch.equal(sa[key], sb[key]), (k, key)
+        assert torch.equal(a.loss, b.loss), k
+        assert torch.equal(a.params, b.params), k
+
+
 def test_lstm_rejected_where_unsupported():
     from src import _lib
     from src.kernels import Net  # noqa: F401
