@@ -1396,12 +1396,17 @@ static NatPlan nat_plan(const NetLayout& L, int64_t B) {
   int64_t o = 0;
   auto take = [&](int64_t floats) { int64_t r = o; o += (floats + 63) & ~(int64_t)63; return r; };
   p.head_split = a3c_gemm_effective_split((int)B, a3c_gemm_plan_split(NT_FC, L.zs, (int)B, 128));
-  // workgroups per dW pass: 1536 (r6dwg: conv3 / conv2 / conv1 dW 62 / 89 / 97 -> 51 / 74 / 81 us
-  // alone against 512, the bench 1.651M -> 1.661M; 256 / 128 lose 16 / 42 %)
-  static const int wgs = (int)A3C_AB_KNOB("A3C_NAT_DW_WGS", 1536);
-  dw_split(B * NT1_P, 2, wgs, p.ns1, p.kc1);      // M = 256 in 128-row tiles
-  dw_split(B * NT2_P, 8, wgs, p.ns2, p.kc2);      // M = 512 in 64-row tiles
-  dw_split(B * NT3_P, 9, wgs, p.ns3, p.kc3);      // M = 576
+  // workgroups per dW pass (the reduction's slab count): conv1 / conv2 / conv3 768 / 2048 / 768,
+  // by whole-bench sweeps (r6dwg2-5, B = 1280): 1.717M against 1.653M for 1536 on all three (the
+  // choice by times alone, r6dwg: 62 / 89 / 97 -> 51 / 74 / 81 us against 512); conv1's count is
+  // the sensitive one (832: 1.65M, 1536: 1.65M, 640: 1.68M)
+  static const int wgs = (int)A3C_AB_KNOB("A3C_NAT_DW_WGS", 0);   // > 0: one count for all three
+  static const int wgs1 = (int)A3C_AB_KNOB("A3C_NAT_DW_WGS1", wgs > 0 ? wgs : 768);
+  static const int wgs2 = (int)A3C_AB_KNOB("A3C_NAT_DW_WGS2", wgs > 0 ? wgs : 2048);
+  static const int wgs3 = (int)A3C_AB_KNOB("A3C_NAT_DW_WGS3", wgs > 0 ? wgs : 768);
+  dw_split(B * NT1_P, 2, wgs1, p.ns1, p.kc1);     // M = 256 in 128-row tiles
+  dw_split(B * NT2_P, 8, wgs2, p.ns2, p.kc2);     // M = 512 in 64-row tiles
+  dw_split(B * NT3_P, 9, wgs3, p.ns3, p.kc3);     // M = 576
   p.dz = take(B * L.zs);
   p.dl4 = take(B * NT_FC);
   p.dl3 = take(B * NT_FLAT);
