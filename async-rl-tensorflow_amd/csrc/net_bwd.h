@@ -20,7 +20,9 @@ struct FinalizeSeg {
   float scale;
   int slot;               // >= 0: block x of the segment writes its fp64 sum of squares to part[slot + x]
 };
+#ifndef FIN_X
 #define FIN_X 32          // k_finalize blocks per segment
+#endif
 struct FinalizeSegs {
   FinalizeSeg s[12];
   int n;

@@ -3,7 +3,9 @@
 #include "../../include/a3c_hip.h"
 
 #define SS_CHUNK 4096          // elements per sum-of-squares partial block
+#ifndef SS_MAX_BLOCKS
 #define SS_MAX_BLOCKS 1024     // partial slots (>= sum over tensors of ceil(size / SS_CHUNK))
+#endif
 enum { OPT_CLIP = 1, OPT_APPLY = 2 };
 
 struct TensorTab {
