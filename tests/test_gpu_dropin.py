@@ -320,6 +320,15 @@ def test_agent_batch_update_matches_oracle():
     agent.batch_action, agent.batch_reward, agent.batch_terminal = list(actions), list(rewards), list(terms)
     agent.step, agent.total_loss, agent.total_q, agent.update_count = 1000, 0., 0., 0
     lr = agent.lr
+    seen = {}
+    lb = agent.net.loss_backward
+
+    def capture(params, s_t, fwd, *a, **kw):          # the kernels' own activations and gradients
+        grads, loss = lb(params, s_t, fwd, *a, **kw)
+        seen.update(fwd={k: v.detach().cpu().numpy().astype(np.float64) for k, v in fwd.items() if v is not None},
+                    grads=grads.detach().cpu().numpy().copy())
+        return grads, loss
+    agent.net.loss_backward = capture
     agent.batch_update(is_chief=True)
     # oracle
     q_next = R.forward(tp, R.states_nhwc(planes[1:]), 'q')['z']
@@ -333,7 +342,26 @@ def test_agent_batch_update_matches_oracle():
         ms, mom = np.ones_like(ref), np.zeros_like(ref)
         R.rmsprop_apply(ref, ms, mom, R.clip_by_norm(g[name].astype(np.float32), 40.0), lr, 0.99, 0.0, 0.1)
         step = w.detach().cpu().numpy() - p[name]
-        assert rel_l2(step, ref - p[name]) < 2e-2, name
+        assert rel_l2(step, ref - p[name]) < 2e-2, name   # independent fp64 forward (ReLU flips)
+    # and at 1e-4 against the oracle backward on the kernels' own activations (the same ReLU masks),
+    # then the applied step against TF ApplyRMSProp of the kernels' own clipped gradients at 1e-5
+    fa = seen['fwd']
+    x0 = R.states_nhwc(planes[:-1]).astype(np.float64) / 255.0
+    zs = fa['z'][:, :fwd['z'].shape[1]]
+    same = dict(z=zs, h3=fa['l3'], flat=fa['l2'], acts=[x0, fa['l1'].reshape(B, 20, 20, 16),
+                                                       fa['l2'].reshape(B, 9, 9, 32)])
+    _, dz_same = R.q_loss_and_dz(zs, actions, target)
+    g_same = R.backward(p, same, dz_same, 'q')
+    g_k = seen['grads']
+    for (name, shp), o, n in zip(agent.names_shapes, agent.offsets, agent.sizes):
+        e = rel_l2(g_k[o:o + n].reshape(shp), g_same[name])
+        assert e < 1e-4, (name, e)
+        ref = p[name].copy()
+        ms, mom = np.ones_like(ref), np.zeros_like(ref)
+        R.rmsprop_apply(ref, ms, mom, R.clip_by_norm(g_k[o:o + n].reshape(shp).astype(np.float32), 40.0),
+                        lr, 0.99, 0.0, 0.1)
+        step = agent.w[name].detach().cpu().numpy() - p[name]
+        assert rel_l2(step, ref - p[name]) < 1e-5, name
 
 
 def test_agent_train_loop_and_target_update(tmp_path):
